@@ -1,0 +1,204 @@
+"""Benchmark: batched madigan market-simulation step on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--fuse F] [--n-envs 8192]
+
+Workload (BASELINE.json configs[2], SURVEY 8d "C3"): 8192 envs x 8 assets per
+GPU, TrendOU generators (config.yaml:116-138), Broker with 1e-4 relative
+slippage and 2% transaction cost, DDR reward (eta=.001, n=1), discrete actions
+U{0,1,2} (Philox, pre-generated on device) turned into units by DQN's
+action_to_transaction (unit_size .05 of available margin), in-kernel
+auto-reset.  A "step" advances every env by one tick and materialises every
+per-step output of the reference's Env.step (State row, reward, done,
+BrokerResponse) plus the shaped reward; `--fuse` steps run per launch with the
+state held in registers.
+
+For N>1 (torchrun, one process per GPU) envs are sharded by global index
+(env_offset) with no per-step collective; one RCCL all-gather of the
+per-env episode statistics closes the timed region.  Prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/sec (batched) at 8192 envs × 8 assets; % HBM roofline"
+TRENDOU_P = [0.001, 100, 500, 0.001, 0.005, 5.0, 0.15, 0.04, 0.001, 0.99]  # config.yaml:116-138
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def c3_kwargs():
+    return dict(required_margin=1.0, maintenance_margin=0.25, slippage_rel=1e-4,
+                transaction_cost_rel=0.02, reward_shaper="DDR", adaptation_rate=0.001,
+                unit_size=0.05, auto_reset=True, init_cash=1_000_000.0)
+
+
+def bytes_per_env_step(A: int, fuse: int, D: int = 1) -> float:
+    """Algorithmic HBM bytes of the fused step kernel per env-step.
+
+    per step: actions A*1 B read; outputs reward 8, agent_reward 8*D, shaped 8*D,
+    done 1, obs_price 8A, obs_port 8(A+1), timestamp 8, tprice/tunits/tcost 24A,
+    risk A, marginCall 1.  Per launch (amortised over `fuse` steps): state read +
+    write of L, meanEntry, borrowed, price, sine_x, ouMean, dY (7*8A), trend len
+    4A + flags A, cash 8, timestamp 8, shaper A/B 16*D, running stats 16, plus
+    the episode-stat counter read 8 and the stats row write 32."""
+    per_step = A + 8 + 16 * D + 1 + 8 * A + 8 * (A + 1) + 8 + 24 * A + A + 1
+    state = 2 * (7 * 8 * A + 4 * A + A + 8 + 8 + 16 * D + 16) + 8 + 32
+    return per_step + state / fuse
+
+
+def load_pmc_traffic(workload: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(workload)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(n_envs: int, A: int, budget_s: float = 12.0):
+    """The oracle's C restatement (fast-math build, reference flags) on one host
+    core, one Env object per env, same C3 workload, bounded sample."""
+    from oracle import oracle as O
+    cfg = dict(n_envs=n_envs, seed=0x6D6164 + 3, transaction_cost_rel=0.02, **{
+        k: v for k, v in c3_kwargs().items() if k not in ("transaction_cost_rel", "auto_reset")})
+    cfg["auto_reset"] = 1
+    srcs = [(O.SRC_TRENDOU, TRENDOU_P)] * A
+    b = O.OracleBatch(cfg, srcs, fast=True)
+    rng = np.random.default_rng(0)
+    chunk = 4
+    acts = rng.integers(0, 3, (chunk, n_envs, A)).astype(np.int8)
+    b.rollout(acts[:1])  # warm
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        b.rollout(acts)
+        steps += chunk
+    dt = time.perf_counter() - t0
+    return dict(value=n_envs * steps / dt, unit="env-steps/s", cores=1, kind="port",
+                sample=f"C3 workload, {n_envs} envs x {A} assets x {steps} steps on one host core "
+                       f"({dt:.1f} s), oracle/madigan_oracle.c built -O3 -march=x86-64-v3 -ffast-math")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2048)
+    ap.add_argument("--warmup", type=int, default=256)
+    ap.add_argument("--fuse", type=int, default=64)
+    ap.add_argument("--n-envs", type=int, default=8192, help="envs per GPU")
+    ap.add_argument("--assets", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from madigan_amd import BatchedEnv
+    from madigan_amd.config import trendou_spec
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    dev = torch.device(f"cuda:{local_rank}")
+    torch.cuda.set_device(dev)
+
+    N, A, F = args.n_envs, args.assets, args.fuse
+    spec = trendou_spec(*[[p] * A for p in TRENDOU_P])
+    env = BatchedEnv(spec, N, device=dev, seed=0x6D6164 + 3, env_offset=rank * N, **c3_kwargs())
+    total = args.warmup + args.steps
+    actions = env.generate_actions(total, seed=0x6D6164)
+    traj = env.alloc_traj(F)
+    stream = torch.cuda.current_stream(dev)
+
+    def run(k0: int, k1: int, ev=None):
+        k = k0
+        while k < k1:
+            n = min(F, k1 - k)
+            out = traj if n == F else {kk: v[:n] for kk, v in traj.items()}
+            if ev is not None:
+                ev[0].append(torch.cuda.Event(enable_timing=True))
+                ev[0][-1].record(stream)
+            env.rollout(actions[k:k + n], out=out)
+            if ev is not None:
+                ev[1].append(torch.cuda.Event(enable_timing=True))
+                ev[1][-1].record(stream)
+                ev[2].append(n)
+            k += n
+
+    run(0, args.warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = ([], [], [])
+    t0 = time.perf_counter()
+    run(args.warmup, total, ev)
+    stats = env.episode_stats
+    if world > 1:
+        gathered = torch.empty((world * N, 4), dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(gathered, stats)
+    else:
+        gathered = stats
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    full = [i for i, n in enumerate(ev[2]) if n == F]
+    launch_ms = [ev[0][i].elapsed_time(ev[1][i]) for i in full] or [
+        ev[0][i].elapsed_time(ev[1][i]) for i in range(len(ev[2]))]
+    avg_launch_s = float(np.mean(launch_ms)) / 1e3
+    steps_per_launch = F if full else ev[2][0]
+    bpes = bytes_per_env_step(A, steps_per_launch, env.D)
+    achieved_gbs = N * steps_per_launch * bpes / avg_launch_s / 1e9
+    value = world * N * args.steps / elapsed
+    episodes = int(gathered[:, 3].sum().item())
+
+    if rank == 0:
+        workload = f"C3_trendou_{N}x{A}_fuse{steps_per_launch}"
+        traffic = load_pmc_traffic(workload)
+        res = {
+            "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": "C3: TrendOU x8 assets per env, slippage 1e-4 + 2% cost broker, "
+                                   "DDR eta=.001 n=1, discrete actions via action_to_transaction, "
+                                   "auto-reset",
+                       "n_envs_per_gpu": N, "n_assets": A, "window": 0,
+                       "steps_per_launch": steps_per_launch,
+                       "parallelism": f"env-sharded x{world} (no per-step collective)"},
+            "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": achieved_gbs / PEAK_HBM_GBS,
+                         "traffic": traffic, "kernel": f"mgn::k_step<1,{A}>",
+                         "bytes_per_env_step": bpes, "avg_launch_us": avg_launch_s * 1e6},
+            "episodes_completed": episodes,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(N, A, args.cpu_budget)
+        print(json.dumps(res))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,208 @@
+/*
+ * madigan_amd.h -- C ABI of the MI355X-native batched market-simulation step.
+ *
+ * One handle = N independent madigan Envs on one GPU, advanced together by
+ * hand-written HIP kernels (libmadigan_hip.so).  Plain pointers and sizes only:
+ * every pointer marked _dev is device memory; nothing here depends on torch.
+ *
+ * Which reference interface each entry point replaces (paths relative to the
+ * reference checkout, madigan/environments/cpp/ unless stated):
+ *   mgn_create        Env(type, initCash, config) + setRequiredMargin/
+ *                     setMaintenanceMargin/setSlippage/setTransactionCost
+ *                     (env.cpp:843-869, Env.h:21-29, :94-111;
+ *                      madigan/environments/__init__.py:9-22 make_env)
+ *   mgn_reset         Env::reset (Env.h:181-187) [+ preprocessor reset_state /
+ *                     initialize_history, madigan/utils/preprocessor.py:191-199]
+ *   mgn_step          Env::step() / step(units) / step(assetIdx, units)
+ *                     (Env.h:189-256, env.cpp:991-1005) plus the n=1 reward
+ *                     shaper (madigan/utils/buffers/nstep_buffer.py:30-204)
+ *   mgn_rollout       K x { DQN.action_to_transaction (modelling/algorithm/
+ *                     dqn.py:160-179); Env::step(units) } fused in one launch
+ *   mgn_set_prices    DataSourceTick plug-in fed from the host
+ *                     (DataSource.h:48-64, PyDataSource.h:9-24, Env.h:174-179)
+ *   mgn_window*       StackerDiscrete.stream_state / current_data
+ *                     (madigan/utils/preprocessor.py:143-199)
+ *   mgn_get_views     zero-copy property views (env.cpp:897-913)
+ *   mgn_last_error    pybind11 exception translation (DataTypes.h:36-46)
+ *
+ * Threading: a handle is not thread-safe; all work is ordered on the handle's
+ * stream and no call synchronises the host unless documented.
+ */
+#ifndef MADIGAN_AMD_H_
+#define MADIGAN_AMD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MGN_ABI_VERSION 1
+#define MGN_MAX_ASSETS 64
+
+/* status codes; the Python layer maps them to the reference's exceptions */
+enum {
+  MGN_OK = 0,
+  MGN_ERR_CONFIG = 1,   /* ConfigError / NotImplemented -> RuntimeError */
+  MGN_ERR_INDEX = 2,    /* std::out_of_range            -> IndexError   */
+  MGN_ERR_LENGTH = 3,   /* std::length_error            -> ValueError   */
+  MGN_ERR_DEVICE = 4,   /* HIP runtime failure                          */
+  MGN_ERR_ARG = 5       /* bad pointer / handle                         */
+};
+
+/* RiskInfo (DataTypes.h:70-75) */
+enum { MGN_GREEN = 0, MGN_INSUFF_MARGIN = 1, MGN_MARGIN_CALL = 2, MGN_BLOWN_OUT = 3 };
+
+/* per-asset generator kind (DataSource.cpp:56-108 factory names) */
+enum { MGN_SRC_EXTERNAL = 0, MGN_SRC_SINE = 1, MGN_SRC_OU = 2, MGN_SRC_TRENDOU = 3 };
+
+enum { MGN_SHAPER_NONE = 0, MGN_SHAPER_DSR = 1, MGN_SHAPER_DDR = 2, MGN_SHAPER_PPC = 3 };
+enum { MGN_REWARD_ENV_LOG = 0, MGN_REWARD_AGENT_SUM = 1, MGN_REWARD_AGENT_PER_ASSET = 2 };
+enum { MGN_NORM_NONE = 0, MGN_NORM_LOG = 1, MGN_NORM_LOOKBACK = 2,
+       MGN_NORM_STANDARD_NORMAL = 3, MGN_NORM_LOOKBACK_LOG = 4 };
+/* step kinds: Env::step() / step(units) / step(assetIdx, units) */
+enum { MGN_STEP_NONE = 0, MGN_STEP_UNITS = 1, MGN_STEP_SINGLE = 2 };
+
+/* Per-asset generator parameters (Composite = concatenation in config order).
+ *  SINE    p = {freq, mu, amp, phase, dX, noise}            DataSource.cpp:455-473
+ *  OU      p = {mean, theta, phi}                           DataSource.cpp:1118-1137
+ *  TRENDOU p = {trendProb, minPeriod, maxPeriod, dYMin, dYMax, start,
+ *               theta, phi, noiseTrend, emaAlpha}           DataSource.cpp:1364-1408 */
+typedef struct {
+  int32_t kind;
+  int32_t pad_;
+  double p[12];
+} mgn_asset_source;
+
+typedef struct {
+  int32_t n_envs;
+  int32_t n_assets;
+  int64_t env_offset;          /* global index of env 0 when sharded over GPUs */
+  uint64_t seed;               /* Philox key */
+  double init_cash;
+  double required_margin;
+  double maintenance_margin;
+  double slippage_rel, slippage_abs;
+  double tc_rel, tc_abs;
+  int32_t shaper;              /* MGN_SHAPER_* (n-step = 1) */
+  int32_t reward_mode;         /* MGN_REWARD_* : raw reward fed to the shaper */
+  double adaptation_rate;      /* DSR/DDR eta */
+  double cosine_temp;          /* PPC alpha */
+  double desired_portfolio[MGN_MAX_ASSETS + 1];
+  int32_t window;              /* StackerDiscrete window_length, 0 = none */
+  int32_t norm_type;           /* MGN_NORM_* applied by mgn_window */
+  int32_t auto_reset;          /* reset done envs inside the step kernel */
+  int32_t action_atoms;        /* discrete actions for mgn_rollout */
+  double unit_size;            /* unit_size_proportion_avM */
+} mgn_config;
+
+/* Per-step outputs.  For mgn_step they are the handle's buffers (see views);
+ * for mgn_rollout the caller passes (K, ...) device arrays, any may be NULL. */
+typedef struct {
+  double *reward;        /* (N)            env log reward                 */
+  double *agent_reward;  /* (N) or (N,A)   offpolicy_q.py:152-164         */
+  double *shaped;        /* (N) or (N,A)   shaper output                  */
+  uint8_t *done;         /* (N)                                           */
+  double *obs_price;     /* (N,A)          State.price                    */
+  double *obs_port;      /* (N,A+1)        State.portfolio                */
+  uint64_t *timestamp;   /* (N)            State.timestamp                */
+  double *tprice;        /* (N,A)          BrokerResponse.transactionPrice */
+  double *tunits;        /* (N,A)                                         */
+  double *tcost;         /* (N,A)                                         */
+  uint8_t *risk;         /* (N,A)          RiskInfo                       */
+  uint8_t *margin_call;  /* (N)                                           */
+} mgn_traj;
+
+/* Device pointers into the handle's arena (row-major, env-major). */
+typedef struct {
+  double *ledger, *mean_entry, *borrowed, *prices;   /* (N,A) */
+  double *sine_x, *ou_mean, *trend_dy;               /* (N,A) generator state */
+  int32_t *trend_len;                                /* (N,A) */
+  uint8_t *trend_flags;                              /* (N,A) bit0 trending, bit1 dir<0 */
+  double *cash;                                      /* (N) */
+  uint64_t *timestamp;                               /* (N) */
+  double *shaper_a, *shaper_b;                       /* (N,D) */
+  double *ep_stats;                                  /* (N,2) running {return, length} */
+  double *episode_stats;                             /* (N,4) {last return, last length,
+                                                               last final equity, done count} */
+  double *ext_prices;                                /* (N,A) external source input */
+  double *units;                                     /* (N,A) staging for mgn_step input */
+  int32_t *asset_idx;                                /* (N)   staging for STEP_SINGLE */
+  double *ring;                                      /* (N,W,2A+1) window ring */
+  uint64_t *ring_ts;                                 /* (N,W) */
+  int32_t *ring_head, *ring_len;                     /* (N) */
+  double *win_price, *win_port;                      /* (N,W,A), (N,W,A+1) gathered window */
+  uint64_t *win_ts;                                  /* (N,W) */
+  uint8_t *reset_mask;                               /* (N) staging for mgn_reset */
+  mgn_traj out;                                      /* mgn_step outputs */
+  int32_t n_envs, n_assets, window, reward_dim;
+} mgn_views;
+
+/* Stand-alone StackerDiscrete ring (preprocessor.py:143-199), caller-owned
+ * device memory: ring (N, W, n_price + n_port), ring_ts (N, W), head/len (N). */
+typedef struct {
+  int32_t n_envs, n_price, n_port, window, norm_type, pad_;
+  double *ring;
+  uint64_t *ring_ts;
+  int32_t *head, *len;
+} mgn_ring;
+
+typedef struct mgn_env mgn_env;
+
+int mgn_abi_version(void);
+/* bytes of device memory a handle needs (caller-provided arena) */
+size_t mgn_arena_bytes(const mgn_config *cfg);
+/* arena: device memory of mgn_arena_bytes() bytes, or NULL to allocate;
+ * stream: hipStream_t or NULL for the null stream.  Runs the Env constructor
+ * (source init + initAccountants' first getData, Env.h:139-165). */
+int mgn_create(const mgn_config *cfg, const mgn_asset_source *sources, void *stream, void *arena,
+               size_t arena_bytes, mgn_env **out);
+int mgn_destroy(mgn_env *env);
+int mgn_set_stream(mgn_env *env, void *stream);
+int mgn_get_views(const mgn_env *env, mgn_views *views);
+/* Env::reset for envs with mask_dev[e] != 0 (NULL: all envs). */
+int mgn_reset(mgn_env *env, const uint8_t *mask_dev);
+/* one Env::step for every env; kind MGN_STEP_*; units_dev (N,A) for UNITS,
+ * (N) for SINGLE with asset_idx_dev (N).  Outputs land in views.out. */
+int mgn_step(mgn_env *env, int32_t kind, const double *units_dev, const int32_t *asset_idx_dev);
+/* k_steps fused steps; actions_dev (K,N,A) int8 discrete atoms */
+int mgn_rollout(mgn_env *env, const int8_t *actions_dev, int32_t k_steps, const mgn_traj *out);
+/* k_steps fused Env::step(units); units_dev (K,N,A) fp64 */
+int mgn_rollout_units(mgn_env *env, const double *units_dev, int32_t k_steps, const mgn_traj *out);
+/* prices (N,A) consumed by the next getData of MGN_SRC_EXTERNAL assets */
+int mgn_set_prices(mgn_env *env, const double *prices_dev);
+/* StackerDiscrete.stream_state with explicit rows (any may be NULL = current State) */
+int mgn_window_push(mgn_env *env, const double *price_dev, const double *port_dev,
+                    const uint64_t *ts_dev);
+/* StackerDiscrete.reset_state for masked envs (NULL: all) */
+int mgn_window_clear(mgn_env *env, const uint8_t *mask_dev);
+/* StackerDiscrete.current_data into caller buffers (NULL: views.win_*) */
+int mgn_window(mgn_env *env, double *price_dev, double *port_dev, uint64_t *ts_dev);
+/* uniform discrete actions U{0..atoms-1} (K,N,A) from Philox (benchmark input) */
+int mgn_generate_actions(mgn_env *env, int8_t *actions_dev, int32_t k_steps, uint64_t seed);
+/* Portfolio accessors for every env into out_dev (N,10): {cash, equity, pnl,
+ * balance, availableMargin, usedMargin, borrowedMargin, borrowedAssetValue,
+ * assetValue, checkRisk} (Portfolio.cpp:170-252, env.cpp:930-960) */
+int mgn_valuation(mgn_env *env, double *out_dev);
+/* Env::setRequiredMargin / setMaintenanceMargin / setSlippage /
+ * setTransactionCost (Env.h:94-111): take effect at the next launch */
+int mgn_set_broker(mgn_env *env, double required_margin, double maintenance_margin,
+                   double slippage_rel, double slippage_abs, double tc_rel, double tc_abs);
+/* stream_state: rows price (N,n_price), port (N,n_port), ts (N) */
+int mgn_ring_push(const mgn_ring *ring, const double *price_dev, const double *port_dev,
+                  const uint64_t *ts_dev, void *stream);
+/* reset_state for masked envs (NULL: all) */
+int mgn_ring_clear(const mgn_ring *ring, const uint8_t *mask_dev, void *stream);
+/* current_data: price (N,W,n_price) normalised, port (N,W,n_port), ts (N,W) */
+int mgn_ring_gather(const mgn_ring *ring, double *price_dev, double *port_dev, uint64_t *ts_dev,
+                    void *stream);
+/* synchronise the handle's stream */
+int mgn_synchronize(mgn_env *env);
+const char *mgn_last_error(const mgn_env *env);
+const char *mgn_global_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,23 @@
+"""madigan_amd -- MI355X-native batched market-simulation step of madigan.
+
+The hot path (Portfolio/Broker accounting, Sine/OU/TrendOU/Composite
+generators, DSR/DDR/PPC rewards, sliding-window observation) runs as
+hand-written HIP kernels for gfx950 behind a C ABI (include/madigan_amd.h,
+libmadigan_hip.so); this package is the host side mirroring the reference's
+Python surface (madigan/environments, madigan/utils/preprocessor.py).
+"""
+from . import _lib
+from .config import ConfigError, SourceSpec, spec_from_config
+from .env import (Asset, BatchedEnv, BrokerResponse, DataSourceTick, Env, EnvInfo, RiskInfo, State,
+                  get_env_info, make_batched_env, make_env)
+from .preprocessor import PreProcessor, StackerDiscrete, make_preprocessor
+
+__all__ = ["Asset", "BatchedEnv", "BrokerResponse", "ConfigError", "DataSourceTick", "Env",
+           "EnvInfo", "PreProcessor", "RiskInfo", "SourceSpec", "StackerDiscrete", "State",
+           "get_env_info", "make_batched_env", "make_env", "make_preprocessor",
+           "spec_from_config"]
+
+
+def load_extension():
+    """Load libmadigan_hip.so (raises if it was not built)."""
+    return _lib.load()

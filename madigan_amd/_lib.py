@@ -1,0 +1,142 @@
+"""ctypes binding of libmadigan_hip.so (the C ABI in include/madigan_amd.h).
+
+The shared library is built in-tree by ``madigan_amd.build`` (hipcc,
+--offload-arch=gfx950).  There is no fallback: if the library or a GPU is
+missing, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmadigan_hip.so")
+MAX_ASSETS = 64
+ABI_VERSION = 1
+
+# status codes -> the reference's exception types (DataTypes.h:36-46, pybind11)
+OK, ERR_CONFIG, ERR_INDEX, ERR_LENGTH, ERR_DEVICE, ERR_ARG = range(6)
+
+GREEN, INSUFF_MARGIN, MARGIN_CALL, BLOWN_OUT = range(4)
+SRC_EXTERNAL, SRC_SINE, SRC_OU, SRC_TRENDOU = range(4)
+SHAPER_NONE, SHAPER_DSR, SHAPER_DDR, SHAPER_PPC = range(4)
+REWARD_ENV_LOG, REWARD_AGENT_SUM, REWARD_AGENT_PER_ASSET = range(3)
+NORM_NONE, NORM_LOG, NORM_LOOKBACK, NORM_STANDARD_NORMAL, NORM_LOOKBACK_LOG = range(5)
+STEP_NONE, STEP_UNITS, STEP_SINGLE = range(3)
+
+
+class MadiganError(RuntimeError):
+    """HIP runtime failure inside the extension."""
+
+
+class AssetSource(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("pad_", C.c_int32), ("p", C.c_double * 12)]
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("n_envs", C.c_int32), ("n_assets", C.c_int32), ("env_offset", C.c_int64),
+        ("seed", C.c_uint64), ("init_cash", C.c_double), ("required_margin", C.c_double),
+        ("maintenance_margin", C.c_double), ("slippage_rel", C.c_double),
+        ("slippage_abs", C.c_double), ("tc_rel", C.c_double), ("tc_abs", C.c_double),
+        ("shaper", C.c_int32), ("reward_mode", C.c_int32), ("adaptation_rate", C.c_double),
+        ("cosine_temp", C.c_double), ("desired_portfolio", C.c_double * (MAX_ASSETS + 1)),
+        ("window", C.c_int32), ("norm_type", C.c_int32), ("auto_reset", C.c_int32),
+        ("action_atoms", C.c_int32), ("unit_size", C.c_double),
+    ]
+
+
+TRAJ_FIELDS = ("reward", "agent_reward", "shaped", "done", "obs_price", "obs_port", "timestamp",
+               "tprice", "tunits", "tcost", "risk", "margin_call")
+
+
+class Traj(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in TRAJ_FIELDS]
+
+
+VIEW_PTR_FIELDS = ("ledger", "mean_entry", "borrowed", "prices", "sine_x", "ou_mean", "trend_dy",
+                   "trend_len", "trend_flags", "cash", "timestamp", "shaper_a", "shaper_b",
+                   "ep_stats", "episode_stats", "ext_prices", "units", "asset_idx", "ring",
+                   "ring_ts", "ring_head", "ring_len", "win_price", "win_port", "win_ts",
+                   "reset_mask")
+
+
+class Views(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in VIEW_PTR_FIELDS] + [
+        ("out", Traj), ("n_envs", C.c_int32), ("n_assets", C.c_int32), ("window", C.c_int32),
+        ("reward_dim", C.c_int32)]
+
+
+class Ring(C.Structure):
+    _fields_ = [("n_envs", C.c_int32), ("n_price", C.c_int32), ("n_port", C.c_int32),
+                ("window", C.c_int32), ("norm_type", C.c_int32), ("pad_", C.c_int32),
+                ("ring", C.c_void_p), ("ring_ts", C.c_void_p), ("head", C.c_void_p),
+                ("len", C.c_void_p)]
+
+
+SYMBOLS = {
+    # name: (restype, argtypes)
+    "mgn_abi_version": (C.c_int, []),
+    "mgn_arena_bytes": (C.c_size_t, [C.POINTER(Config)]),
+    "mgn_create": (C.c_int, [C.POINTER(Config), C.POINTER(AssetSource), C.c_void_p, C.c_void_p,
+                             C.c_size_t, C.POINTER(C.c_void_p)]),
+    "mgn_destroy": (C.c_int, [C.c_void_p]),
+    "mgn_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mgn_get_views": (C.c_int, [C.c_void_p, C.POINTER(Views)]),
+    "mgn_reset": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mgn_step": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
+    "mgn_rollout": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(Traj)]),
+    "mgn_rollout_units": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(Traj)]),
+    "mgn_set_prices": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mgn_window_push": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mgn_window_clear": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mgn_window": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mgn_generate_actions": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_uint64]),
+    "mgn_valuation": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mgn_set_broker": (C.c_int, [C.c_void_p] + [C.c_double] * 6),
+    "mgn_ring_push": (C.c_int, [C.POINTER(Ring), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mgn_ring_clear": (C.c_int, [C.POINTER(Ring), C.c_void_p, C.c_void_p]),
+    "mgn_ring_gather": (C.c_int, [C.POINTER(Ring), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mgn_synchronize": (C.c_int, [C.c_void_p]),
+    "mgn_last_error": (C.c_char_p, [C.c_void_p]),
+    "mgn_global_error": (C.c_char_p, []),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load the HIP extension (no GPU needed to load it)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} is missing: build it with `python -m madigan_amd.build` "
+            "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    lib = C.CDLL(path)
+    for name, (res, args) in SYMBOLS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.mgn_abi_version() != ABI_VERSION:
+        raise ImportError("libmadigan_hip.so ABI version mismatch; rebuild the extension")
+    _lib = lib
+    return lib
+
+
+def check(status: int, handle=None) -> None:
+    if status == OK:
+        return
+    lib = load()
+    msg = (lib.mgn_last_error(handle) if handle else lib.mgn_global_error()) or b""
+    msg = msg.decode(errors="replace")
+    if status == ERR_CONFIG:
+        raise RuntimeError(msg)
+    if status == ERR_INDEX:
+        raise IndexError(msg)
+    if status == ERR_LENGTH:
+        raise ValueError(msg)
+    if status == ERR_ARG:
+        raise TypeError(msg)
+    raise MadiganError(msg)

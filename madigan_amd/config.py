@@ -1,0 +1,229 @@
+"""Reference config dict -> per-asset generator table and env knobs.
+
+Mirrors the reference's config handling for the data sources on the hot path:
+  makeConfigFromPyDict               madigan/environments/cpp/Config.cpp:5-164
+  Synth keys  (freq mu amp phase dX noise)             Config.cpp:166-214
+  OU keys     (mean theta phi)                         Config.cpp:353-386
+  TrendOU keys(trend_prob min_period max_period dYMin dYMax start theta phi
+               noise_trend ema_alpha)                   Config.cpp:479-549
+  Composite   {name: {data_source_type, data_source_config}} Config.cpp:107-126,
+              children concatenated, one per type, duplicate asset codes
+              renamed code+"_1"                         DataSource.cpp:411-437
+  default constructors Synth()/OU()/TrendOU()          DataSource.cpp:475-482, :1142,
+                                                       :1418-1423
+Errors follow the reference: missing keys -> RuntimeError (ConfigError),
+mismatched vector lengths -> ValueError (std::length_error), unknown source
+type -> RuntimeError (NotImplemented).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Any, List, Tuple
+
+from . import _lib as L
+
+SUPPORTED = ("Synth", "OU", "TrendOU", "Composite")
+NOT_YET = ("SawTooth", "Triangle", "SineAdder", "SineDynamic", "SineDynamicTrend", "Gaussian",
+           "OUPair", "SimpleTrend", "TrendyOU", "HDFSourceSingle")
+
+
+class ConfigError(RuntimeError):
+    """madigan::ConfigError (DataTypes.h:36-40) surfaces as RuntimeError."""
+
+
+@dataclass
+class SourceSpec:
+    kinds: List[int] = field(default_factory=list)
+    params: List[List[float]] = field(default_factory=list)
+    assets: List[str] = field(default_factory=list)
+
+    @property
+    def n_assets(self) -> int:
+        return len(self.kinds)
+
+    def extend(self, other: "SourceSpec") -> None:
+        for k, p, a in zip(other.kinds, other.params, other.assets):
+            self.kinds.append(k)
+            self.params.append(p)
+            # Composite renames duplicate codes (DataSource.cpp:428-431)
+            self.assets.append(a + "_1" if a in self.assets else a)
+
+
+def _get(cfg: Any, key: str, default=None):
+    if isinstance(cfg, dict):
+        return cfg.get(key, default)
+    return getattr(cfg, key, default)
+
+
+def _require(params: dict, keys: Tuple[str, ...]) -> None:
+    for k in keys:
+        if k not in params:
+            raise ConfigError(f"{k} key not found in data_source_config in config")
+
+
+def _same_len(name: str, *vecs) -> int:
+    n = len(vecs[0])
+    if any(len(v) != n for v in vecs):
+        raise ValueError(f"parameters passed to DataSource<PriceVector> of type {name} need to be "
+                         "vectors of same length")
+    return n
+
+
+def synth_spec(freq, mu, amp, phase, dX, noise=0.0) -> SourceSpec:
+    n = _same_len("Synth", freq, mu, amp, phase)
+    s = SourceSpec()
+    for i in range(n):
+        s.kinds.append(L.SRC_SINE)
+        s.params.append([float(freq[i]), float(mu[i]), float(amp[i]), float(phase[i]), float(dX),
+                         float(noise)])
+        s.assets.append(f"sine_{i}")
+    return s
+
+
+def ou_spec(mean, theta, phi) -> SourceSpec:
+    n = _same_len("OU", mean, theta, phi)
+    s = SourceSpec()
+    for i in range(n):
+        s.kinds.append(L.SRC_OU)
+        s.params.append([float(mean[i]), float(theta[i]), float(phi[i])])
+        s.assets.append(f"OU_{i}")
+    return s
+
+
+def trendou_spec(trendProb, minPeriod, maxPeriod, dYMin, dYMax, start, theta, phi, noiseTrend,
+                 emaAlpha) -> SourceSpec:
+    n = _same_len("TrendOU", trendProb, minPeriod, maxPeriod, dYMin, dYMax, start, theta, phi,
+                  noiseTrend, emaAlpha)
+    s = SourceSpec()
+    for i in range(n):
+        s.kinds.append(L.SRC_TRENDOU)
+        s.params.append([float(trendProb[i]), float(int(minPeriod[i])), float(int(maxPeriod[i])),
+                         float(dYMin[i]), float(dYMax[i]), float(start[i]), float(theta[i]),
+                         float(phi[i]), float(noiseTrend[i]), float(emaAlpha[i])])
+        s.assets.append(f"TrendOU_{i}")
+    return s
+
+
+def default_spec(source_type: str) -> SourceSpec:
+    """Default constructors (Env(type, initCash) without config)."""
+    if source_type == "Synth":
+        return synth_spec([1., 0.3, 2., 0.5], [2., 2.1, 2.2, 2.3], [1., 1.2, 1.3, 1.],
+                          [0., 1., 2., 1.], 0.01, 0.)
+    if source_type == "OU":
+        return ou_spec([2., 4.3, 3., 0.5], [1., 0.3, 2., 0.5], [2., 2.1, 2.2, 2.3])
+    if source_type == "TrendOU":
+        return trendou_spec([0.001, 0.001], [100, 500], [200, 1500], [0.001, 0.01], [0.003, 0.03],
+                            [10., 15.], [1., 0.5], [2., 2.1], [1., 1.2], [0.1, 0.2])
+    return _not_implemented(source_type)
+
+
+def _not_implemented(source_type: str):
+    if source_type in NOT_YET:
+        raise RuntimeError(f"Constructor from config for {source_type} as dataSource is not "
+                           "implemented on the MI355X path yet (SURVEY 8f)")
+    raise RuntimeError(f"Constructor from config for{source_type} as dataSource is not implemented")
+
+
+def spec_from_config(config: Any) -> SourceSpec:
+    """makeConfigFromPyDict + makeDataSource<PriceVector>(type, config)."""
+    source_type = _get(config, "data_source_type")
+    if source_type is None:
+        raise ConfigError("Config needs entry for data_source_type")
+    params = _get(config, "data_source_config")
+    if source_type == "Composite":
+        if params is None:
+            raise ConfigError("config passed but doesn't contain generator params")
+        children = {}
+        for _, sub in dict(params).items():
+            ctype = _get(sub, "data_source_type")
+            children[ctype] = sub  # keyed by type: one child per type (Config.cpp:121)
+        spec = SourceSpec()
+        for ctype, sub in children.items():
+            spec.extend(spec_from_config(sub))
+        return spec
+    if params is None:
+        raise ConfigError(f"config for DataSource type {source_type} needs generator params")
+    params = dict(params)
+    if source_type == "Synth":
+        _require(params, ("freq", "mu", "amp", "phase", "dX", "noise"))
+        return synth_spec(params["freq"], params["mu"], params["amp"], params["phase"],
+                          params["dX"], params["noise"])
+    if source_type == "OU":
+        _require(params, ("mean", "theta", "phi"))
+        return ou_spec(params["mean"], params["theta"], params["phi"])
+    if source_type == "TrendOU":
+        _require(params, ("trend_prob", "min_period", "max_period", "dYMin", "dYMax", "start",
+                          "theta", "phi", "noise_trend", "ema_alpha"))
+        return trendou_spec(params["trend_prob"], params["min_period"], params["max_period"],
+                            params["dYMin"], params["dYMax"], params["start"], params["theta"],
+                            params["phi"], params["noise_trend"], params["ema_alpha"])
+    return _not_implemented(source_type)
+
+
+SHAPER_CODES = {None: L.SHAPER_NONE, "None": L.SHAPER_NONE, "none": L.SHAPER_NONE,
+                "DSR": L.SHAPER_DSR, "DDR": L.SHAPER_DDR, "PPC": L.SHAPER_PPC, "cosine": L.SHAPER_PPC,
+                "cosine_similarity": L.SHAPER_PPC, "cosine_port_shaper": L.SHAPER_PPC}
+REWARD_MODES = {"env_log": L.REWARD_ENV_LOG, "agent_sum": L.REWARD_AGENT_SUM,
+                "agent_per_asset": L.REWARD_AGENT_PER_ASSET}
+NORM_CODES = {None: L.NORM_NONE, "none": L.NORM_NONE, "log": L.NORM_LOG,
+              "lookback": L.NORM_LOOKBACK, "standard_normal": L.NORM_STANDARD_NORMAL,
+              "lookback_log": L.NORM_LOOKBACK_LOG}
+
+
+def shaper_code(name) -> int:
+    if name not in SHAPER_CODES:
+        raise NotImplementedError(f"Reward Shaper type {name} not implemented")
+    return SHAPER_CODES[name]
+
+
+def norm_code(name) -> int:
+    if name not in NORM_CODES:
+        raise NotImplementedError(
+            f"norm_type {name} is not implemented. choose from : 'lookback', 'lookback_log', "
+            "'standard_normal', 'log'")
+    return NORM_CODES[name]
+
+
+def build_config(spec: SourceSpec, *, n_envs: int, init_cash: float = 1_000_000.0,
+                 required_margin: float = 0.0, maintenance_margin: float = 0.0,
+                 slippage_rel: float = 0.0, slippage_abs: float = 0.0,
+                 transaction_cost_rel: float = 0.0, transaction_cost_abs: float = 0.0,
+                 reward_shaper=None, reward_mode: str = "env_log", adaptation_rate: float = 0.001,
+                 cosine_temp: float = 0.0, desired_portfolio=None, window: int = 0,
+                 norm_type=None, auto_reset: bool = False, action_atoms: int = 3,
+                 unit_size: float = 0.05, seed: int = 0, env_offset: int = 0):
+    A = spec.n_assets
+    if A < 1 or A > L.MAX_ASSETS:
+        raise ValueError(f"n_assets must be in [1, {L.MAX_ASSETS}], got {A}")
+    c = L.Config()
+    c.n_envs = int(n_envs)
+    c.n_assets = A
+    c.env_offset = int(env_offset)
+    c.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    c.init_cash = float(init_cash)
+    c.required_margin = float(required_margin)
+    c.maintenance_margin = float(maintenance_margin)
+    c.slippage_rel, c.slippage_abs = float(slippage_rel), float(slippage_abs)
+    c.tc_rel, c.tc_abs = float(transaction_cost_rel), float(transaction_cost_abs)
+    c.shaper = shaper_code(reward_shaper)
+    if reward_mode not in REWARD_MODES:
+        raise ConfigError(f"unknown reward_mode {reward_mode}")
+    c.reward_mode = REWARD_MODES[reward_mode]
+    c.adaptation_rate = float(adaptation_rate)
+    c.cosine_temp = float(cosine_temp)
+    dp = list(desired_portfolio) if desired_portfolio is not None else [1.0] + [0.0] * A
+    if len(dp) != A + 1:
+        raise ValueError(f"desired_portfolio needs {A + 1} entries (cash + assets), got {len(dp)}")
+    for i, v in enumerate(dp):
+        c.desired_portfolio[i] = float(v)
+    c.window = int(window)
+    c.norm_type = norm_code(norm_type)
+    c.auto_reset = 1 if auto_reset else 0
+    c.action_atoms = int(action_atoms)
+    c.unit_size = float(unit_size)
+    srcs = (L.AssetSource * A)()
+    for i, (k, p) in enumerate(zip(spec.kinds, spec.params)):
+        srcs[i].kind = k
+        for j, v in enumerate(p):
+            srcs[i].p[j] = v
+    return c, srcs

@@ -1,0 +1,481 @@
+// mgn_api.hip -- C ABI (include/madigan_amd.h) over the gfx950 kernels.
+//
+// One handle owns every device buffer of N envs in one arena (caller-provided
+// or hipMalloc'd), launches on one stream and never synchronises the host
+// except in mgn_create's parameter upload and mgn_synchronize.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "../../include/madigan_amd.h"
+#include "mgn_kernels.h"
+
+namespace {
+
+thread_local std::string g_error;
+
+struct Layout {
+  size_t off[40];
+  int n = 0;
+  size_t total = 0;
+  size_t add(size_t bytes) {
+    const size_t o = total;
+    off[n++] = o;
+    total += (bytes + 255) & ~size_t(255);
+    return o;
+  }
+};
+
+int next_pow2(int a) {
+  int p = 1;
+  while (p < a) p <<= 1;
+  return p;
+}
+
+}  // namespace
+
+struct mgn_env {
+  mgn_config cfg;
+  int N, A, W, D, apad;
+  hipStream_t stream;
+  void* arena;
+  bool own_arena;
+  size_t arena_bytes;
+  mgn_views v;
+  mgn_asset_source* src_dev;
+  double* target_dev;
+  std::string err;
+};
+
+namespace {
+
+struct Offsets {
+  size_t L, mep, Bm, P, sx, oum, dy, tlen, tfl, cash, ts, sA, sB, ep, epstats, ext, units, aidx,
+      ring, ring_ts, rhead, rlen, wprice, wport, wts, mask, reward, areward, shaped, done, obsp,
+      obsport, obsts, tprice, tunits, tcost, risk, mcall, src, target;
+  size_t total;
+};
+
+Offsets plan(const mgn_config* c) {
+  const size_t N = (size_t)c->n_envs, A = (size_t)c->n_assets;
+  const size_t W = (size_t)(c->window > 0 ? c->window : 0);
+  const size_t D = (c->reward_mode == MGN_REWARD_AGENT_PER_ASSET) ? A : 1;
+  Layout l;
+  Offsets o;
+  o.L = l.add(N * A * 8);
+  o.mep = l.add(N * A * 8);
+  o.Bm = l.add(N * A * 8);
+  o.P = l.add(N * A * 8);
+  o.sx = l.add(N * A * 8);
+  o.oum = l.add(N * A * 8);
+  o.dy = l.add(N * A * 8);
+  o.tlen = l.add(N * A * 4);
+  o.tfl = l.add(N * A);
+  o.cash = l.add(N * 8);
+  o.ts = l.add(N * 8);
+  o.sA = l.add(N * D * 8);
+  o.sB = l.add(N * D * 8);
+  o.ep = l.add(N * 2 * 8);
+  o.epstats = l.add(N * 4 * 8);
+  o.ext = l.add(N * A * 8);
+  o.units = l.add(N * A * 8);
+  o.aidx = l.add(N * 4);
+  o.ring = l.add(N * W * (2 * A + 1) * 8);
+  o.ring_ts = l.add(N * W * 8);
+  o.rhead = l.add(N * 4);
+  o.rlen = l.add(N * 4);
+  o.wprice = l.add(N * W * A * 8);
+  o.wport = l.add(N * W * (A + 1) * 8);
+  o.wts = l.add(N * W * 8);
+  o.mask = l.add(N);
+  o.reward = l.add(N * 8);
+  o.areward = l.add(N * D * 8);
+  o.shaped = l.add(N * D * 8);
+  o.done = l.add(N);
+  o.obsp = l.add(N * A * 8);
+  o.obsport = l.add(N * (A + 1) * 8);
+  o.obsts = l.add(N * 8);
+  o.tprice = l.add(N * A * 8);
+  o.tunits = l.add(N * A * 8);
+  o.tcost = l.add(N * A * 8);
+  o.risk = l.add(N * A);
+  o.mcall = l.add(N);
+  o.src = l.add(A * sizeof(mgn_asset_source));
+  o.target = l.add((A + 1) * 8);
+  o.total = l.total;
+  return o;
+}
+
+int fail(mgn_env* e, int code, const std::string& msg) {
+  if (e) e->err = msg;
+  g_error = msg;
+  return code;
+}
+
+int check_hip(mgn_env* e, hipError_t st, const char* what) {
+  if (st == hipSuccess) return MGN_OK;
+  return fail(e, MGN_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(st));
+}
+
+int validate(const mgn_config* c, const mgn_asset_source* s, std::string& msg) {
+  if (!c || !s) { msg = "null config"; return MGN_ERR_ARG; }
+  if (c->n_envs < 1) { msg = "n_envs must be >= 1"; return MGN_ERR_LENGTH; }
+  if (c->n_assets < 1 || c->n_assets > MGN_MAX_ASSETS) {
+    msg = "n_assets must be in [1, 64]";
+    return MGN_ERR_LENGTH;
+  }
+  if (c->window < 0) { msg = "window must be >= 0"; return MGN_ERR_CONFIG; }
+  if (c->shaper < 0 || c->shaper > MGN_SHAPER_PPC) { msg = "unknown reward shaper"; return MGN_ERR_CONFIG; }
+  if (c->reward_mode < 0 || c->reward_mode > MGN_REWARD_AGENT_PER_ASSET) {
+    msg = "unknown reward_mode";
+    return MGN_ERR_CONFIG;
+  }
+  if (c->norm_type < 0 || c->norm_type > MGN_NORM_LOOKBACK_LOG) { msg = "unknown norm_type"; return MGN_ERR_CONFIG; }
+  for (int i = 0; i < c->n_assets; ++i) {
+    const int k = s[i].kind;
+    if (k < MGN_SRC_EXTERNAL || k > MGN_SRC_TRENDOU) {
+      msg = "unknown data source kind for asset " + std::to_string(i);
+      return MGN_ERR_CONFIG;
+    }
+    if (k == MGN_SRC_TRENDOU && s[i].p[2] < s[i].p[1]) {
+      msg = "TrendOU maxPeriod < minPeriod for asset " + std::to_string(i);
+      return MGN_ERR_CONFIG;
+    }
+  }
+  return MGN_OK;
+}
+
+mgn::KParams kparams(const mgn_env* e) {
+  mgn::KParams p;
+  const mgn_config& c = e->cfg;
+  p.N = e->N; p.A = e->A; p.W = e->W; p.D = e->D;
+  p.env_offset = c.env_offset; p.seed = c.seed;
+  p.init_cash = c.init_cash; p.reqM = c.required_margin; p.mainM = c.maintenance_margin;
+  p.slip_rel = c.slippage_rel; p.slip_abs = c.slippage_abs; p.tc_rel = c.tc_rel; p.tc_abs = c.tc_abs;
+  p.shaper = c.shaper; p.reward_mode = c.reward_mode; p.auto_reset = c.auto_reset;
+  p.atoms = c.action_atoms; p.eta = c.adaptation_rate; p.cos_temp = c.cosine_temp;
+  p.unit_size = c.unit_size;
+  const mgn_views& v = e->v;
+  p.L = v.ledger; p.mep = v.mean_entry; p.Bm = v.borrowed; p.P = v.prices;
+  p.sx = v.sine_x; p.oum = v.ou_mean; p.dy = v.trend_dy; p.tlen = v.trend_len; p.tfl = v.trend_flags;
+  p.cash = v.cash; p.ts = v.timestamp; p.sA = v.shaper_a; p.sB = v.shaper_b;
+  p.ep = v.ep_stats; p.epstats = v.episode_stats; p.ext = v.ext_prices;
+  p.ring = v.ring; p.ring_ts = v.ring_ts; p.rhead = v.ring_head; p.rlen = v.ring_len;
+  p.src = e->src_dev; p.target = e->target_dev;
+  return p;
+}
+
+// dispatch on APAD with one asset per lane (M = 1, S = APAD)
+template <template <int, int> class F, typename... Args>
+void dispatch(int apad, Args&&... args) {
+  switch (apad) {
+    case 1: F<1, 1>::run(args...); break;
+    case 2: F<1, 2>::run(args...); break;
+    case 4: F<1, 4>::run(args...); break;
+    case 8: F<1, 8>::run(args...); break;
+    case 16: F<1, 16>::run(args...); break;
+    case 32: F<1, 32>::run(args...); break;
+    default: F<1, 64>::run(args...); break;
+  }
+}
+
+template <int M, int S>
+struct StepL {
+  static void run(const mgn_env* e, const mgn_traj& out, int in_kind, const double* units,
+                  const int32_t* aidx, const int8_t* act, int K) {
+    const int epb = mgn::BLOCK / S;
+    const int grid = (e->N + epb - 1) / epb;
+    hipLaunchKernelGGL((mgn::k_step<M, S>), dim3(grid), dim3(mgn::BLOCK), 0, e->stream, kparams(e),
+                       out, in_kind, units, aidx, act, K);
+  }
+};
+
+template <int M, int S>
+struct InitL {
+  static void run(const mgn_env* e, int mode, const uint8_t* mask) {
+    const int epb = mgn::BLOCK / S;
+    const int grid = (e->N + epb - 1) / epb;
+    hipLaunchKernelGGL((mgn::k_init_reset<M, S>), dim3(grid), dim3(mgn::BLOCK), 0, e->stream,
+                       kparams(e), mode, mask);
+  }
+};
+
+template <int M, int S>
+struct ValL {
+  static void run(const mgn_env* e, double* out) {
+    const int epb = mgn::BLOCK / S;
+    const int grid = (e->N + epb - 1) / epb;
+    hipLaunchKernelGGL((mgn::k_valuation<M, S>), dim3(grid), dim3(mgn::BLOCK), 0, e->stream,
+                       kparams(e), out);
+  }
+};
+
+mgn::RingDesc ring_desc(const mgn_env* e) {
+  mgn::RingDesc r;
+  r.N = e->N; r.F = e->A; r.Pn = e->A + 1; r.W = e->W; r.norm = e->cfg.norm_type;
+  r.ring = e->v.ring; r.ring_ts = e->v.ring_ts; r.head = e->v.ring_head; r.len = e->v.ring_len;
+  return r;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mgn_abi_version(void) { return MGN_ABI_VERSION; }
+
+size_t mgn_arena_bytes(const mgn_config* cfg) {
+  if (!cfg || cfg->n_envs < 1 || cfg->n_assets < 1 || cfg->n_assets > MGN_MAX_ASSETS) return 0;
+  return plan(cfg).total;
+}
+
+int mgn_create(const mgn_config* cfg, const mgn_asset_source* sources, void* stream, void* arena,
+               size_t arena_bytes, mgn_env** out) {
+  if (!out) return fail(nullptr, MGN_ERR_ARG, "out handle pointer is null");
+  *out = nullptr;
+  std::string msg;
+  int st = validate(cfg, sources, msg);
+  if (st != MGN_OK) return fail(nullptr, st, msg);
+  mgn_env* e = new (std::nothrow) mgn_env();
+  if (!e) return fail(nullptr, MGN_ERR_DEVICE, "host allocation failed");
+  e->cfg = *cfg;
+  e->N = cfg->n_envs;
+  e->A = cfg->n_assets;
+  e->W = cfg->window > 0 ? cfg->window : 0;
+  e->D = (cfg->reward_mode == MGN_REWARD_AGENT_PER_ASSET) ? e->A : 1;
+  e->apad = next_pow2(e->A);
+  e->stream = (hipStream_t)stream;
+  const Offsets o = plan(cfg);
+  e->arena_bytes = o.total;
+  if (arena) {
+    if (arena_bytes < o.total) {
+      delete e;
+      return fail(nullptr, MGN_ERR_LENGTH, "arena smaller than mgn_arena_bytes()");
+    }
+    e->arena = arena;
+    e->own_arena = false;
+  } else {
+    hipError_t h = hipMalloc(&e->arena, o.total);
+    if (h != hipSuccess) {
+      delete e;
+      return fail(nullptr, MGN_ERR_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(h));
+    }
+    e->own_arena = true;
+  }
+  char* b = (char*)e->arena;
+  mgn_views& v = e->v;
+  v.ledger = (double*)(b + o.L); v.mean_entry = (double*)(b + o.mep); v.borrowed = (double*)(b + o.Bm);
+  v.prices = (double*)(b + o.P); v.sine_x = (double*)(b + o.sx); v.ou_mean = (double*)(b + o.oum);
+  v.trend_dy = (double*)(b + o.dy); v.trend_len = (int32_t*)(b + o.tlen); v.trend_flags = (uint8_t*)(b + o.tfl);
+  v.cash = (double*)(b + o.cash); v.timestamp = (uint64_t*)(b + o.ts);
+  v.shaper_a = (double*)(b + o.sA); v.shaper_b = (double*)(b + o.sB);
+  v.ep_stats = (double*)(b + o.ep); v.episode_stats = (double*)(b + o.epstats);
+  v.ext_prices = (double*)(b + o.ext); v.units = (double*)(b + o.units); v.asset_idx = (int32_t*)(b + o.aidx);
+  v.ring = e->W ? (double*)(b + o.ring) : nullptr; v.ring_ts = e->W ? (uint64_t*)(b + o.ring_ts) : nullptr;
+  v.ring_head = (int32_t*)(b + o.rhead); v.ring_len = (int32_t*)(b + o.rlen);
+  v.win_price = e->W ? (double*)(b + o.wprice) : nullptr; v.win_port = e->W ? (double*)(b + o.wport) : nullptr;
+  v.win_ts = e->W ? (uint64_t*)(b + o.wts) : nullptr; v.reset_mask = (uint8_t*)(b + o.mask);
+  v.out.reward = (double*)(b + o.reward); v.out.agent_reward = (double*)(b + o.areward);
+  v.out.shaped = (double*)(b + o.shaped); v.out.done = (uint8_t*)(b + o.done);
+  v.out.obs_price = (double*)(b + o.obsp); v.out.obs_port = (double*)(b + o.obsport);
+  v.out.timestamp = (uint64_t*)(b + o.obsts); v.out.tprice = (double*)(b + o.tprice);
+  v.out.tunits = (double*)(b + o.tunits); v.out.tcost = (double*)(b + o.tcost);
+  v.out.risk = (uint8_t*)(b + o.risk); v.out.margin_call = (uint8_t*)(b + o.mcall);
+  v.n_envs = e->N; v.n_assets = e->A; v.window = e->W; v.reward_dim = e->D;
+  e->src_dev = (mgn_asset_source*)(b + o.src);
+  e->target_dev = (double*)(b + o.target);
+
+  int rc = check_hip(e, hipMemsetAsync(e->arena, 0, o.total, e->stream), "hipMemsetAsync");
+  if (rc == MGN_OK)
+    rc = check_hip(e, hipMemcpyAsync(e->src_dev, sources, sizeof(mgn_asset_source) * e->A,
+                                     hipMemcpyHostToDevice, e->stream), "hipMemcpyAsync(src)");
+  if (rc == MGN_OK)
+    rc = check_hip(e, hipMemcpyAsync(e->target_dev, cfg->desired_portfolio, 8 * (e->A + 1),
+                                     hipMemcpyHostToDevice, e->stream), "hipMemcpyAsync(target)");
+  if (rc == MGN_OK) {
+    dispatch<InitL>(e->apad, e, 0, (const uint8_t*)nullptr);
+    rc = check_hip(e, hipGetLastError(), "k_init_reset");
+  }
+  if (rc == MGN_OK) rc = check_hip(e, hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+  if (rc != MGN_OK) {
+    const std::string m = e->err;
+    if (e->own_arena) (void)hipFree(e->arena);
+    delete e;
+    return fail(nullptr, rc, m);
+  }
+  *out = e;
+  return MGN_OK;
+}
+
+int mgn_destroy(mgn_env* e) {
+  if (!e) return MGN_ERR_ARG;
+  (void)hipStreamSynchronize(e->stream);
+  if (e->own_arena) (void)hipFree(e->arena);
+  delete e;
+  return MGN_OK;
+}
+
+int mgn_set_stream(mgn_env* e, void* stream) {
+  if (!e) return MGN_ERR_ARG;
+  e->stream = (hipStream_t)stream;
+  return MGN_OK;
+}
+
+int mgn_get_views(const mgn_env* e, mgn_views* views) {
+  if (!e || !views) return MGN_ERR_ARG;
+  *views = e->v;
+  return MGN_OK;
+}
+
+int mgn_reset(mgn_env* e, const uint8_t* mask_dev) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  dispatch<InitL>(e->apad, e, 1, mask_dev);
+  return check_hip(e, hipGetLastError(), "mgn_reset");
+}
+
+int mgn_step(mgn_env* e, int32_t kind, const double* units_dev, const int32_t* aidx_dev) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  int in_kind;
+  if (kind == MGN_STEP_NONE) in_kind = mgn::IN_NONE;
+  else if (kind == MGN_STEP_UNITS) in_kind = mgn::IN_UNITS;
+  else if (kind == MGN_STEP_SINGLE) in_kind = mgn::IN_SINGLE;
+  else return fail(e, MGN_ERR_CONFIG, "unknown step kind");
+  if (in_kind != mgn::IN_NONE && !units_dev) return fail(e, MGN_ERR_ARG, "units pointer is null");
+  if (in_kind == mgn::IN_SINGLE && !aidx_dev) return fail(e, MGN_ERR_ARG, "asset index pointer is null");
+  dispatch<StepL>(e->apad, e, e->v.out, in_kind, units_dev, aidx_dev, (const int8_t*)nullptr, 1);
+  return check_hip(e, hipGetLastError(), "mgn_step");
+}
+
+int mgn_rollout(mgn_env* e, const int8_t* actions_dev, int32_t k_steps, const mgn_traj* out) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  if (!actions_dev || !out) return fail(e, MGN_ERR_ARG, "null actions/out");
+  if (k_steps < 1) return fail(e, MGN_ERR_LENGTH, "k_steps must be >= 1");
+  dispatch<StepL>(e->apad, e, *out, (int)mgn::IN_DISCRETE, (const double*)nullptr,
+                  (const int32_t*)nullptr, actions_dev, (int)k_steps);
+  return check_hip(e, hipGetLastError(), "mgn_rollout");
+}
+
+int mgn_rollout_units(mgn_env* e, const double* units_dev, int32_t k_steps, const mgn_traj* out) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  if (!units_dev || !out) return fail(e, MGN_ERR_ARG, "null units/out");
+  if (k_steps < 1) return fail(e, MGN_ERR_LENGTH, "k_steps must be >= 1");
+  dispatch<StepL>(e->apad, e, *out, (int)mgn::IN_UNITS, units_dev, (const int32_t*)nullptr,
+                  (const int8_t*)nullptr, (int)k_steps);
+  return check_hip(e, hipGetLastError(), "mgn_rollout_units");
+}
+
+int mgn_set_prices(mgn_env* e, const double* prices_dev) {
+  if (!e || !prices_dev) return fail(e, MGN_ERR_ARG, "null handle/prices");
+  return check_hip(e, hipMemcpyAsync(e->v.ext_prices, prices_dev, sizeof(double) * e->N * e->A,
+                                     hipMemcpyDeviceToDevice, e->stream), "mgn_set_prices");
+}
+
+int mgn_window_push(mgn_env* e, const double* price_dev, const double* port_dev, const uint64_t* ts_dev) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  if (e->W == 0) return fail(e, MGN_ERR_CONFIG, "handle has no window (window_length = 0)");
+  const mgn::RingDesc r = ring_desc(e);
+  const double* pr = price_dev ? price_dev : e->v.out.obs_price;
+  const double* po = port_dev ? port_dev : e->v.out.obs_port;
+  const uint64_t* t = ts_dev ? ts_dev : e->v.out.timestamp;
+  hipLaunchKernelGGL(mgn::k_ring_push, dim3((e->N + 255) / 256), dim3(256), 0, e->stream, r, pr, po, t);
+  return check_hip(e, hipGetLastError(), "mgn_window_push");
+}
+
+int mgn_window_clear(mgn_env* e, const uint8_t* mask_dev) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  if (e->W == 0) return fail(e, MGN_ERR_CONFIG, "handle has no window (window_length = 0)");
+  hipLaunchKernelGGL(mgn::k_ring_clear, dim3((e->N + 255) / 256), dim3(256), 0, e->stream,
+                     ring_desc(e), mask_dev);
+  return check_hip(e, hipGetLastError(), "mgn_window_clear");
+}
+
+int mgn_window(mgn_env* e, double* price_dev, double* port_dev, uint64_t* ts_dev) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  if (e->W == 0) return fail(e, MGN_ERR_CONFIG, "handle has no window (window_length = 0)");
+  const mgn::RingDesc r = ring_desc(e);
+  const int64_t threads = (int64_t)e->N * (2 * e->A + 1);
+  hipLaunchKernelGGL(mgn::k_ring_gather, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     e->stream, r, price_dev ? price_dev : e->v.win_price,
+                     port_dev ? port_dev : e->v.win_port, ts_dev ? ts_dev : e->v.win_ts);
+  return check_hip(e, hipGetLastError(), "mgn_window");
+}
+
+int mgn_generate_actions(mgn_env* e, int8_t* actions_dev, int32_t k_steps, uint64_t seed) {
+  if (!e || !actions_dev) return fail(e, MGN_ERR_ARG, "null handle/actions");
+  const int64_t total = (int64_t)k_steps * e->N * e->A;
+  hipLaunchKernelGGL(mgn::k_gen_actions, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     e->stream, actions_dev, (int)k_steps, e->N, e->A, e->cfg.action_atoms, seed,
+                     e->cfg.env_offset);
+  return check_hip(e, hipGetLastError(), "mgn_generate_actions");
+}
+
+int mgn_valuation(mgn_env* e, double* out_dev) {
+  if (!e || !out_dev) return fail(e, MGN_ERR_ARG, "null handle/out");
+  dispatch<ValL>(e->apad, e, out_dev);
+  return check_hip(e, hipGetLastError(), "mgn_valuation");
+}
+
+int mgn_set_broker(mgn_env* e, double required_margin, double maintenance_margin,
+                   double slippage_rel, double slippage_abs, double tc_rel, double tc_abs) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  e->cfg.required_margin = required_margin;
+  e->cfg.maintenance_margin = maintenance_margin;
+  e->cfg.slippage_rel = slippage_rel;
+  e->cfg.slippage_abs = slippage_abs;
+  e->cfg.tc_rel = tc_rel;
+  e->cfg.tc_abs = tc_abs;
+  return MGN_OK;
+}
+
+static mgn::RingDesc ring_from(const mgn_ring* r) {
+  mgn::RingDesc d;
+  d.N = r->n_envs; d.F = r->n_price; d.Pn = r->n_port; d.W = r->window; d.norm = r->norm_type;
+  d.ring = r->ring; d.ring_ts = r->ring_ts; d.head = r->head; d.len = r->len;
+  return d;
+}
+
+static int ring_ok(const mgn_ring* r) {
+  if (!r || !r->ring || !r->ring_ts || !r->head || !r->len) return fail(nullptr, MGN_ERR_ARG, "null ring buffers");
+  if (r->n_envs < 1 || r->window < 1 || r->n_price < 0 || r->n_port < 0)
+    return fail(nullptr, MGN_ERR_LENGTH, "bad ring dimensions");
+  if (r->norm_type < 0 || r->norm_type > MGN_NORM_LOOKBACK_LOG) return fail(nullptr, MGN_ERR_CONFIG, "unknown norm_type");
+  return MGN_OK;
+}
+
+int mgn_ring_push(const mgn_ring* r, const double* price_dev, const double* port_dev,
+                  const uint64_t* ts_dev, void* stream) {
+  int rc = ring_ok(r);
+  if (rc != MGN_OK) return rc;
+  hipLaunchKernelGGL(mgn::k_ring_push, dim3((r->n_envs + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     ring_from(r), price_dev, port_dev, ts_dev);
+  return check_hip(nullptr, hipGetLastError(), "mgn_ring_push");
+}
+
+int mgn_ring_clear(const mgn_ring* r, const uint8_t* mask_dev, void* stream) {
+  int rc = ring_ok(r);
+  if (rc != MGN_OK) return rc;
+  hipLaunchKernelGGL(mgn::k_ring_clear, dim3((r->n_envs + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     ring_from(r), mask_dev);
+  return check_hip(nullptr, hipGetLastError(), "mgn_ring_clear");
+}
+
+int mgn_ring_gather(const mgn_ring* r, double* price_dev, double* port_dev, uint64_t* ts_dev, void* stream) {
+  int rc = ring_ok(r);
+  if (rc != MGN_OK) return rc;
+  const int64_t threads = (int64_t)r->n_envs * (r->n_price + r->n_port);
+  hipLaunchKernelGGL(mgn::k_ring_gather, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, ring_from(r), price_dev, port_dev, ts_dev);
+  return check_hip(nullptr, hipGetLastError(), "mgn_ring_gather");
+}
+
+int mgn_synchronize(mgn_env* e) {
+  if (!e) return MGN_ERR_ARG;
+  return check_hip(e, hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+}
+
+const char* mgn_last_error(const mgn_env* e) { return e ? e->err.c_str() : g_error.c_str(); }
+const char* mgn_global_error(void) { return g_error.c_str(); }
+
+}  // extern "C"

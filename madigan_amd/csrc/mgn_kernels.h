@@ -1,0 +1,869 @@
+// mgn_kernels.h -- HIP kernels of the batched market-simulation step (gfx950).
+//
+// Thread mapping: an environment is owned by a segment of S adjacent lanes of
+// one wavefront; each lane holds M consecutive assets (S*M = APAD, the next
+// power of two >= n_assets) in registers.  State is struct-of-arrays, env-major
+// (N,A) row-major in HBM, so a wave-wide load of one field is one contiguous
+// burst.  Portfolio-wide quantities (asset value, pnl, balance, borrowed
+// margin) are reduced with the canonical pairwise tree: a register tree over
+// the lane's M slots, then an xor butterfly across the S lanes -- the same tree
+// the oracle evaluates, so ledger state is bit-identical.
+//
+// The Broker's per-asset loop is a true serial dependency (each order's risk
+// check sees the cash/ledger left by the previous one, Broker.cpp:149-155):
+// round i is executed by the lane owning asset i after a segment reduction,
+// and the new cash is broadcast back to the segment.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/madigan_amd.h"
+#include "mgn_math.h"
+
+namespace mgn {
+
+constexpr int BLOCK = 256;
+
+struct KParams {
+  int N, A, W, D;
+  int64_t env_offset;
+  uint64_t seed;
+  double init_cash, reqM, mainM, slip_rel, slip_abs, tc_rel, tc_abs;
+  int shaper, reward_mode, auto_reset, atoms;
+  double eta, cos_temp, unit_size;
+  // state
+  double *L, *mep, *Bm, *P, *sx, *oum, *dy;
+  int32_t *tlen;
+  uint8_t *tfl;
+  double *cash;
+  uint64_t *ts;
+  double *sA, *sB;
+  double *ep;       // (N,2)
+  double *epstats;  // (N,4)
+  const double *ext;
+  double *ring;
+  uint64_t *ring_ts;
+  int32_t *rhead, *rlen;
+  const mgn_asset_source *src;  // (A)
+  const double *target;         // (A+1)
+};
+
+// ---------------------------------------------------------------------------
+// reductions
+template <int M>
+__device__ __forceinline__ double tree(const double (&v)[M]) {
+  if constexpr (M == 1) {
+    return v[0];
+  } else {
+    double t[M / 2];
+#pragma unroll
+    for (int i = 0; i < M / 2; ++i) t[i] = v[2 * i] + v[2 * i + 1];
+    return tree<M / 2>(t);
+  }
+}
+
+template <int S>
+__device__ __forceinline__ double seg_sum(double v) {
+#pragma unroll
+  for (int o = 1; o < S; o <<= 1) v = v + __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int S>
+__device__ __forceinline__ int seg_or(int v) {
+#pragma unroll
+  for (int o = 1; o < S; o <<= 1) v = v | __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int M, int S>
+__device__ __forceinline__ double canon(const double (&v)[M]) {
+  return seg_sum<S>(tree<M>(v));
+}
+
+struct Sums {
+  double lp, ml, sh, b;
+};
+
+// Portfolio.cpp:180-209 -- the four sums every valuation is built from
+template <int M, int S>
+__device__ __forceinline__ Sums port_sums(const double (&L)[M], const double (&mep)[M],
+                                          const double (&Bm)[M], const double (&P)[M]) {
+  double tlp[M], tml[M], tsh[M], tb[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    tlp[m] = L[m] * P[m];
+    tml[m] = mep[m] * L[m];
+    const double mask = (L[m] < 0.) ? 1.0 : 0.0;
+    tsh[m] = L[m] * (mep[m] * mask);
+    tb[m] = Bm[m];
+  }
+  Sums s;
+  s.lp = canon<M, S>(tlp);
+  s.ml = canon<M, S>(tml);
+  s.sh = canon<M, S>(tsh);
+  s.b = canon<M, S>(tb);
+  return s;
+}
+
+// Portfolio::checkRisk() == margin_call, Portfolio.cpp:243-252
+__device__ __forceinline__ bool margin_call(const Sums& s, double cash, double mainM) {
+  const double pnl = s.lp - s.ml;
+  const double equity = (cash + s.lp) - s.b;
+  const double balance = cash + s.sh;
+  const double mr = mainM * pnl;
+  return (equity <= -mr) || ((balance + pnl) <= -mr);
+}
+
+// ---------------------------------------------------------------------------
+// per-lane register state
+template <int M>
+struct Lane {
+  double L[M], mep[M], Bm[M], P[M], sx[M], oum[M], dy[M];
+  int32_t tlen[M];
+  uint8_t tfl[M];  // bit0 trending, bit1 dir<0
+  int kind[M];
+  int asset[M];
+  bool valid[M];
+};
+
+// DataSource::getData for the lane's slots (DataSource.cpp:535-543, 1173-1180,
+// 1457-1493; Composite concatenation :439-451) ; tick = timestamp before ++.
+template <int M>
+__device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, uint64_t tick) {
+  const uint64_t genv = (uint64_t)(p.env_offset + env);
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    if (!s.valid[m]) continue;
+    const int a = s.asset[m];
+    const double* q = p.src[a].p;
+    const int kind = s.kind[m];
+    if (kind == MGN_SRC_TRENDOU) {
+      double y = s.P[m];
+      if (s.tfl[m] & 1) {
+        const double n = normal(p.seed, genv, (uint32_t)a, 0, tick) * q[8] + 0.0;
+        const double dir = (s.tfl[m] & 2) ? -1.0 : 1.0;
+        y += y * (s.dy[m] * dir + n);
+        s.tlen[m] -= 1;
+        if (s.tlen[m] == 0) {
+          s.tfl[m] &= ~1;
+          s.oum[m] = y;
+        }
+        y = (0.01 < y) ? y : 0.01;
+        if (y <= .1) s.tfl[m] &= ~2;
+      } else {
+        const double n = normal(p.seed, genv, (uint32_t)a, 0, tick) * q[7] + 0.0;
+        const double ou_noise = y * n;
+        const double ou_rev = q[6] * (s.oum[m] - y);
+        y += ou_rev + ou_noise;
+        double u_trend, u_dir;
+        uniform2(p.seed, genv, (uint32_t)a, 1, tick, u_trend, u_dir);
+        if (u_trend < q[0]) {
+          double u_len, u_dy;
+          uniform2(p.seed, genv, (uint32_t)a, 2, tick, u_len, u_dy);
+          const int32_t lo = (int32_t)q[1], hi = (int32_t)q[2];
+          int32_t len = lo + (int32_t)(u_len * (double)(hi - lo + 1));
+          if (len > hi) len = hi;
+          s.tlen[m] = len;
+          s.dy[m] = (q[4] - q[3]) * u_dy + q[3];
+          s.tfl[m] = (uint8_t)(1 | ((u_dir < 0.5) ? 2 : 0));
+        }
+      }
+      s.P[m] = y;
+    } else if (kind == MGN_SRC_OU) {
+      const double z = normal(p.seed, genv, (uint32_t)a, 0, tick) * 1.0 + 0.0;
+      double x = s.P[m];
+      x += (q[1] * (q[0] - x)) + q[0] * q[2] * z;
+      s.P[m] = x;
+    } else if (kind == MGN_SRC_SINE) {
+      double noise = 0.0;
+      if (q[5] != 0.0) noise = normal(p.seed, genv, (uint32_t)a, 0, tick) * q[5] + 0.0;
+      const double PI2 = 3.141592653589793238463 * 2;
+      s.P[m] = noise + q[1] + q[2] * det_sin(PI2 * s.sx[m] * q[0]);
+      s.sx[m] += q[4];
+    } else {
+      s.P[m] = p.ext[(size_t)env * p.A + a];
+    }
+  }
+}
+
+// source reset (DataSource.h:466, :232; DataSource.cpp:1495-1502)
+template <int M>
+__device__ __forceinline__ void src_reset(Lane<M>& s, const KParams& p) {
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    if (s.valid[m] && s.kind[m] == MGN_SRC_TRENDOU) {
+      const double start = p.src[s.asset[m]].p[5];
+      s.tfl[m] &= ~1;
+      s.P[m] = start;
+      s.tlen[m] = 0;
+      s.oum[m] = start;
+    }
+  }
+}
+
+// StackerDiscrete.stream_state of the current State (preprocessor.py:172-175)
+template <int M, int S>
+__device__ __forceinline__ void ring_push(const Lane<M>& s, const KParams& p, int env, int ls,
+                                          double cash, uint64_t ts, int32_t& head, int32_t& len) {
+  const Sums q = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
+  const double eq = (cash + q.lp) - q.b;
+  head = (head + 1) % p.W;
+  if (len < p.W) len += 1;
+  const int R = 2 * p.A + 1;
+  double* row = p.ring + ((size_t)env * p.W + head) * R;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    if (!s.valid[m]) continue;
+    row[s.asset[m]] = s.P[m];
+    row[p.A + 1 + s.asset[m]] = (s.L[m] * s.P[m]) / eq;
+  }
+  if (ls == 0) {
+    row[p.A] = (cash - q.b) / eq;
+    p.ring_ts[(size_t)env * p.W + head] = ts;
+  }
+}
+
+// Env::reset (+ agent preprocessor reset) for one env, in registers.
+template <int M, int S>
+__device__ __forceinline__ void env_reset(Lane<M>& s, const KParams& p, int env, int ls,
+                                          double& cash, uint64_t& ts, int32_t& head, int32_t& len) {
+  src_reset<M>(s, p);
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    s.L[m] = 0.;
+    s.mep[m] = 0.;
+    s.Bm[m] = 0.;
+  }
+  cash = p.init_cash;
+  gen_tick<M>(s, p, env, ts);
+  ts += 1;
+  if (p.W > 0) {
+    len = 0;
+    head = p.W - 1;
+    ring_push<M, S>(s, p, env, ls, cash, ts, head, len);
+    while (len < p.W) {
+      gen_tick<M>(s, p, env, ts);
+      ts += 1;
+      ring_push<M, S>(s, p, env, ls, cash, ts, head, len);
+    }
+  }
+}
+
+template <int M>
+__device__ __forceinline__ void load_lane(Lane<M>& s, const KParams& p, int env, int ls) {
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int a = ls * M + m;
+    s.asset[m] = a;
+    s.valid[m] = a < p.A;
+    if (s.valid[m]) {
+      const size_t i = (size_t)env * p.A + a;
+      s.L[m] = p.L[i];
+      s.mep[m] = p.mep[i];
+      s.Bm[m] = p.Bm[i];
+      s.P[m] = p.P[i];
+      s.sx[m] = p.sx[i];
+      s.oum[m] = p.oum[i];
+      s.dy[m] = p.dy[i];
+      s.tlen[m] = p.tlen[i];
+      s.tfl[m] = p.tfl[i];
+      s.kind[m] = p.src[a].kind;
+    } else {
+      s.L[m] = s.mep[m] = s.Bm[m] = s.P[m] = s.sx[m] = s.oum[m] = s.dy[m] = 0.;
+      s.tlen[m] = 0;
+      s.tfl[m] = 0;
+      s.kind[m] = -1;
+    }
+  }
+}
+
+template <int M>
+__device__ __forceinline__ void store_lane(const Lane<M>& s, const KParams& p, int env) {
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    if (!s.valid[m]) continue;
+    const size_t i = (size_t)env * p.A + s.asset[m];
+    p.L[i] = s.L[m];
+    p.mep[i] = s.mep[m];
+    p.Bm[i] = s.Bm[m];
+    p.P[i] = s.P[m];
+    p.sx[i] = s.sx[m];
+    p.oum[i] = s.oum[m];
+    p.dy[i] = s.dy[m];
+    p.tlen[i] = s.tlen[m];
+    p.tfl[i] = s.tfl[m];
+  }
+}
+
+// input selector
+enum { IN_NONE = 0, IN_UNITS = 1, IN_SINGLE = 2, IN_DISCRETE = 3 };
+
+__device__ __forceinline__ double dsr_one(double r, double A, double B) {
+  const double dA = r - A;
+  const double dB = r * r - B;
+  const double t = B - A * A;
+  return (B * dA - (A * dB) / 2) / (pow(t * t, 3.0 / 4.0) + 1.1920928955078125e-07);
+}
+__device__ __forceinline__ double ddr_one(double r, double A, double B) {
+  if (r > 0.) return (r - A / 2) / (sqrt(B) + 1.1920928955078125e-07);
+  return (B * (r - A / 2) - (A * (r * r)) / 2) / (pow(B, 3.0 / 2.0) + 1.1920928955078125e-07);
+}
+__device__ __forceinline__ double clip1(double v) { return v < -1. ? -1. : (v > 1. ? 1. : v); }
+
+// one shaper evaluation + parameter update, n = 1 (nstep_buffer.py:62-91, :128-162)
+__device__ __forceinline__ double shape(int shaper, double r, double& A, double& B, double eta,
+                                        double cos_term) {
+  if (shaper == MGN_SHAPER_DSR) {
+    const double out = clip1((0.0 + 1.0 * dsr_one(r, A, B)) / 1);
+    A += eta * (r - A);
+    B += eta * (r * r - B);
+    return out;
+  }
+  if (shaper == MGN_SHAPER_DDR) {
+    const double out = clip1((0.0 + 1.0 * ddr_one(r, A, B)) / 1);
+    double m = r < 0. ? r : 0.;
+    if (r != r) m = r;
+    A += eta * (r - A);
+    B += eta * (m * m - B);
+    return out;
+  }
+  if (shaper == MGN_SHAPER_PPC) return 1.0 * (r + cos_term);
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// The fused step kernel: K consecutive Env steps per launch, state held in
+// registers between steps.  in_kind selects Env::step() / step(units) /
+// step(assetIdx, units) / discrete actions via action_to_transaction.
+template <int M, int S>
+__global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_kind,
+                                                const double* __restrict__ units_in,
+                                                const int32_t* __restrict__ aidx_in,
+                                                const int8_t* __restrict__ act_in, int K) {
+  constexpr int EPB = BLOCK / S;  // envs per block
+  const int tid = threadIdx.x;
+  const int ls = tid % S;
+  const int env = blockIdx.x * EPB + tid / S;
+  if (env >= p.N) return;
+  const int seg_base = (int)(__lane_id()) - ls;
+  const int A = p.A;
+  const int D = p.D;
+
+  Lane<M> s;
+  load_lane<M>(s, p, env, ls);
+  double cash = p.cash[env];
+  uint64_t ts = p.ts[env];
+  double shA[M], shB[M];  // shaper state: slot values for D==A, [0] for D==1
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    if (D == 1) {
+      shA[m] = p.sA[env];
+      shB[m] = p.sB[env];
+    } else {
+      shA[m] = s.valid[m] ? p.sA[(size_t)env * A + s.asset[m]] : 0.;
+      shB[m] = s.valid[m] ? p.sB[(size_t)env * A + s.asset[m]] : 0.;
+    }
+  }
+  double ep_ret = p.ep[(size_t)env * 2], ep_len = p.ep[(size_t)env * 2 + 1];
+  int32_t head = 0, len = 0;
+  if (p.W > 0) {
+    head = p.rhead[env];
+    len = p.rlen[env];
+  }
+  // PPC target norm: entry 0 + canonical tree over the assets
+  double cos_qn = 0.;
+  if (p.shaper == MGN_SHAPER_PPC) {
+    double qq[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const double q = s.valid[m] ? p.target[1 + s.asset[m]] : 0.;
+      qq[m] = q * q;
+    }
+    cos_qn = sqrt(p.target[0] * p.target[0] + canon<M, S>(qq));
+  }
+
+  for (int k = 0; k < K; ++k) {
+    const size_t oN = (size_t)k * p.N, oNA = (size_t)k * p.N * A;
+    // ---- action -> units for this lane's slots
+    double uc[M];
+    Sums s0 = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
+    const double prevEq = (cash + s0.lp) - s0.b;  // Env.h:208
+    if (in_kind == IN_DISCRETE) {                  // dqn.py:160-179
+      const double avM = ((cash + s0.sh) + (s0.lp - s0.ml)) / p.reqM;
+      const int half = p.atoms / 2;
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        uc[m] = 0.;
+        if (!s.valid[m]) continue;
+        const int a = act_in[oNA + (size_t)env * A + s.asset[m]];
+        const double u = p.unit_size * avM / s.P[m];
+        uc[m] = (double)(a - half) * u;
+        if (a == 0) uc[m] = (s.L[m] != 0) ? -s.L[m] : 0.;
+      }
+    } else if (in_kind == IN_UNITS) {
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        uc[m] = s.valid[m] ? units_in[oNA + (size_t)env * A + s.asset[m]] : 0.;
+    } else if (in_kind == IN_SINGLE) {
+      const int ai = aidx_in[env];
+      const double u = units_in[oN + env];
+#pragma unroll
+      for (int m = 0; m < M; ++m) uc[m] = (s.valid[m] && s.asset[m] == ai) ? u : 0.;
+    } else {
+#pragma unroll
+      for (int m = 0; m < M; ++m) uc[m] = 0.;
+    }
+    double prevVal[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) prevVal[m] = s.L[m] * s.P[m];
+
+    // ---- Broker::handleTransaction(units): serial rounds over assets
+    double tp[M], tu[M], tc[M];
+    int rk[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      tp[m] = 0.;
+      tu[m] = 0.;
+      tc[m] = 0.;
+      rk[m] = MGN_GREEN;
+    }
+    for (int j = 0; j < S; ++j) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const int i = j * M + m;
+        if (i >= A) break;
+        const bool act = (ls == j) && (uc[m] != 0.);
+        if (__ballot(act) == 0) continue;
+        const Sums q = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
+        const double pnl = q.lp - q.ml;
+        const double balance = cash + q.sh;
+        const double availM = (balance + pnl) / p.reqM;
+        if (act) {
+          const double u = uc[m];
+          const double cur = s.L[m];
+          const double price = s.P[m];
+          int risk;  // Portfolio::checkRisk(i, u), Portfolio.cpp:254-279
+          if (signbit(u) != signbit(cur)) {
+            risk = MGN_GREEN;
+            if (u > -1 * cur) {
+              const double excess = u + cur;
+              if (availM <= fabs(price * excess) || balance <= 0.) risk = MGN_INSUFF_MARGIN;
+            }
+          } else {
+            const double equity = (cash + q.lp) - q.b;
+            const double mr = p.mainM * pnl;
+            if ((equity <= -mr) || ((balance + pnl) <= -mr)) risk = MGN_MARGIN_CALL;
+            else if (availM <= fabs(price * u) || balance <= 0.) risk = MGN_INSUFF_MARGIN;
+            else risk = MGN_GREEN;
+          }
+          rk[m] = risk;
+          if (risk == MGN_GREEN) {  // Broker.cpp:128-135
+            const double slippage = (price * p.slip_rel) + p.slip_abs;
+            const double tprice = u < 0 ? (price - slippage) : (price + slippage);
+            const double tcost = fabs(u * price) * p.tc_rel + p.tc_abs;
+            // Portfolio::handleTransaction, Portfolio.cpp:284-323
+            double units = u;
+            double cu = cur;
+            double me = s.mep[m];
+            if (signbit(cu) != signbit(units)) {
+              if (fabs(units) > fabs(cu)) {
+                units += cu;
+                cash += cu * tprice;
+                cu = 0.;
+                me = tprice;
+              }
+            } else {
+              me += (tprice - me) * (units / (units + cu));
+            }
+            const double amt = tprice * units;
+            const double use = amt * p.reqM;
+            const double brw = amt - use;
+            double bm = s.Bm[m];
+            bm += brw;
+            cash -= (use + tcost);
+            cu += units;
+            if (fabs(cu) < 0.000001) {
+              me = 0.;
+              if (bm > 0.) {
+                cash -= bm;
+                bm = 0.;
+              }
+            }
+            if (bm < 0.) {
+              cash -= bm;
+              bm = 0.;
+            }
+            s.L[m] = cu;
+            s.mep[m] = me;
+            s.Bm[m] = bm;
+            tp[m] = tprice;
+            tu[m] = u;
+            tc[m] = tcost;
+          }
+        }
+        cash = __shfl(cash, seg_base + j, 64);
+      }
+    }
+    // BrokerResponse.marginCall (Broker.cpp:156-157)
+    int mcall = 0;
+    if (in_kind != IN_NONE) {
+      const Sums q = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
+      mcall = margin_call(q, cash, p.mainM) ? 1 : 0;
+    }
+
+    // ---- dataSource->getData()
+    gen_tick<M>(s, p, env, ts);
+    ts += 1;
+
+    // ---- reward / done (Env.h:211-223)
+    const Sums q = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
+    const double curEq = (cash + q.lp) - q.b;
+    const double ratio = curEq / prevEq;
+    const double clampv = (in_kind == IN_SINGLE) ? 0.01 : 0.3;
+    const double reward = log((ratio < clampv) ? clampv : ratio);
+    int bad = 0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) bad |= (rk[m] != MGN_GREEN && rk[m] != MGN_INSUFF_MARGIN) ? 1 : 0;
+    bad = seg_or<S>(bad);
+    const bool done = bad || margin_call(q, cash, p.mainM) || (curEq < 0.1 * p.init_cash);
+
+    // ---- State.portfolio = ledgerNormedFull (Portfolio.cpp:150-155)
+    const double port0 = (cash - q.b) / curEq;
+    double portA[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) portA[m] = (s.L[m] * s.P[m]) / curEq;
+
+    // ---- agent-side per-asset reward (offpolicy_q.py:152-164)
+    double ar[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      if (!s.valid[m]) {
+        ar[m] = 0.;
+        continue;
+      }
+      double v = (((s.L[m] * s.P[m]) - prevVal[m]) - (tu[m] * tp[m] + tc[m])) / prevEq;
+      v += 1;
+      v = (v < .35) ? .35 : v;
+      ar[m] = log(v);
+    }
+    // ---- reward shaping
+    double cos_term = 0.;
+    if (p.shaper == MGN_SHAPER_PPC) {
+      double pp[M], pq[M];
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const double qv = s.valid[m] ? p.target[1 + s.asset[m]] : 0.;
+        const double pv = s.valid[m] ? portA[m] : 0.;
+        pp[m] = pv * pv;
+        pq[m] = pv * qv;
+      }
+      const double np_ = sqrt(port0 * port0 + canon<M, S>(pp));
+      const double dot = port0 * p.target[0] + canon<M, S>(pq);
+      cos_term = p.cos_temp * (dot / (np_ * cos_qn));
+    }
+    double shaped_s = 0., rin_s = 0.;
+    double shaped_v[M];
+    if (D == 1) {
+      rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
+      shaped_s = shape(p.shaper, rin_s, shA[0], shB[0], p.eta, cos_term);
+    } else {
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        shaped_v[m] = s.valid[m] ? shape(p.shaper, ar[m], shA[m], shB[m], p.eta, cos_term) : 0.;
+    }
+
+    // ---- outputs
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      if (!s.valid[m]) continue;
+      const size_t i = oNA + (size_t)env * A + s.asset[m];
+      if (out.obs_price) out.obs_price[i] = s.P[m];
+      if (out.tprice) out.tprice[i] = tp[m];
+      if (out.tunits) out.tunits[i] = tu[m];
+      if (out.tcost) out.tcost[i] = tc[m];
+      if (out.risk) out.risk[i] = (uint8_t)rk[m];
+      if (out.obs_port) out.obs_port[(size_t)k * p.N * (A + 1) + (size_t)env * (A + 1) + 1 + s.asset[m]] = portA[m];
+      if (D != 1) {
+        if (out.agent_reward) out.agent_reward[i] = ar[m];
+        if (out.shaped) out.shaped[i] = shaped_v[m];
+      }
+    }
+    if (ls == 0) {
+      if (out.reward) out.reward[oN + env] = reward;
+      if (out.done) out.done[oN + env] = done ? 1 : 0;
+      if (out.timestamp) out.timestamp[oN + env] = ts;
+      if (out.margin_call) out.margin_call[oN + env] = (uint8_t)mcall;
+      if (out.obs_port) out.obs_port[(size_t)k * p.N * (A + 1) + (size_t)env * (A + 1)] = port0;
+      if (D == 1) {
+        if (out.agent_reward) out.agent_reward[oN + env] = rin_s;
+        if (out.shaped) out.shaped[oN + env] = shaped_s;
+      }
+    }
+
+    // ---- episode statistics
+    ep_ret += reward;
+    ep_len += 1;
+    if (done) {
+      if (ls == 0) {
+        double* st = p.epstats + (size_t)env * 4;
+        st[0] = ep_ret;
+        st[1] = ep_len;
+        st[2] = curEq;
+        st[3] = st[3] + 1;
+      }
+      ep_ret = 0;
+      ep_len = 0;
+    }
+    // ---- window + auto reset
+    if (p.W > 0) ring_push<M, S>(s, p, env, ls, cash, ts, head, len);
+    if (done && p.auto_reset) env_reset<M, S>(s, p, env, ls, cash, ts, head, len);
+  }
+
+  // ---- write back state
+  store_lane<M>(s, p, env);
+  if (ls == 0) {
+    p.cash[env] = cash;
+    p.ts[env] = ts;
+    p.ep[(size_t)env * 2] = ep_ret;
+    p.ep[(size_t)env * 2 + 1] = ep_len;
+    if (p.W > 0) {
+      p.rhead[env] = head;
+      p.rlen[env] = len;
+    }
+    if (D == 1) {
+      p.sA[env] = shA[0];
+      p.sB[env] = shB[0];
+    }
+  }
+  if (D != 1) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      if (!s.valid[m]) continue;
+      p.sA[(size_t)env * A + s.asset[m]] = shA[m];
+      p.sB[(size_t)env * A + s.asset[m]] = shB[m];
+    }
+  }
+}
+
+// Env constructor (mode 0: initMembers + initAccountants) or Env::reset for
+// masked envs (mode 1), Env.h:139-187.
+template <int M, int S>
+__global__ __launch_bounds__(BLOCK) void k_init_reset(KParams p, int mode,
+                                                      const uint8_t* __restrict__ mask) {
+  constexpr int EPB = BLOCK / S;
+  const int tid = threadIdx.x;
+  const int ls = tid % S;
+  const int env = blockIdx.x * EPB + tid / S;
+  if (env >= p.N) return;
+  if (mode == 1 && mask && !mask[env]) return;
+  Lane<M> s;
+  double cash;
+  uint64_t ts;
+  int32_t head = 0, len = 0;
+  if (mode == 0) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int a = ls * M + m;
+      s.asset[m] = a;
+      s.valid[m] = a < p.A;
+      s.L[m] = s.mep[m] = s.Bm[m] = s.P[m] = s.sx[m] = s.oum[m] = s.dy[m] = 0.;
+      s.tlen[m] = 0;
+      s.tfl[m] = 0;
+      s.kind[m] = s.valid[m] ? p.src[a].kind : -1;
+      if (!s.valid[m]) continue;
+      const double* q = p.src[a].p;
+      if (s.kind[m] == MGN_SRC_SINE) s.sx[m] = q[3];
+      else if (s.kind[m] == MGN_SRC_OU) s.P[m] = q[0];
+      else if (s.kind[m] == MGN_SRC_TRENDOU) {
+        s.P[m] = q[5];
+        s.oum[m] = q[5];
+      }
+    }
+    ts = 0;
+    cash = p.init_cash;
+    gen_tick<M>(s, p, env, ts);  // initAccountants' getData (Env.h:160)
+    ts += 1;
+    if (ls == 0) {
+      p.ep[(size_t)env * 2] = 0.;
+      p.ep[(size_t)env * 2 + 1] = 0.;
+      for (int f = 0; f < 4; ++f) p.epstats[(size_t)env * 4 + f] = 0.;
+      if (p.W > 0) {
+        p.rhead[env] = p.W - 1;
+        p.rlen[env] = 0;
+      }
+    }
+  } else {
+    load_lane<M>(s, p, env, ls);
+    cash = p.cash[env];
+    ts = p.ts[env];
+    if (p.W > 0) {
+      head = p.rhead[env];
+      len = p.rlen[env];
+    }
+    env_reset<M, S>(s, p, env, ls, cash, ts, head, len);
+    if (ls == 0 && p.W > 0) {
+      p.rhead[env] = head;
+      p.rlen[env] = len;
+    }
+  }
+  store_lane<M>(s, p, env);
+  if (ls == 0) {
+    p.cash[env] = cash;
+    p.ts[env] = ts;
+  }
+}
+
+// Portfolio accessors (Portfolio.cpp:170-252) for every env, same canonical
+// sums as the step: out (N, 10) = {cash, equity, pnl, balance, availableMargin,
+// usedMargin, borrowedMargin, borrowedAssetValue, assetValue, checkRisk}.
+template <int M, int S>
+__global__ __launch_bounds__(BLOCK) void k_valuation(KParams p, double* __restrict__ out) {
+  constexpr int EPB = BLOCK / S;
+  const int tid = threadIdx.x;
+  const int ls = tid % S;
+  const int env = blockIdx.x * EPB + tid / S;
+  if (env >= p.N) return;
+  Lane<M> s;
+  load_lane<M>(s, p, env, ls);
+  const double cash = p.cash[env];
+  const Sums q = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
+  double tu[M], tb[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    tu[m] = fabs(s.L[m]) * s.mep[m];                       // :199-201
+    const double mask = (s.L[m] < 0.) ? 1.0 : 0.0;
+    tb[m] = s.L[m] * (s.P[m] * mask);                      // :219-223
+  }
+  const double used = p.reqM * canon<M, S>(tu);
+  const double bav = canon<M, S>(tb);
+  if (ls != 0) return;
+  const double pnl = q.lp - q.ml;
+  const double balance = cash + q.sh;
+  double* o = out + (size_t)env * 10;
+  o[0] = cash;
+  o[1] = (cash + q.lp) - q.b;
+  o[2] = pnl;
+  o[3] = balance;
+  o[4] = (balance + pnl) / p.reqM;
+  o[5] = used;
+  o[6] = q.b;
+  o[7] = bav;
+  o[8] = q.lp;
+  o[9] = margin_call(q, cash, p.mainM) ? (double)MGN_MARGIN_CALL : (double)MGN_GREEN;
+}
+
+// ---------------------------------------------------------------------------
+// Window kernels (StackerDiscrete, preprocessor.py:143-199).  Ring layout
+// (N, W, C) with C = F + P columns (price features then portfolio entries).
+struct RingDesc {
+  int N, F, Pn, W, norm;
+  double* ring;
+  uint64_t* ring_ts;
+  int32_t* head;
+  int32_t* len;
+};
+
+// stream_state: one thread per env (rare; the fused step writes its own rows)
+__global__ void k_ring_push(RingDesc r, const double* __restrict__ price,
+                            const double* __restrict__ port, const uint64_t* __restrict__ ts) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= r.N) return;
+  const int C = r.F + r.Pn;
+  const int h = (r.head[env] + 1) % r.W;
+  double* row = r.ring + ((size_t)env * r.W + h) * C;
+  for (int c = 0; c < r.F; ++c) row[c] = price ? price[(size_t)env * r.F + c] : 0.;
+  for (int c = 0; c < r.Pn; ++c) row[r.F + c] = port ? port[(size_t)env * r.Pn + c] : 0.;
+  r.ring_ts[(size_t)env * r.W + h] = ts ? ts[env] : 0;
+  r.head[env] = h;
+  if (r.len[env] < r.W) r.len[env] += 1;
+}
+
+__global__ void k_ring_clear(RingDesc r, const uint8_t* __restrict__ mask) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= r.N) return;
+  if (mask && !mask[env]) return;
+  r.head[env] = r.W - 1;
+  r.len[env] = 0;
+}
+
+// current_data: one thread per (env, column); rows oldest -> newest, norm on
+// price columns (log_norm :79-81, lookback :63-66, standard_norm :83-92).
+__global__ __launch_bounds__(BLOCK) void k_ring_gather(RingDesc r, double* __restrict__ price_out,
+                                                       double* __restrict__ port_out,
+                                                       uint64_t* __restrict__ ts_out) {
+  const int C = r.F + r.Pn;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (int64_t)r.N * C) return;
+  const int env = (int)(gid / C);
+  const int c = (int)(gid % C);
+  const int W = r.W;
+  const int len = r.len[env];
+  const int hd = r.head[env];
+  const double* base = r.ring + (size_t)env * W * C;
+  auto row_of = [&](int w) { return (hd - (len - 1) + w + 2 * W) % W; };
+  if (c >= r.F) {
+    const int pc = c - r.F;
+    if (port_out)
+      for (int w = 0; w < W; ++w)
+        port_out[((size_t)env * W + w) * r.Pn + pc] = (w < len) ? base[(size_t)row_of(w) * C + c] : 0.;
+    return;
+  }
+  if (c == 0 && ts_out)
+    for (int w = 0; w < W; ++w)
+      ts_out[(size_t)env * W + w] = (w < len) ? r.ring_ts[(size_t)env * W + row_of(w)] : 0;
+  if (!price_out) return;
+  double* o = price_out + (size_t)env * W * r.F + c;
+  const int nt = r.norm;
+  if (nt == MGN_NORM_STANDARD_NORMAL) {
+    double sum = 0.;
+    for (int w = 0; w < len; ++w) sum += base[(size_t)row_of(w) * C + c];
+    const double mean = sum / len;
+    double ss = 0.;
+    for (int w = 0; w < len; ++w) {
+      const double d = base[(size_t)row_of(w) * C + c] - mean;
+      ss += d * d;
+    }
+    const double sd = sqrt(ss / len);
+    for (int w = 0; w < W; ++w) {
+      double v = 0.;
+      if (w < len) {
+        v = (base[(size_t)row_of(w) * C + c] - mean) / sd;
+        if (v != v) v = 0.;
+        else if (v == __builtin_inf()) v = 1.7976931348623157e308;
+        else if (v == -__builtin_inf()) v = -1.7976931348623157e308;
+      }
+      o[(size_t)w * r.F] = v;
+    }
+    return;
+  }
+  const double last = (len > 0) ? base[(size_t)row_of(len - 1) * C + c] : 1.;
+  for (int w = 0; w < W; ++w) {
+    double v = 0.;
+    if (w < len) {
+      v = base[(size_t)row_of(w) * C + c];
+      if (nt == MGN_NORM_LOG) v = log((v < 1e-5) ? 1e-5 : v);
+      else if (nt == MGN_NORM_LOOKBACK) v = v / last;
+      else if (nt == MGN_NORM_LOOKBACK_LOG) v = log(v / last);
+    }
+    o[(size_t)w * r.F] = v;
+  }
+}
+
+// Philox discrete actions U{0..atoms-1}: counter (k, env, asset, 0xAC7)
+__global__ void k_gen_actions(int8_t* __restrict__ out, int K, int N, int A, int atoms,
+                              uint64_t seed, int64_t env_offset) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)K * N * A;
+  if (gid >= total) return;
+  const int a = (int)(gid % A);
+  const int64_t ke = gid / A;
+  const int env = (int)(ke % N);
+  const uint32_t k = (uint32_t)(ke / N);
+  const u4 x = philox4x32_10(k, (uint32_t)(env_offset + env), (uint32_t)a, 0xAC7u, (uint32_t)seed,
+                             (uint32_t)(seed >> 32));
+  out[gid] = (int8_t)(((uint64_t)x.x * (uint32_t)atoms) >> 32);
+}
+
+}  // namespace mgn

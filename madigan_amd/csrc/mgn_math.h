@@ -1,0 +1,170 @@
+// mgn_math.h -- device-side RNG and deterministic math for the generators.
+//
+// The reference draws its noise from std::default_random_engine seeded with
+// the wall clock (madigan/environments/cpp/DataSource.cpp:472, :1131, :1407),
+// so its streams cannot be replayed.  This framework's variates are a fixed
+// specification instead: Philox4x32-10 keyed by (seed), counter
+// (tick, env, asset|slot<<16), Box-Muller on 53-bit uniforms, with fdlibm's
+// log/sin/cos kernels evaluated in plain IEEE binary64 (compiled with
+// -ffp-contract=off) so every host restatement reproduces the device bits.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mgn {
+
+__device__ __forceinline__ double bits_to_d(uint64_t u) { return __longlong_as_double((long long)u); }
+__device__ __forceinline__ uint64_t d_to_bits(double d) { return (uint64_t)__double_as_longlong(d); }
+
+struct u4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ u4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                            uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c0;
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0;
+    const uint32_t n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return u4{c0, c1, c2, c3};
+}
+
+// two 53-bit integers from one Philox block
+__device__ __forceinline__ void draw53(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot,
+                                       uint64_t tick, uint64_t& a, uint64_t& b) {
+  const u4 x = philox4x32_10((uint32_t)tick, (uint32_t)env, asset | (slot << 16),
+                             (uint32_t)(tick >> 32) ^ (uint32_t)(env >> 32), (uint32_t)seed,
+                             (uint32_t)(seed >> 32));
+  a = (((uint64_t)x.y << 32) | x.x) >> 11;
+  b = (((uint64_t)x.w << 32) | x.z) >> 11;
+}
+
+constexpr double TWO_M53 = 1.1102230246251565404e-16;
+
+__device__ __forceinline__ void uniform2(uint64_t seed, uint64_t env, uint32_t asset,
+                                         uint32_t slot, uint64_t tick, double& u0, double& u1) {
+  uint64_t a, b;
+  draw53(seed, env, asset, slot, tick, a, b);
+  u0 = (double)a * TWO_M53;
+  u1 = (double)b * TWO_M53;
+}
+
+// fdlibm e_log.c, normal positive arguments
+__device__ __forceinline__ double det_log(double x) {
+  const double ln2_hi = bits_to_d(0x3fe62e42fee00000ull);
+  const double ln2_lo = bits_to_d(0x3dea39ef35793c76ull);
+  const double Lg1 = bits_to_d(0x3FE5555555555593ull), Lg2 = bits_to_d(0x3FD999999997FA04ull),
+               Lg3 = bits_to_d(0x3FD2492494229359ull), Lg4 = bits_to_d(0x3FCC71C51D8E78AFull),
+               Lg5 = bits_to_d(0x3FC7466496CB03DEull), Lg6 = bits_to_d(0x3FC39A09D078C69Full),
+               Lg7 = bits_to_d(0x3FC2F112DF3E5244ull);
+  const uint64_t ix = d_to_bits(x);
+  int32_t hx = (int32_t)(ix >> 32);
+  int32_t k = ((hx >> 20) & 0x7ff) - 1023;
+  hx &= 0x000fffff;
+  const int32_t i = (hx + 0x95f64) & 0x100000;
+  k += (i >> 20);
+  const uint64_t mb = ((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (ix & 0xffffffffull);
+  const double f = bits_to_d(mb) - 1.0;
+  const double s = f / (2.0 + f);
+  const double dk = (double)k;
+  const double z = s * s;
+  const double w = z * z;
+  const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
+__device__ __forceinline__ double k_sin(double x, double y, bool tail) {
+  const double S1 = bits_to_d(0xBFC5555555555549ull), S2 = bits_to_d(0x3F8111111110F8A6ull),
+               S3 = bits_to_d(0xBF2A01A019C161D5ull), S4 = bits_to_d(0x3EC71DE357B1FE7Dull),
+               S5 = bits_to_d(0xBE5AE5E68A2B9CEBull), S6 = bits_to_d(0x3DE5D93A5ACFD57Cull);
+  const double z = x * x;
+  const double v = z * x;
+  const double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+  if (!tail) return x + v * (S1 + z * r);
+  return x - ((z * (0.5 * y - v * r) - y) - v * S1);
+}
+
+__device__ __forceinline__ double k_cos(double x, double y) {
+  const double C1 = bits_to_d(0x3FA555555555554Cull), C2 = bits_to_d(0xBF56C16C16C15177ull),
+               C3 = bits_to_d(0x3EFA01A019CB1590ull), C4 = bits_to_d(0xBE927E4F809C52ADull),
+               C5 = bits_to_d(0x3E21EE9EBDB4B1C4ull), C6 = bits_to_d(0xBDA8FAE9BE8838D4ull);
+  const double z = x * x;
+  const double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+  const double hz = 0.5 * z;
+  const double w = 1.0 - hz;
+  return w + (((1.0 - w) - hz) + (z * r - x * y));
+}
+
+// cos(2 pi u), u in [0,1)
+__device__ __forceinline__ double det_cos2pi(double u) {
+  const double pio2 = bits_to_d(0x3FF921FB54442D18ull);
+  const double t = 4.0 * u;
+  const double q = floor(t + 0.5);
+  const double f = t - q;
+  const double r = f * pio2;
+  const int iq = ((int)q) & 3;
+  const double c = k_cos(r, 0.0);
+  const double s = k_sin(r, 0.0, false);
+  // branch-free quadrant select (same values as the oracle's switch)
+  double v = (iq & 1) ? s : c;
+  return (iq == 1 || iq == 2) ? -v : v;
+}
+
+// sin(x) with fdlibm's medium Cody-Waite reduction
+__device__ __noinline__ double det_sin(double x) {
+  const double invpio2 = bits_to_d(0x3FE45F306DC9C883ull);
+  const double pio2_1 = bits_to_d(0x3FF921FB54400000ull), pio2_1t = bits_to_d(0x3DD0B4611A626331ull);
+  const double pio2_2 = bits_to_d(0x3DD0B4611A600000ull), pio2_2t = bits_to_d(0x3BA3198A2E037073ull);
+  const double pio2_3 = bits_to_d(0x3BA3198A2E000000ull), pio2_3t = bits_to_d(0x397B839A252049C1ull);
+  const double ax = fabs(x);
+  if (ax <= 0.78539816339744827900) return k_sin(x, 0.0, false);
+  if (!(ax < __builtin_inf())) return x - x;
+  const double fn = floor(x * invpio2 + 0.5);
+  const int32_t n = (int32_t)(int64_t)fn;
+  double r = x - fn * pio2_1;
+  double w = fn * pio2_1t;
+  double y0 = r - w;
+  const int32_t j = (int32_t)((d_to_bits(x) >> 52) & 0x7ff);
+  int32_t i = j - (int32_t)((d_to_bits(y0) >> 52) & 0x7ff);
+  if (i > 16) {
+    double t = r;
+    w = fn * pio2_2;
+    r = t - w;
+    w = fn * pio2_2t - ((t - r) - w);
+    y0 = r - w;
+    i = j - (int32_t)((d_to_bits(y0) >> 52) & 0x7ff);
+    if (i > 49) {
+      t = r;
+      w = fn * pio2_3;
+      r = t - w;
+      w = fn * pio2_3t - ((t - r) - w);
+      y0 = r - w;
+    }
+  }
+  const double y1 = (r - y0) - w;
+  const int q = n & 3;
+  const double v = (q & 1) ? k_cos(y0, y1) : k_sin(y0, y1, true);
+  return (q >= 2) ? -v : v;
+}
+
+// standard normal: Box-Muller on one Philox block
+__device__ __forceinline__ double normal(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot,
+                                         uint64_t tick) {
+  uint64_t a, b;
+  draw53(seed, env, asset, slot, tick, a, b);
+  const double u1 = (double)(a + 1) * TWO_M53;
+  const double u2 = (double)b * TWO_M53;
+  return sqrt(-2.0 * det_log(u1)) * det_cos2pi(u2);
+}
+
+}  // namespace mgn

@@ -1,0 +1,804 @@
+"""Batched MI355X environments and the drop-in ``Env`` (N = 1 view).
+
+``BatchedEnv`` owns one handle of the C ABI: N independent envs whose state
+lives in HBM (struct-of-arrays, env-major) and which one HIP launch advances by
+one step (``step``) or K steps (``rollout``).  Outputs are device tensors that
+alias the handle's buffers (valid until the next launch), mirroring the
+reference's zero-copy property views (madigan/environments/cpp/env.cpp:897-913).
+
+``Env`` keeps the reference's Python surface (env.cpp:843-1005,
+madigan/environments/__init__.py) for one environment: ``reset()``,
+``step()``, ``step(units)``, ``step(assetIdx, units)``, ``step(assetCode,
+units)`` and the property accessors, returning host numpy values exactly like
+the pybind11 module did.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from collections import namedtuple
+from typing import Any, Optional
+
+import numpy as np
+
+from . import _lib as L
+from .config import SourceSpec, build_config, default_spec, spec_from_config
+
+RISK_NAMES = {L.GREEN: "green", L.INSUFF_MARGIN: "insuff_margin", L.MARGIN_CALL: "margin_call",
+              L.BLOWN_OUT: "blown_out"}
+
+VALUATION_FIELDS = ("cash", "equity", "pnl", "balance", "availableMargin", "usedMargin",
+                    "borrowedMargin", "borrowedAssetValue", "assetValue", "checkRisk")
+
+StepOutput = namedtuple("StepOutput", ["reward", "done", "obs_price", "obs_port", "timestamp",
+                                       "tprice", "tunits", "tcost", "risk", "margin_call",
+                                       "shaped", "agent_reward"])
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class RiskInfo(int):
+    """RiskInfo enum (DataTypes.h:70-75) with the pybind11 names."""
+    green = L.GREEN
+    insuff_margin = L.INSUFF_MARGIN
+    margin_call = L.MARGIN_CALL
+    blown_out = L.BLOWN_OUT
+
+    def __repr__(self):
+        return f"RiskInfo.{RISK_NAMES.get(int(self), int(self))}"
+
+    __str__ = __repr__
+
+
+for _v, _n in RISK_NAMES.items():
+    setattr(RiskInfo, _n, RiskInfo(_v))
+
+
+class State:
+    """State{price, portfolio, timestamp} (DataTypes.h:52-63)."""
+    __slots__ = ("price", "portfolio", "timestamp")
+
+    def __init__(self, price, portfolio, timestamp):
+        self.price = price
+        self.portfolio = portfolio
+        self.timestamp = timestamp
+
+    def __iter__(self):
+        return iter((self.price, self.portfolio, self.timestamp))
+
+    def __repr__(self):
+        return f"State(price={self.price!r}, portfolio={self.portfolio!r}, timestamp={self.timestamp!r})"
+
+
+class BrokerResponse:
+    """BrokerResponse<T> (DataTypes.h:103-135)."""
+
+    def __init__(self, transactionPrice, transactionUnits, transactionCost, riskInfo, marginCall,
+                 timestamp=0, event=""):
+        self.transactionPrice = transactionPrice
+        self.transactionUnits = transactionUnits
+        self.transactionCost = transactionCost
+        self.riskInfo = riskInfo
+        self.marginCall = marginCall
+        self.timestamp = timestamp
+        self.event = event
+
+    def __repr__(self):
+        return (f"timestamp:        {self.timestamp}\ntransactionPrice: \n{self.transactionPrice}\n"
+                f"transactionUnits:  \n{self.transactionUnits}\ntransactionCost:  \n"
+                f"{self.transactionCost}\nriskInfo:         \n{self.riskInfo}\nmarginCall:         \n"
+                f"{self.marginCall}\n")
+
+
+class EnvInfo:
+    """EnvInfo<T> (DataTypes.h:141-149)."""
+
+    def __init__(self, brokerResponse=None, dataEnd=False):
+        self.brokerResponse = brokerResponse
+        self.dataEnd = dataEnd
+
+
+class Asset:
+    def __init__(self, code):
+        self.code = code
+
+    def __repr__(self):
+        return self.code
+
+    def __eq__(self, other):
+        return getattr(other, "code", other) == self.code
+
+    def __hash__(self):
+        return hash(self.code)
+
+
+class BatchedEnv:
+    """N independent madigan Envs on one GPU (one handle of the C ABI)."""
+
+    def __init__(self, spec: SourceSpec, n_envs: int, *, device=None, seed: int = 0,
+                 env_offset: int = 0, init_cash: float = 1_000_000.0,
+                 required_margin: float = 0.0, maintenance_margin: float = 0.0,
+                 slippage_rel: float = 0.0, slippage_abs: float = 0.0,
+                 transaction_cost_rel: float = 0.0, transaction_cost_abs: float = 0.0,
+                 reward_shaper=None, reward_mode: str = "env_log",
+                 adaptation_rate: float = 0.001, cosine_temp: float = 0.0,
+                 desired_portfolio=None, window: int = 0, norm_type=None,
+                 auto_reset: bool = False, action_atoms: int = 3, unit_size: float = 0.05):
+        torch = _torch()
+        self.lib = L.load()
+        if not torch.cuda.is_available():
+            raise RuntimeError("madigan_amd needs a ROCm GPU (gfx950); there is no CPU fallback")
+        self.device = torch.device(device if device is not None else "cuda")
+        self.spec = spec
+        self.cfg, self._srcs = build_config(
+            spec, n_envs=n_envs, init_cash=init_cash, required_margin=required_margin,
+            maintenance_margin=maintenance_margin, slippage_rel=slippage_rel,
+            slippage_abs=slippage_abs, transaction_cost_rel=transaction_cost_rel,
+            transaction_cost_abs=transaction_cost_abs, reward_shaper=reward_shaper,
+            reward_mode=reward_mode, adaptation_rate=adaptation_rate, cosine_temp=cosine_temp,
+            desired_portfolio=desired_portfolio, window=window, norm_type=norm_type,
+            auto_reset=auto_reset, action_atoms=action_atoms, unit_size=unit_size, seed=seed,
+            env_offset=env_offset)
+        self.N = int(n_envs)
+        self.A = spec.n_assets
+        self.W = int(window)
+        nbytes = self.lib.mgn_arena_bytes(C.byref(self.cfg))
+        if nbytes == 0:
+            raise ValueError("invalid env dimensions")
+        with torch.cuda.device(self.device):
+            self.arena = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            self.stream = torch.cuda.current_stream(self.device)
+        h = C.c_void_p()
+        L.check(self.lib.mgn_create(C.byref(self.cfg), self._srcs, C.c_void_p(self.stream.cuda_stream),
+                                    C.c_void_p(self.arena.data_ptr()), nbytes, C.byref(h)))
+        self.h = h
+        v = L.Views()
+        L.check(self.lib.mgn_get_views(self.h, C.byref(v)), self.h)
+        self._v = v
+        self.D = v.reward_dim
+        self._build_views()
+        self._val = torch.empty((self.N, 10), dtype=torch.float64, device=self.device)
+
+    # ---- tensor views over the arena --------------------------------------
+    def _t(self, ptr, dtype, shape):
+        torch = _torch()
+        if not ptr:
+            return None
+        n = int(np.prod(shape))
+        item = torch.empty((), dtype=dtype).element_size()
+        off = ptr - self.arena.data_ptr()
+        return self.arena[off:off + n * item].view(dtype).view(shape)
+
+    def _build_views(self):
+        torch = _torch()
+        f64, i32, u8, i64 = torch.float64, torch.int32, torch.uint8, torch.int64
+        N, A, W, D, v = self.N, self.A, self.W, self.D, self._v
+        NA = (N, A)
+        Dsh = (N,) if D == 1 else (N, A)
+        self.ledger = self._t(v.ledger, f64, NA)
+        self.mean_entry = self._t(v.mean_entry, f64, NA)
+        self.borrowed = self._t(v.borrowed, f64, NA)
+        self.prices = self._t(v.prices, f64, NA)
+        self.sine_x = self._t(v.sine_x, f64, NA)
+        self.ou_mean = self._t(v.ou_mean, f64, NA)
+        self.trend_dy = self._t(v.trend_dy, f64, NA)
+        self.trend_len = self._t(v.trend_len, i32, NA)
+        self.trend_flags = self._t(v.trend_flags, u8, NA)
+        self.cash = self._t(v.cash, f64, (N,))
+        self.timestamp = self._t(v.timestamp, i64, (N,))
+        self.shaper_a = self._t(v.shaper_a, f64, Dsh)
+        self.shaper_b = self._t(v.shaper_b, f64, Dsh)
+        self.ep_stats = self._t(v.ep_stats, f64, (N, 2))
+        self.episode_stats = self._t(v.episode_stats, f64, (N, 4))
+        self.ext_prices = self._t(v.ext_prices, f64, NA)
+        self.units_buf = self._t(v.units, f64, NA)
+        self.asset_idx_buf = self._t(v.asset_idx, i32, (N,))
+        self.reset_mask_buf = self._t(v.reset_mask, u8, (N,))
+        if W:
+            self.ring = self._t(v.ring, f64, (N, W, 2 * A + 1))
+            self.win_price = self._t(v.win_price, f64, (N, W, A))
+            self.win_port = self._t(v.win_port, f64, (N, W, A + 1))
+            self.win_ts = self._t(v.win_ts, i64, (N, W))
+            self.ring_len = self._t(v.ring_len, i32, (N,))
+        o = v.out
+        self.out = StepOutput(
+            reward=self._t(o.reward, f64, (N,)), done=self._t(o.done, u8, (N,)),
+            obs_price=self._t(o.obs_price, f64, NA), obs_port=self._t(o.obs_port, f64, (N, A + 1)),
+            timestamp=self._t(o.timestamp, i64, (N,)), tprice=self._t(o.tprice, f64, NA),
+            tunits=self._t(o.tunits, f64, NA), tcost=self._t(o.tcost, f64, NA),
+            risk=self._t(o.risk, u8, NA), margin_call=self._t(o.margin_call, u8, (N,)),
+            shaped=self._t(o.shaped, f64, Dsh), agent_reward=self._t(o.agent_reward, f64, Dsh))
+        # the whole step-output block is contiguous in the arena: one D2H copy
+        lo = o.reward - self.arena.data_ptr()
+        hi = o.margin_call - self.arena.data_ptr() + N
+        self._out_span = (lo, hi)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            try:
+                self.lib.mgn_destroy(h)
+            except Exception:
+                pass
+            self.h = None
+
+    # ---- inputs -------------------------------------------------------------
+    def _dev(self, x, dtype, shape, staging):
+        torch = _torch()
+        if isinstance(x, torch.Tensor) and x.device == self.device and x.dtype == dtype \
+                and x.is_contiguous() and tuple(x.shape) == tuple(shape):
+            return x
+        t = torch.as_tensor(np.asarray(x) if not isinstance(x, torch.Tensor) else x)
+        if t.numel() != int(np.prod(shape)):
+            raise ValueError(f"expected {int(np.prod(shape))} values, got {t.numel()}")
+        staging.view(-1)[: t.numel()].copy_(t.reshape(-1).to(dtype), non_blocking=False)
+        return staging.view(-1)[: t.numel()].view(shape)
+
+    # ---- API ------------------------------------------------------------------
+    def set_broker(self, required_margin=None, maintenance_margin=None, slippage_rel=None,
+                   slippage_abs=None, transaction_cost_rel=None, transaction_cost_abs=None):
+        c = self.cfg
+        if required_margin is not None:
+            c.required_margin = float(required_margin)
+        if maintenance_margin is not None:
+            c.maintenance_margin = float(maintenance_margin)
+        if slippage_rel is not None:
+            c.slippage_rel = float(slippage_rel)
+        if slippage_abs is not None:
+            c.slippage_abs = float(slippage_abs)
+        if transaction_cost_rel is not None:
+            c.tc_rel = float(transaction_cost_rel)
+        if transaction_cost_abs is not None:
+            c.tc_abs = float(transaction_cost_abs)
+        L.check(self.lib.mgn_set_broker(self.h, c.required_margin, c.maintenance_margin,
+                                        c.slippage_rel, c.slippage_abs, c.tc_rel, c.tc_abs), self.h)
+
+    def reset(self, mask=None):
+        """Env::reset for every env (mask None) or the masked ones."""
+        torch = _torch()
+        ptr = None
+        if mask is not None:
+            m = self._dev(mask, torch.uint8, (self.N,), self.reset_mask_buf)
+            ptr = C.c_void_p(m.data_ptr())
+        L.check(self.lib.mgn_reset(self.h, ptr), self.h)
+
+    def step(self, units=None, asset_idx=None) -> StepOutput:
+        """Env::step() (units None), step(units (N,A)) or step(asset_idx (N), units (N))."""
+        torch = _torch()
+        if units is None:
+            L.check(self.lib.mgn_step(self.h, L.STEP_NONE, None, None), self.h)
+        elif asset_idx is None:
+            u = self._dev(units, torch.float64, (self.N, self.A), self.units_buf)
+            L.check(self.lib.mgn_step(self.h, L.STEP_UNITS, C.c_void_p(u.data_ptr()), None), self.h)
+        else:
+            u = self._dev(units, torch.float64, (self.N,), self.units_buf)
+            ix = self._dev(asset_idx, torch.int32, (self.N,), self.asset_idx_buf)
+            L.check(self.lib.mgn_step(self.h, L.STEP_SINGLE, C.c_void_p(u.data_ptr()),
+                                      C.c_void_p(ix.data_ptr())), self.h)
+        return self.out
+
+    def alloc_traj(self, k_steps: int, fields=None):
+        """(K, ...) device buffers for rollout outputs (None fields are skipped)."""
+        torch = _torch()
+        K, N, A, D = k_steps, self.N, self.A, self.D
+        shapes = dict(reward=((K, N), torch.float64), agent_reward=(((K, N) if D == 1 else (K, N, A)), torch.float64),
+                      shaped=(((K, N) if D == 1 else (K, N, A)), torch.float64), done=((K, N), torch.uint8),
+                      obs_price=((K, N, A), torch.float64), obs_port=((K, N, A + 1), torch.float64),
+                      timestamp=((K, N), torch.int64), tprice=((K, N, A), torch.float64),
+                      tunits=((K, N, A), torch.float64), tcost=((K, N, A), torch.float64),
+                      risk=((K, N, A), torch.uint8), margin_call=((K, N), torch.uint8))
+        fields = L.TRAJ_FIELDS if fields is None else fields
+        return {k: torch.empty(s, dtype=dt, device=self.device) for k, (s, dt) in shapes.items()
+                if k in fields}
+
+    @staticmethod
+    def _traj_struct(out: dict) -> L.Traj:
+        t = L.Traj()
+        for k in L.TRAJ_FIELDS:
+            v = out.get(k)
+            setattr(t, k, None if v is None else v.data_ptr())
+        return t
+
+    def rollout(self, actions, out: Optional[dict] = None) -> dict:
+        """K fused steps from discrete actions (K,N,A) int8 via action_to_transaction."""
+        torch = _torch()
+        if not (isinstance(actions, torch.Tensor) and actions.device == self.device
+                and actions.dtype == torch.int8 and actions.is_contiguous()):
+            actions = torch.as_tensor(actions).to(self.device, torch.int8).contiguous()
+        if actions.dim() != 3 or actions.shape[1] != self.N or actions.shape[2] != self.A:
+            raise ValueError(f"actions must be (K, {self.N}, {self.A}), got {tuple(actions.shape)}")
+        K = int(actions.shape[0])
+        out = self.alloc_traj(K) if out is None else out
+        t = self._traj_struct(out)
+        L.check(self.lib.mgn_rollout(self.h, C.c_void_p(actions.data_ptr()), K, C.byref(t)), self.h)
+        return out
+
+    def rollout_units(self, units, out: Optional[dict] = None) -> dict:
+        """K fused Env::step(units) from units (K,N,A) fp64."""
+        torch = _torch()
+        u = torch.as_tensor(units).to(self.device, torch.float64).contiguous()
+        K = int(u.shape[0])
+        out = self.alloc_traj(K) if out is None else out
+        t = self._traj_struct(out)
+        L.check(self.lib.mgn_rollout_units(self.h, C.c_void_p(u.data_ptr()), K, C.byref(t)), self.h)
+        return out
+
+    def generate_actions(self, k_steps: int, seed: int = 0x6D6164):
+        torch = _torch()
+        a = torch.empty((k_steps, self.N, self.A), dtype=torch.int8, device=self.device)
+        L.check(self.lib.mgn_generate_actions(self.h, C.c_void_p(a.data_ptr()), k_steps, seed), self.h)
+        return a
+
+    def set_prices(self, prices):
+        torch = _torch()
+        p = self._dev(prices, torch.float64, (self.N, self.A), self.ext_prices)
+        if p.data_ptr() != self.ext_prices.data_ptr():
+            L.check(self.lib.mgn_set_prices(self.h, C.c_void_p(p.data_ptr())), self.h)
+
+    def valuation(self) -> dict:
+        """Portfolio accessors for every env as (N,) device tensors."""
+        L.check(self.lib.mgn_valuation(self.h, C.c_void_p(self._val.data_ptr())), self.h)
+        return {k: self._val[:, i] for i, k in enumerate(VALUATION_FIELDS)}
+
+    def window(self):
+        """StackerDiscrete.current_data of the handle's ring: (N,W,A), (N,W,A+1), (N,W)."""
+        if not self.W:
+            raise RuntimeError("env built with window=0")
+        L.check(self.lib.mgn_window(self.h, None, None, None), self.h)
+        return self.win_price, self.win_port, self.win_ts
+
+    def window_push(self, price=None, port=None, ts=None):
+        ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
+        L.check(self.lib.mgn_window_push(self.h, ptr(price), ptr(port), ptr(ts)), self.h)
+
+    def window_clear(self, mask=None):
+        torch = _torch()
+        ptr = None
+        if mask is not None:
+            m = self._dev(mask, torch.uint8, (self.N,), self.reset_mask_buf)
+            ptr = C.c_void_p(m.data_ptr())
+        L.check(self.lib.mgn_window_clear(self.h, ptr), self.h)
+
+    def synchronize(self):
+        L.check(self.lib.mgn_synchronize(self.h), self.h)
+
+    def host_outputs(self) -> dict:
+        """One D2H copy of the whole step-output block, sliced into numpy arrays."""
+        lo, hi = self._out_span
+        blob = self.arena[lo:hi].cpu().numpy()
+        base = self.arena.data_ptr() + lo
+        N, A, D = self.N, self.A, self.D
+        o = self._v.out
+        def arr(ptr, dtype, shape):  # noqa: E306
+            off = ptr - base
+            n = int(np.prod(shape)) * np.dtype(dtype).itemsize
+            return blob[off:off + n].view(dtype).reshape(shape)
+        Dsh = (N,) if D == 1 else (N, A)
+        return dict(reward=arr(o.reward, np.float64, (N,)), agent_reward=arr(o.agent_reward, np.float64, Dsh),
+                    shaped=arr(o.shaped, np.float64, Dsh), done=arr(o.done, np.uint8, (N,)),
+                    obs_price=arr(o.obs_price, np.float64, (N, A)),
+                    obs_port=arr(o.obs_port, np.float64, (N, A + 1)),
+                    timestamp=arr(o.timestamp, np.uint64, (N,)), tprice=arr(o.tprice, np.float64, (N, A)),
+                    tunits=arr(o.tunits, np.float64, (N, A)), tcost=arr(o.tcost, np.float64, (N, A)),
+                    risk=arr(o.risk, np.uint8, (N, A)), margin_call=arr(o.margin_call, np.uint8, (N,)))
+
+
+# ---------------------------------------------------------------------------
+# Drop-in single Env (pybind11 module surface, env.cpp:843-1005)
+
+
+class DataSourceTick:
+    """Plug-in base class for host data sources (DataSource.h:48-64).
+
+    Subclass and override getData()/currentPrices(); pass an instance to
+    Env.setDataSource (PyDataSource trampoline, PyDataSource.h:9-24).  Its
+    prices are streamed to the device as the external source of every asset.
+    """
+
+    def getData(self):
+        raise NotImplementedError
+
+    def currentData(self):
+        return self.currentPrices()
+
+    def currentPrices(self):
+        raise NotImplementedError
+
+    def reset(self):
+        pass
+
+    def currentTime(self):
+        return 0
+
+    def dataEnd(self):
+        return False
+
+    @property
+    def nAssets(self):
+        return len(np.asarray(self.currentPrices()))
+
+    @property
+    def nFeats(self):
+        return len(np.asarray(self.currentData()))
+
+    @property
+    def assets(self):
+        return [Asset(f"asset_{i}") for i in range(self.nAssets)]
+
+
+class _DeviceSourceView:
+    """Env.dataSource for the device generators (read-only view)."""
+
+    def __init__(self, env):
+        self._env = env
+
+    def currentData(self):
+        return self._env.currentPrices.copy()
+
+    currentPrices = currentData
+
+    def currentTime(self):
+        return self._env.timestamp
+
+    def dataEnd(self):
+        return False
+
+    @property
+    def nAssets(self):
+        return self._env.nAssets
+
+    @property
+    def nFeats(self):
+        return self._env.nFeats
+
+    @property
+    def assets(self):
+        return self._env.assets
+
+
+class PortfolioView:
+    """Env.portfolio: the default Portfolio's accessors (Portfolio.h)."""
+
+    def __init__(self, env):
+        self._env = env
+
+    def __getattr__(self, name):
+        if name.startswith("_"):
+            raise AttributeError(name)
+        return getattr(self._env, name)
+
+    def checkRisk(self, *args):
+        return self._env.checkRisk()
+
+
+class Env:
+    """Drop-in for madigan.environments.cpp.Env (one env on the GPU)."""
+
+    def __init__(self, dataSourceType: str, initCash: float = 1_000_000.0, config_dict=None, *,
+                 device=None, seed: int = 0):
+        self._type = dataSourceType
+        if config_dict is not None and len(dict(config_dict)) > 0:
+            cfg = dict(config_dict)
+            cfg.setdefault("data_source_type", dataSourceType)
+            spec = spec_from_config(cfg)
+        else:
+            spec = default_spec(dataSourceType)
+        self._init_cash = float(initCash)
+        self._device = device
+        self._seed = seed
+        self._source = None
+        # Env::requiredMargin_ / maintenanceMargin_ default to 0 (Env.h:131-132)
+        self._broker = dict(required_margin=0.0, maintenance_margin=0.0, slippage_rel=0.0,
+                            slippage_abs=0.0, transaction_cost_rel=0.0, transaction_cost_abs=0.0)
+        self._make(spec)
+
+    def _make(self, spec):
+        self._spec = spec
+        self._b = BatchedEnv(spec, 1, device=self._device, seed=self._seed,
+                             init_cash=self._init_cash, **self._broker)
+
+    # ---- setters (Env.h:94-111) ------------------------------------------------
+    def setRequiredMargin(self, requiredMargin):
+        self._broker["required_margin"] = float(requiredMargin)
+        self._b.set_broker(required_margin=requiredMargin)
+
+    def setMaintenanceMargin(self, maintenanceMargin):
+        self._broker["maintenance_margin"] = float(maintenanceMargin)
+        self._b.set_broker(maintenance_margin=maintenanceMargin)
+
+    def setSlippage(self, relativeSlippage=0.0, absSlippage=0.0):
+        self._broker.update(slippage_rel=float(relativeSlippage), slippage_abs=float(absSlippage))
+        self._b.set_broker(slippage_rel=relativeSlippage, slippage_abs=absSlippage)
+
+    def setTransactionCost(self, relativeCost=0.0, absCost=0.0):
+        self._broker.update(transaction_cost_rel=float(relativeCost),
+                            transaction_cost_abs=float(absCost))
+        self._b.set_broker(transaction_cost_rel=relativeCost, transaction_cost_abs=absCost)
+
+    def setDataSource(self, dataSource):
+        """Env::setDataSource (Env.h:174-179): a host DataSourceTick feeds every asset."""
+        prices = np.asarray(dataSource.currentPrices(), dtype=np.float64).reshape(-1)
+        spec = SourceSpec(kinds=[L.SRC_EXTERNAL] * len(prices), params=[[]] * len(prices),
+                          assets=[a.code if hasattr(a, "code") else str(a)
+                                  for a in getattr(dataSource, "assets", [])] or
+                          [f"asset_{i}" for i in range(len(prices))])
+        self._source = dataSource
+        torch = _torch()
+        self._make(spec)
+        # the constructor's first tick read zeros; load the source's prices as current
+        self._b.prices.copy_(torch.from_numpy(prices).view(1, -1))
+
+    # ---- stepping -----------------------------------------------------------------
+    def _feed_external(self):
+        if self._source is not None:
+            p = np.asarray(self._source.getData(), dtype=np.float64).reshape(1, -1)
+            self._b.set_prices(p)
+
+    def _state(self, o):
+        return State(o["obs_price"][0].copy(), o["obs_port"][0].copy(), int(o["timestamp"][0]))
+
+    def reset(self):
+        if self._source is not None:
+            self._source.reset()
+            self._feed_external()
+        self._b.reset()
+        return State(self.currentPrices.copy(), self.ledgerNormedFull, self.timestamp)
+
+    def step(self, *args):
+        if len(args) == 0:
+            self._feed_external()
+            self._b.step()
+            o = self._b.host_outputs()
+            return self._state(o), float(o["reward"][0]), bool(o["done"][0]), EnvInfo(
+                BrokerResponse(0.0, 0.0, 0.0, RiskInfo.green, False), self.dataEnd())
+        if len(args) == 2:
+            idx, units = args
+            if isinstance(idx, str):
+                codes = [a.code for a in self.assets]
+                if idx not in codes:
+                    raise IndexError(f"asset code {idx} not found")
+                idx = codes.index(idx)
+            idx = int(idx)
+            if not 0 <= idx < self.nAssets:
+                raise IndexError(f"asset index {idx} out of range")
+            self._feed_external()
+            self._b.step(units=np.array([float(units)]), asset_idx=np.array([idx], np.int32))
+            o = self._b.host_outputs()
+            resp = BrokerResponse(float(o["tprice"][0, idx]), float(o["tunits"][0, idx]),
+                                  float(o["tcost"][0, idx]), RiskInfo(int(o["risk"][0, idx])),
+                                  bool(o["margin_call"][0]))
+            return self._state(o), float(o["reward"][0]), bool(o["done"][0]), EnvInfo(resp, self.dataEnd())
+        if len(args) == 1:
+            units = np.asarray(args[0], dtype=np.float64).reshape(-1)
+            if units.shape[0] != self.nAssets:
+                raise ValueError(f"units must have {self.nAssets} entries, got {units.shape[0]}")
+            self._feed_external()
+            self._b.step(units=units.reshape(1, -1))
+            o = self._b.host_outputs()
+            resp = BrokerResponse(o["tprice"][0].copy(), o["tunits"][0].copy(), o["tcost"][0].copy(),
+                                  [RiskInfo(int(r)) for r in o["risk"][0]], bool(o["margin_call"][0]))
+            return self._state(o), float(o["reward"][0]), bool(o["done"][0]), EnvInfo(resp, self.dataEnd())
+        raise TypeError("step() takes (), (units), (assetIdx, units) or (assetCode, units)")
+
+    # ---- accessors (env.cpp:872-969) --------------------------------------------------
+    def _vals(self):
+        v = self._b.valuation()
+        host = self._b._val.cpu().numpy()[0]
+        return dict(zip(v.keys(), host))
+
+    @property
+    def currentPrices(self):
+        return self._b.prices[0].cpu().numpy()
+
+    @property
+    def ledger(self):
+        return self._b.ledger[0].cpu().numpy()
+
+    @property
+    def meanEntryPrices(self):
+        return self._b.mean_entry[0].cpu().numpy()
+
+    @property
+    def timestamp(self):
+        return int(self._b.timestamp[0].item())
+
+    currentTime = timestamp
+
+    @property
+    def equity(self):
+        return float(self._vals()["equity"])
+
+    @property
+    def cash(self):
+        return float(self._b.cash[0].item())
+
+    @property
+    def pnl(self):
+        return float(self._vals()["pnl"])
+
+    @property
+    def balance(self):
+        return float(self._vals()["balance"])
+
+    @property
+    def availableMargin(self):
+        return float(self._vals()["availableMargin"])
+
+    @property
+    def usedMargin(self):
+        return float(self._vals()["usedMargin"])
+
+    @property
+    def borrowedMargin(self):
+        return float(self._vals()["borrowedMargin"])
+
+    @property
+    def borrowedAssetValue(self):
+        return float(self._vals()["borrowedAssetValue"])
+
+    @property
+    def assetValue(self):
+        return float(self._vals()["assetValue"])
+
+    @property
+    def requiredMargin(self):
+        return self._broker["required_margin"]
+
+    @property
+    def maintenanceMargin(self):
+        return self._broker["maintenance_margin"]
+
+    @property
+    def positionValues(self):
+        return self.ledger * self.currentPrices
+
+    @property
+    def pnlPositions(self):
+        return self.positionValues - self.meanEntryPrices * self.ledger
+
+    @property
+    def positionValuesFull(self):
+        v = self._vals()
+        return np.concatenate([[v["cash"] - v["borrowedMargin"]], self.positionValues])
+
+    @property
+    def ledgerFull(self):
+        v = self._vals()
+        return np.concatenate([[v["cash"] - v["borrowedMargin"]], self.ledger])
+
+    @property
+    def ledgerNormed(self):
+        return self.positionValues / self._vals()["equity"]
+
+    @property
+    def ledgerNormedFull(self):
+        v = self._vals()
+        eq = v["equity"]
+        return np.concatenate([[(v["cash"] - v["borrowedMargin"]) / eq], self.positionValues / eq])
+
+    @property
+    def ledgerAbsNormed(self):
+        ln = self.ledgerNormed
+        return ln / np.abs(ln).sum()
+
+    @property
+    def ledgerAbsNormedFull(self):
+        ln = self.ledgerNormedFull
+        return ln / np.abs(ln).sum()
+
+    @property
+    def nAssets(self):
+        return self._spec.n_assets
+
+    @property
+    def nFeats(self):
+        return self._spec.n_assets
+
+    @property
+    def assets(self):
+        return [Asset(a) for a in self._spec.assets]
+
+    @property
+    def isDateTime(self):
+        return False
+
+    @property
+    def dataSource(self):
+        return self._source if self._source is not None else _DeviceSourceView(self)
+
+    @property
+    def portfolio(self):
+        return PortfolioView(self)
+
+    @property
+    def broker(self):
+        return PortfolioView(self)
+
+    @property
+    def account(self):
+        return PortfolioView(self)
+
+    def dataEnd(self):
+        return bool(self._source.dataEnd()) if self._source is not None else False
+
+    def checkRisk(self):
+        return RiskInfo(int(self._vals()["checkRisk"]))
+
+    @property
+    def batched(self) -> BatchedEnv:
+        return self._b
+
+
+# ---------------------------------------------------------------------------
+# madigan/environments/__init__.py surface
+
+
+def _cfg_get(config: Any, key: str, default=None):
+    if isinstance(config, dict):
+        return config.get(key, default)
+    return getattr(config, key, default)
+
+
+def make_env(config, test: bool = False, **kw) -> Env:
+    """make_env (madigan/environments/__init__.py:9-22)."""
+    import copy
+    config = copy.deepcopy(dict(config))
+    if test and "data_source_config_test" in config:
+        config["data_source_config"] = config["data_source_config_test"]
+    if config.get("env_type", "Synth") in ("Synth",):
+        if config.get("data_source_config") is not None:
+            env = Env(config["data_source_type"], config["init_cash"], config, **kw)
+        else:
+            env = Env(config["data_source_type"], config["init_cash"], **kw)
+        env.setRequiredMargin(config["required_margin"])
+        env.setMaintenanceMargin(config["maintenance_margin"])
+        env.setTransactionCost(config["transaction_cost_rel"], config["transaction_cost_abs"])
+        env.setSlippage(config["slippage_rel"], config["slippage_abs"])
+        return env
+    raise NotImplementedError(f"Env type {config.get('env_type')} not implemented")
+
+
+def make_batched_env(config, n_envs: int, **kw) -> BatchedEnv:
+    """BatchedEnv from a reference experiment config (env, preprocessor and
+    reward-shaper keys: madigan/utils/config.py:104-115, config.yaml:280-310)."""
+    spec = spec_from_config(config)
+    pconf = _cfg_get(config, "preprocessor_config") or {}
+    rconf = _cfg_get(config, "reward_shaper_config") or {}
+    window = int(kw.pop("window", _cfg_get(pconf, "window_length", 0) or 0))
+    norm = _cfg_get(pconf, "norm", False)
+    norm_type = kw.pop("norm_type", _cfg_get(pconf, "norm_type", None) if norm else None)
+    shaper = kw.pop("reward_shaper", _cfg_get(rconf, "reward_shaper", None))
+    return BatchedEnv(
+        spec, n_envs, init_cash=_cfg_get(config, "init_cash", 1_000_000.0),
+        required_margin=_cfg_get(config, "required_margin", 1.0),
+        maintenance_margin=_cfg_get(config, "maintenance_margin", 0.25),
+        slippage_rel=_cfg_get(config, "slippage_rel", 0.0),
+        slippage_abs=_cfg_get(config, "slippage_abs", 0.0),
+        transaction_cost_rel=_cfg_get(config, "transaction_cost_rel", 0.0),
+        transaction_cost_abs=_cfg_get(config, "transaction_cost_abs", 0.0),
+        reward_shaper=shaper, adaptation_rate=_cfg_get(rconf, "adaptation_rate", 0.001),
+        cosine_temp=_cfg_get(rconf, "cosine_temp", 0.0),
+        desired_portfolio=_cfg_get(rconf, "desired_portfolio", None) if shaper in (
+            "cosine", "cosine_similarity", "cosine_port_shaper") else None,
+        window=window, norm_type=norm_type, **kw)
+
+
+def get_env_info(env: Env) -> dict:
+    """get_env_info (madigan/environments/__init__.py:41-56)."""
+    return {
+        "timestamp": env.timestamp,
+        "riskInfo": env.checkRisk(),
+        "prices": np.array(env.currentPrices, copy=True),
+        "equity": env.equity,
+        "cash": env.cash,
+        "pnl": env.pnl,
+        "balance": env.portfolio.balance,
+        "availableMargin": env.availableMargin,
+        "usedMargin": env.usedMargin,
+        "borrowedAssetValue": env.borrowedAssetValue,
+        "borrowedMargin": env.borrowedMargin,
+        "ledger": np.array(env.ledger, copy=True),
+        "ledgerNormed": np.array(env.ledgerNormed, copy=True),
+    }

@@ -1,0 +1,941 @@
+/*
+ * madigan_oracle.c -- CPU restatement of madigan's market-simulation step.
+ *
+ * TEST INFRASTRUCTURE ONLY (see madigan_oracle.h).  Restates, statement by
+ * statement and in the reference's operation order:
+ *   Portfolio   madigan/environments/cpp/Portfolio.cpp:150-323
+ *   Broker      madigan/environments/cpp/Broker.cpp:124-178
+ *   Env         madigan/environments/cpp/Env.h:150-256
+ *   Sine        madigan/environments/cpp/DataSource.cpp:455-543
+ *   OU          madigan/environments/cpp/DataSource.cpp:1118-1180
+ *   TrendOU     madigan/environments/cpp/DataSource.cpp:1364-1502
+ *   Composite   madigan/environments/cpp/DataSource.cpp:411-451
+ *   DSR/DDR/PPC madigan/utils/buffers/nstep_buffer.py:20-204
+ *   Stacker     madigan/utils/preprocessor.py:53-107, :143-199
+ *   agent step  madigan/modelling/algorithm/dqn.py:160-179,
+ *               madigan/modelling/algorithm/offpolicy_q.py:138-164
+ *
+ * Build strict IEEE: gcc -O2 -ffp-contract=off (oracle/Makefile).  The same
+ * source built with -O3 -march=native -ffast-math (the reference's own flags,
+ * madigan/environments/cpp/CMakeLists.txt:5) is the CPU-baseline timing build.
+ */
+#include "madigan_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define MAXA ORC_MAX_ASSETS
+
+/* ------------------------------------------------------------------------ */
+/* Deterministic math: the random-variate transform is this framework's own */
+/* specification (the reference seeds std::default_random_engine from the   */
+/* wall clock, DataSource.cpp:472/1131/1407, so its stream is not            */
+/* reproducible).  Device code implements the identical algorithms.          */
+/* ------------------------------------------------------------------------ */
+
+static inline double from_bits(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
+static inline uint64_t to_bits(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
+
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+  uint32_t k0 = key[0], k1 = key[1];
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c0 = hi1 ^ c1 ^ k0;
+    c1 = lo1;
+    c2 = hi0 ^ c3 ^ k1;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+static void draw(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot, uint64_t tick,
+                 uint64_t *a, uint64_t *b) {
+  uint32_t ctr[4] = {(uint32_t)tick, (uint32_t)env, asset | (slot << 16),
+                     (uint32_t)(tick >> 32) ^ (uint32_t)(env >> 32)};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t x[4];
+  orc_philox4x32_10(ctr, key, x);
+  *a = (((uint64_t)x[1] << 32) | x[0]) >> 11;
+  *b = (((uint64_t)x[3] << 32) | x[2]) >> 11;
+}
+
+static const double TWO_M53 = 1.1102230246251565404e-16; /* 2^-53 */
+
+void orc_uniform2(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot, uint64_t tick,
+                  double *u0, double *u1) {
+  uint64_t a, b;
+  draw(seed, env, asset, slot, tick, &a, &b);
+  *u0 = (double)a * TWO_M53;
+  *u1 = (double)b * TWO_M53;
+}
+
+/* fdlibm e_log.c algorithm (public domain, Sun Microsystems) for normal x>0 */
+double orc_log(double x) {
+  const double ln2_hi = from_bits(0x3fe62e42fee00000ull);
+  const double ln2_lo = from_bits(0x3dea39ef35793c76ull);
+  const double Lg1 = from_bits(0x3FE5555555555593ull), Lg2 = from_bits(0x3FD999999997FA04ull),
+               Lg3 = from_bits(0x3FD2492494229359ull), Lg4 = from_bits(0x3FCC71C51D8E78AFull),
+               Lg5 = from_bits(0x3FC7466496CB03DEull), Lg6 = from_bits(0x3FC39A09D078C69Full),
+               Lg7 = from_bits(0x3FC2F112DF3E5244ull);
+  uint64_t ix = to_bits(x);
+  int32_t hx = (int32_t)(ix >> 32);
+  int32_t k = ((hx >> 20) & 0x7ff) - 1023;
+  hx &= 0x000fffff;
+  int32_t i = (hx + 0x95f64) & 0x100000; /* normalize m into [sqrt(2)/2, sqrt(2)) */
+  k += (i >> 20);
+  uint64_t mb = ((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (ix & 0xffffffffull);
+  double f = from_bits(mb) - 1.0;
+  double s = f / (2.0 + f);
+  double dk = (double)k;
+  double z = s * s;
+  double w = z * z;
+  double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  double R = t2 + t1;
+  double hfsq = 0.5 * f * f;
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
+/* fdlibm k_sin.c / k_cos.c kernels on |x| <= pi/4 with tail y */
+static double k_sin(double x, double y, int iy) {
+  const double S1 = from_bits(0xBFC5555555555549ull), S2 = from_bits(0x3F8111111110F8A6ull),
+               S3 = from_bits(0xBF2A01A019C161D5ull), S4 = from_bits(0x3EC71DE357B1FE7Dull),
+               S5 = from_bits(0xBE5AE5E68A2B9CEBull), S6 = from_bits(0x3DE5D93A5ACFD57Cull);
+  double z = x * x;
+  double v = z * x;
+  double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+  if (iy == 0) return x + v * (S1 + z * r);
+  return x - ((z * (0.5 * y - v * r) - y) - v * S1);
+}
+static double k_cos(double x, double y) {
+  const double C1 = from_bits(0x3FA555555555554Cull), C2 = from_bits(0xBF56C16C16C15177ull),
+               C3 = from_bits(0x3EFA01A019CB1590ull), C4 = from_bits(0xBE927E4F809C52ADull),
+               C5 = from_bits(0x3E21EE9EBDB4B1C4ull), C6 = from_bits(0xBDA8FAE9BE8838D4ull);
+  double z = x * x;
+  double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+  double hz = 0.5 * z;
+  double w = 1.0 - hz;
+  return w + (((1.0 - w) - hz) + (z * r - x * y));
+}
+
+/* cos(2*pi*u), u in [0,1): exact octant reduction t=4u, q=rint(t). */
+double orc_cos2pi(double u) {
+  const double pio2 = from_bits(0x3FF921FB54442D18ull);
+  double t = 4.0 * u;
+  double q = floor(t + 0.5);
+  double f = t - q;           /* exact, |f| <= 0.5 */
+  double r = f * pio2;        /* |r| <= pi/4 */
+  int iq = ((int)q) & 3;
+  switch (iq) {
+    case 0: return k_cos(r, 0.0);
+    case 1: return -k_sin(r, 0.0, 0);
+    case 2: return -k_cos(r, 0.0);
+    default: return k_sin(r, 0.0, 0);
+  }
+}
+
+/* sin(x): fdlibm medium-range Cody-Waite reduction (e_rem_pio2.c), kernels above. */
+double orc_sin(double x) {
+  const double invpio2 = from_bits(0x3FE45F306DC9C883ull);
+  const double pio2_1 = from_bits(0x3FF921FB54400000ull), pio2_1t = from_bits(0x3DD0B4611A626331ull);
+  const double pio2_2 = from_bits(0x3DD0B4611A600000ull), pio2_2t = from_bits(0x3BA3198A2E037073ull);
+  const double pio2_3 = from_bits(0x3BA3198A2E000000ull), pio2_3t = from_bits(0x397B839A252049C1ull);
+  double ax = fabs(x);
+  if (ax <= 0.78539816339744827900) return k_sin(x, 0.0, 0);
+  if (!(ax < INFINITY)) return x - x;
+  double fn = floor(x * invpio2 + 0.5);
+  int32_t n = (int32_t)(int64_t)fn;
+  double r = x - fn * pio2_1;
+  double w = fn * pio2_1t;
+  double y0 = r - w;
+  int32_t j = (int32_t)((to_bits(x) >> 52) & 0x7ff);
+  int32_t i = j - (int32_t)((to_bits(y0) >> 52) & 0x7ff);
+  if (i > 16) { /* 2nd iteration, good to 118 bits */
+    double t = r;
+    w = fn * pio2_2;
+    r = t - w;
+    w = fn * pio2_2t - ((t - r) - w);
+    y0 = r - w;
+    i = j - (int32_t)((to_bits(y0) >> 52) & 0x7ff);
+    if (i > 49) { /* 3rd iteration, 151 bits */
+      t = r;
+      w = fn * pio2_3;
+      r = t - w;
+      w = fn * pio2_3t - ((t - r) - w);
+      y0 = r - w;
+    }
+  }
+  double y1 = (r - y0) - w;
+  switch (n & 3) {
+    case 0: return k_sin(y0, y1, 1);
+    case 1: return k_cos(y0, y1);
+    case 2: return -k_sin(y0, y1, 1);
+    default: return -k_cos(y0, y1);
+  }
+}
+
+/* Box-Muller on one Philox block: z = sqrt(-2 log u1) cos(2 pi u2), u1 in (0,1]. */
+double orc_normal(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot, uint64_t tick) {
+  uint64_t a, b;
+  draw(seed, env, asset, slot, tick, &a, &b);
+  double u1 = (double)(a + 1) * TWO_M53;
+  double u2 = (double)b * TWO_M53;
+  return sqrt(-2.0 * orc_log(u1)) * orc_cos2pi(u2);
+}
+
+/* Canonical reduction: pairwise tree over v[0..n-1], padded with +0.0 to the
+ * next power of two.  The HIP kernels use the same tree. */
+double orc_canon_sum(const double *v, int n) {
+  double t[2 * MAXA + 2];
+  int p = 1;
+  while (p < n) p <<= 1;
+  for (int i = 0; i < p; ++i) t[i] = (i < n) ? v[i] : 0.0;
+  for (int w = p; w > 1; w >>= 1)
+    for (int i = 0; i < w / 2; ++i) t[i] = t[2 * i] + t[2 * i + 1];
+  return t[0];
+}
+
+/* ------------------------------------------------------------------------ */
+/* Environment state                                                        */
+/* ------------------------------------------------------------------------ */
+
+typedef struct {
+  /* Portfolio (Portfolio.h:109-130) */
+  double L[MAXA], mep[MAXA], Bm[MAXA];
+  double cash;
+  /* DataSource state */
+  double P[MAXA];
+  double x[MAXA];       /* Synth phase accumulator (DataSource.h:246) */
+  double ouMean[MAXA];  /* TrendOU (DataSource.h:670) */
+  double dY[MAXA];
+  int32_t tlen[MAXA];
+  uint8_t trending[MAXA];
+  int8_t dir[MAXA];
+  uint64_t ts;
+  /* shaper state (nstep_buffer.py:38-60): index 0 for scalar */
+  double sA[MAXA], sB[MAXA];
+  /* episode statistics */
+  double ep_ret, ep_len, last_ret, last_len, last_eq, n_done;
+  /* StackerDiscrete deques (preprocessor.py:150-152) */
+  double *ring;          /* W rows of (A + A+1) */
+  uint64_t *ring_ts;
+  int wlen, whead;
+} orc_env;
+
+struct orc_batch {
+  orc_config cfg;
+  orc_asset_src src[MAXA];
+  int N, A;
+  orc_env *envs;
+  double *ext;  /* (N,A) external prices */
+};
+
+/* ---- Portfolio valuation (Portfolio.cpp:170-235) ------------------------ */
+
+static double p_asset_value(const orc_env *s, int A) {           /* :180-182 */
+  double t[MAXA];
+  for (int i = 0; i < A; ++i) t[i] = s->L[i] * s->P[i];
+  return orc_canon_sum(t, A);
+}
+static double p_pnl(const orc_env *s, int A) {                   /* :184-186 */
+  double t[MAXA];
+  for (int i = 0; i < A; ++i) t[i] = s->mep[i] * s->L[i];
+  return p_asset_value(s, A) - orc_canon_sum(t, A);
+}
+static double p_balance(const orc_env *s, int A) {               /* :192-197 */
+  double t[MAXA];
+  for (int i = 0; i < A; ++i) {
+    double mask = (s->L[i] < 0.) ? 1.0 : 0.0;
+    t[i] = s->L[i] * (s->mep[i] * mask);
+  }
+  return s->cash + orc_canon_sum(t, A);
+}
+static double p_borrowed_margin(const orc_env *s, int A) {       /* :207-209 */
+  return orc_canon_sum(s->Bm, A);
+}
+static double p_equity(const orc_env *s, int A) {                /* :211-213 */
+  return s->cash + p_asset_value(s, A) - p_borrowed_margin(s, A);
+}
+static double p_available_margin(const orc_env *s, int A, double reqM) { /* :229-231 */
+  return (p_balance(s, A) + p_pnl(s, A)) / reqM;
+}
+static double p_used_margin(const orc_env *s, int A, double reqM) {      /* :199-201 */
+  double t[MAXA];
+  for (int i = 0; i < A; ++i) t[i] = fabs(s->L[i]) * s->mep[i];
+  return reqM * orc_canon_sum(t, A);
+}
+static double p_borrowed_asset_value(const orc_env *s, int A) {  /* :219-223 */
+  double t[MAXA];
+  for (int i = 0; i < A; ++i) {
+    double mask = (s->L[i] < 0.) ? 1.0 : 0.0;
+    t[i] = s->L[i] * (s->P[i] * mask);
+  }
+  return orc_canon_sum(t, A);
+}
+
+/* Portfolio::checkRisk() -- Portfolio.cpp:243-252 */
+static int p_check_risk(const orc_env *s, int A, double mainM) {
+  double marginRequired = mainM * p_pnl(s, A);
+  if (p_equity(s, A) <= -marginRequired) return ORC_MARGIN_CALL;
+  if ((p_balance(s, A) + p_pnl(s, A)) <= -marginRequired) return ORC_MARGIN_CALL;
+  return ORC_GREEN;
+}
+
+/* Portfolio::checkRisk(assetIdx, units) -- Portfolio.cpp:254-279 */
+static int p_check_risk_order(const orc_env *s, int A, double reqM, double mainM, int i,
+                              double units) {
+  double cashAmount = s->P[i] * units;
+  double currentUnits = s->L[i];
+  if (signbit(units) != signbit(currentUnits)) {
+    if (units > -1 * currentUnits) {
+      double excess = units + currentUnits;
+      if (p_available_margin(s, A, reqM) <= fabs(s->P[i] * excess) || p_balance(s, A) <= 0.)
+        return ORC_INSUFF_MARGIN;
+    }
+    return ORC_GREEN;
+  }
+  if (p_check_risk(s, A, mainM) == ORC_MARGIN_CALL) return ORC_MARGIN_CALL;
+  if (p_available_margin(s, A, reqM) <= fabs(cashAmount) || p_balance(s, A) <= 0.)
+    return ORC_INSUFF_MARGIN;
+  return ORC_GREEN;
+}
+
+/* Portfolio::handleTransaction -- Portfolio.cpp:284-323 */
+static void p_handle_transaction(orc_env *s, double reqM, int i, double transactionPrice,
+                                 double units, double transactionCost) {
+  double *currentUnits = &s->L[i];
+  double *meanEntryPrice = &s->mep[i];
+  if (signbit(*currentUnits) != signbit(units)) {
+    if (fabs(units) > fabs(*currentUnits)) {
+      units += *currentUnits;
+      s->cash += *currentUnits * transactionPrice;
+      *currentUnits = 0.;
+      *meanEntryPrice = transactionPrice;
+    }
+  } else {
+    *meanEntryPrice += (transactionPrice - *meanEntryPrice) * (units / (units + *currentUnits));
+  }
+  double amount_in_base_currency = transactionPrice * units;
+  double marginToUse = amount_in_base_currency * reqM;
+  double marginToBorrow = amount_in_base_currency - marginToUse;
+  double *borrowedMarginRef = &s->Bm[i];
+  *borrowedMarginRef += marginToBorrow;
+  s->cash -= (marginToUse + transactionCost);
+  *currentUnits += units;
+  if (fabs(*currentUnits) < 0.000001) {
+    *meanEntryPrice = 0.;
+    if (*borrowedMarginRef > 0.) {
+      s->cash -= *borrowedMarginRef;
+      *borrowedMarginRef = 0.;
+    }
+  }
+  if (*borrowedMarginRef < 0.) {
+    s->cash -= *borrowedMarginRef;
+    *borrowedMarginRef = 0.;
+  }
+}
+
+/* Portfolio::ledgerNormedFull -- Portfolio.cpp:150-155 */
+static void p_ledger_normed_full(const orc_env *s, int A, double *out) {
+  double eq = p_equity(s, A);
+  out[0] = (s->cash - p_borrowed_margin(s, A)) / eq;
+  for (int i = 0; i < A; ++i) out[1 + i] = (s->L[i] * s->P[i]) / eq;
+}
+
+/* Broker::handleTransaction(port, i, u) -- Broker.cpp:124-142, :171-178 */
+static void b_handle_transaction(const orc_config *c, orc_env *s, int A, int i, double units,
+                                 double *tp_o, double *u_o, double *cost_o, int *risk_o) {
+  *tp_o = 0.; *u_o = 0.; *cost_o = 0.; *risk_o = ORC_GREEN;
+  if (units != 0.) {
+    int risk = p_check_risk_order(s, A, c->required_margin, c->maintenance_margin, i, units);
+    *risk_o = risk;
+    if (risk == ORC_GREEN) {
+      double currentPrice = s->P[i];
+      double slippage = (currentPrice * c->slippage_rel) + c->slippage_abs;  /* :172 */
+      double transactionPrice = units < 0 ? (currentPrice - slippage) : (currentPrice + slippage);
+      double transactionCost = fabs(units * currentPrice) * c->tc_rel + c->tc_abs; /* :131,:176 */
+      p_handle_transaction(s, c->required_margin, i, transactionPrice, units, transactionCost);
+      *tp_o = transactionPrice; *u_o = units; *cost_o = transactionCost;
+    }
+  }
+}
+
+/* ---- DataSource::getData ------------------------------------------------ */
+
+static void src_get_data(orc_batch *b, int e) {
+  orc_env *s = &b->envs[e];
+  uint64_t genv = (uint64_t)(b->cfg.env_offset + e);
+  uint64_t seed = b->cfg.seed;
+  uint64_t tick = s->ts;
+  for (int i = 0; i < b->A; ++i) {
+    const double *p = b->src[i].p;
+    switch (b->src[i].kind) {
+      case ORC_SRC_SINE: { /* Synth::getData, DataSource.cpp:535-543 */
+        double noise = 0.0;
+        if (p[5] != 0.0) noise = orc_normal(seed, genv, (uint32_t)i, 0, tick) * p[5] + 0.0;
+        const double PI2 = 3.141592653589793238463 * 2;
+        s->P[i] = noise + p[1] + p[2] * orc_sin(PI2 * s->x[i] * p[0]);
+        s->x[i] += p[4];
+        break;
+      }
+      case ORC_SRC_OU: { /* OU::getData, DataSource.cpp:1173-1180 */
+        double z = orc_normal(seed, genv, (uint32_t)i, 0, tick) * 1.0 + 0.0;
+        double x = s->P[i];
+        x += (p[1] * (p[0] - x)) + p[0] * p[2] * z;
+        s->P[i] = x;
+        break;
+      }
+      case ORC_SRC_TRENDOU: { /* TrendOU::getData, DataSource.cpp:1457-1493 */
+        double y = s->P[i];
+        if (s->trending[i]) {
+          double n = orc_normal(seed, genv, (uint32_t)i, 0, tick) * p[8] + 0.0;
+          y += y * (s->dY[i] * (double)s->dir[i] + n);
+          s->tlen[i] -= 1;
+          if (s->tlen[i] == 0) {
+            s->trending[i] = 0;
+            s->ouMean[i] = y;
+          }
+          y = (0.01 < y) ? y : 0.01;   /* std::max(0.01, y) */
+          if (y <= .1) s->dir[i] = 1;
+        } else {
+          double n = orc_normal(seed, genv, (uint32_t)i, 0, tick) * p[7] + 0.0;
+          double ou_noise = y * n;
+          double ou_reverting_component = p[6] * (s->ouMean[i] - y);
+          y += ou_reverting_component + ou_noise;
+          double u_trend, u_dir;
+          orc_uniform2(seed, genv, (uint32_t)i, 1, tick, &u_trend, &u_dir);
+          if (u_trend < p[0]) {
+            double u_len, u_dy;
+            orc_uniform2(seed, genv, (uint32_t)i, 2, tick, &u_len, &u_dy);
+            s->trending[i] = 1;
+            s->dir[i] = (u_dir < 0.5) ? -1 : 1;
+            int32_t lo = (int32_t)p[1], hi = (int32_t)p[2];
+            int32_t len = lo + (int32_t)(u_len * (double)(hi - lo + 1));
+            if (len > hi) len = hi;
+            s->tlen[i] = len;
+            s->dY[i] = (p[4] - p[3]) * u_dy + p[3];
+          }
+        }
+        s->P[i] = y;
+        break;
+      }
+      default: /* external replay: prices supplied via orc_set_prices */
+        s->P[i] = b->ext[(size_t)e * b->A + i];
+        break;
+    }
+  }
+  s->ts += 1;  /* timestamp_ += 1 (Composite and children tick together) */
+}
+
+/* DataSource::reset: OU no-op (DataSource.h:466), Synth no-op (:232),
+ * TrendOU restores start (DataSource.cpp:1495-1502). */
+static void src_reset(orc_batch *b, int e) {
+  orc_env *s = &b->envs[e];
+  for (int i = 0; i < b->A; ++i) {
+    if (b->src[i].kind == ORC_SRC_TRENDOU) {
+      s->trending[i] = 0;
+      s->P[i] = b->src[i].p[5];
+      s->tlen[i] = 0;
+      s->ouMean[i] = b->src[i].p[5];
+    }
+  }
+}
+
+/* source construction (initParams) */
+static void src_init(orc_batch *b, int e) {
+  orc_env *s = &b->envs[e];
+  for (int i = 0; i < b->A; ++i) {
+    const double *p = b->src[i].p;
+    switch (b->src[i].kind) {
+      case ORC_SRC_SINE: s->x[i] = p[3]; s->P[i] = 0.0; break;        /* :466 */
+      case ORC_SRC_OU: s->P[i] = p[0]; break;                           /* :1128 */
+      case ORC_SRC_TRENDOU:                                             /* :1380-1400, quirk 1 fixed */
+        s->P[i] = p[5]; s->ouMean[i] = p[5]; s->dir[i] = 1; s->tlen[i] = 0;
+        s->dY[i] = 0.; s->trending[i] = 0; break;
+      default: s->P[i] = 0.0; break;
+    }
+  }
+  s->ts = 0;
+}
+
+/* Env::initAccountants -- Env.h:150-165: fresh Broker/Portfolio, one getData */
+static void env_init_accountants(orc_batch *b, int e) {
+  orc_env *s = &b->envs[e];
+  for (int i = 0; i < b->A; ++i) { s->L[i] = 0.; s->mep[i] = 0.; s->Bm[i] = 0.; }
+  s->cash = b->cfg.init_cash;
+  src_get_data(b, e);
+}
+
+/* ---- window (StackerDiscrete) ------------------------------------------- */
+
+static void window_stream(orc_batch *b, int e) {  /* preprocessor.py:172-175 */
+  int W = b->cfg.window;
+  if (W <= 0) return;
+  orc_env *s = &b->envs[e];
+  int A = b->A, R = 2 * A + 1;
+  int h = (s->whead + 1) % W;
+  double *row = s->ring + (size_t)h * R;
+  for (int i = 0; i < A; ++i) row[i] = s->P[i];
+  p_ledger_normed_full(s, A, row + A);
+  s->ring_ts[h] = s->ts;
+  s->whead = h;
+  if (s->wlen < W) s->wlen++;
+}
+
+static void window_clear(orc_batch *b, int e) {  /* reset_state, preprocessor.py:196-199 */
+  b->envs[e].wlen = 0;
+  b->envs[e].whead = b->cfg.window > 0 ? b->cfg.window - 1 : 0;
+}
+
+/* Agent reset: env.reset(); preprocessor.reset_state(); stream_state(state);
+ * initialize_history(env) -- offpolicy_q.py:93-99, preprocessor.py:191-194 */
+static void env_reset_one(orc_batch *b, int e) {
+  src_reset(b, e);
+  env_init_accountants(b, e);
+  if (b->cfg.window > 0) {
+    window_clear(b, e);
+    window_stream(b, e);
+    while (b->envs[e].wlen < b->cfg.window) {
+      src_get_data(b, e);  /* Env::step() with no action: only the tick matters */
+      window_stream(b, e);
+    }
+  }
+}
+
+/* ---- shapers (nstep_buffer.py) ------------------------------------------ */
+
+static const double ORC_EPS = 1.1920928955078125e-07; /* np.finfo(np.float32).eps, :20 */
+
+static double dsr_one(double r, double A, double B) { /* _DSR.calculate_dsr :80-85 */
+  double dA = r - A;
+  double dB = r * r - B;
+  double t = B - A * A;
+  return (B * dA - (A * dB) / 2) / (pow(t * t, 3.0 / 4.0) + ORC_EPS);
+}
+static double ddr_one(double r, double A, double B) { /* _DDR.calculate_ddr :146-156 */
+  if (r > 0.) return (r - A / 2) / (sqrt(B) + ORC_EPS);
+  return (B * (r - A / 2) - (A * (r * r)) / 2) / (pow(B, 3.0 / 2.0) + ORC_EPS);
+}
+static double clip1(double v) { /* np.clip(v, -1, 1) */
+  if (v < -1.) return -1.;
+  if (v > 1.) return 1.;
+  return v;
+}
+
+void orc_dsr(const double *rewards, int L, int D, const double *discounts, double eta,
+             double *A, double *B, double *out) {
+  for (int d = 0; d < D; ++d) {
+    double acc = 0.0;
+    for (int k = 0; k < L; ++k) acc += discounts[k] * dsr_one(rewards[k * D + d], A[d], B[d]);
+    out[d] = clip1(acc / L);
+    double r0 = rewards[d];                     /* update_parameters :87-91 */
+    A[d] += eta * (r0 - A[d]);
+    B[d] += eta * (r0 * r0 - B[d]);
+  }
+}
+
+void orc_ddr(const double *rewards, int L, int D, const double *discounts, double eta,
+             double *A, double *B, double *out) {
+  for (int d = 0; d < D; ++d) {
+    double acc = 0.0;
+    for (int k = 0; k < L; ++k) acc += discounts[k] * ddr_one(rewards[k * D + d], A[d], B[d]);
+    out[d] = clip1(acc / L);
+    double r0 = rewards[d];                     /* update_parameters :158-162 */
+    double m = r0 < 0. ? r0 : 0.;               /* np.minimum(r, 0.) */
+    if (r0 != r0) m = r0;
+    A[d] += eta * (r0 - A[d]);
+    B[d] += eta * (m * m - B[d]);
+  }
+}
+
+/* cosine_similarity (nstep_buffer.py:173-178) over the A+1 entries of
+ * ledgerNormedFull: canonical order = entry 0 (cash) + tree over the A assets. */
+static double sum_full(const double *v, int n) { return v[0] + orc_canon_sum(v + 1, n - 1); }
+static double cosine_sim(const double *p, const double *q, int n) {
+  double pp[MAXA + 1], qq[MAXA + 1], pq[MAXA + 1];
+  for (int i = 0; i < n; ++i) { pp[i] = p[i] * p[i]; qq[i] = q[i] * q[i]; pq[i] = p[i] * q[i]; }
+  double norm_p = sqrt(sum_full(pp, n));
+  double norm_q = sqrt(sum_full(qq, n));
+  return sum_full(pq, n) / (norm_p * norm_q);
+}
+
+/* ---- public API ---------------------------------------------------------- */
+
+orc_batch *orc_create(const orc_config *cfg, const orc_asset_src *srcs) {
+  if (cfg->n_assets < 1 || cfg->n_assets > MAXA || cfg->n_envs < 1) return NULL;
+  orc_batch *b = (orc_batch *)calloc(1, sizeof(orc_batch));
+  b->cfg = *cfg;
+  b->N = cfg->n_envs;
+  b->A = cfg->n_assets;
+  memcpy(b->src, srcs, sizeof(orc_asset_src) * (size_t)b->A);
+  b->envs = (orc_env *)calloc((size_t)b->N, sizeof(orc_env));
+  b->ext = (double *)calloc((size_t)b->N * b->A, sizeof(double));
+  int W = cfg->window;
+  for (int e = 0; e < b->N; ++e) {
+    if (W > 0) {
+      b->envs[e].ring = (double *)calloc((size_t)W * (2 * b->A + 1), sizeof(double));
+      b->envs[e].ring_ts = (uint64_t *)calloc((size_t)W, sizeof(uint64_t));
+    }
+    window_clear(b, e);
+    src_init(b, e);               /* Env::initMembers -> makeDataSource (Env.h:139-148) */
+    env_init_accountants(b, e);   /* -> initAccountants (one getData) */
+  }
+  return b;
+}
+
+void orc_destroy(orc_batch *b) {
+  if (!b) return;
+  for (int e = 0; e < b->N; ++e) { free(b->envs[e].ring); free(b->envs[e].ring_ts); }
+  free(b->envs);
+  free(b->ext);
+  free(b);
+}
+
+void orc_reset(orc_batch *b, const uint8_t *mask) {
+  for (int e = 0; e < b->N; ++e)
+    if (!mask || mask[e]) env_reset_one(b, e);
+}
+
+void orc_set_prices(orc_batch *b, const double *prices) {
+  memcpy(b->ext, prices, sizeof(double) * (size_t)b->N * b->A);
+}
+
+/* agent per-asset reward: offpolicy_q.py:152-164 */
+static void agent_reward(const orc_env *s, int A, const double *prevVal, double prevEq,
+                         const double *tp, const double *tu, const double *tc, double *r) {
+  for (int i = 0; i < A; ++i) {
+    double curr = s->L[i] * s->P[i];
+    double mar_diff = tu[i] * tp[i] + tc[i];
+    double v = ((curr - prevVal[i]) - mar_diff) / prevEq;
+    v += 1;
+    v = (v < .35) ? .35 : v;  /* np.maximum(reward, .35) */
+    if (v != v) v = NAN;
+    r[i] = log(v);
+  }
+}
+
+static void step_one(orc_batch *b, int e, int kind, const double *units, int32_t single_idx,
+                     double single_u, const orc_out *o) {
+  const orc_config *c = &b->cfg;
+  orc_env *s = &b->envs[e];
+  const int A = b->A;
+  double tp[MAXA], tu[MAXA], tc[MAXA], prevVal[MAXA];
+  int risk[MAXA];
+  for (int i = 0; i < A; ++i) { tp[i] = 0.; tu[i] = 0.; tc[i] = 0.; risk[i] = ORC_GREEN; }
+  for (int i = 0; i < A; ++i) prevVal[i] = s->L[i] * s->P[i];
+
+  double prevEq = p_equity(s, A);                                      /* Env.h:208 */
+  if (kind == ORC_STEP_UNITS) {                                        /* Broker.cpp:144-158 */
+    for (int i = 0; i < A; ++i) {
+      int r;
+      b_handle_transaction(c, s, A, i, units[i], &tp[i], &tu[i], &tc[i], &r);
+      risk[i] = r;
+    }
+  } else if (kind == ORC_STEP_SINGLE) {                                /* Env.h:235 */
+    int r;
+    int i = single_idx;
+    b_handle_transaction(c, s, A, i, single_u, &tp[i], &tu[i], &tc[i], &r);
+    risk[i] = r;
+  }
+  /* BrokerResponse.marginCall (Broker.cpp:156-157); Env::step() has none (Env.h:199) */
+  int marginCall = (kind != ORC_STEP_NONE) &&
+                   p_check_risk(s, A, c->maintenance_margin) == ORC_MARGIN_CALL;
+  src_get_data(b, e);                                                  /* Env.h:210 */
+  double currentEq = p_equity(s, A);                                   /* :211 */
+  double ratio = currentEq / prevEq;
+  double clampv = (kind == ORC_STEP_SINGLE) ? 0.01 : 0.3;              /* :212, :238 */
+  double reward = log((ratio < clampv) ? clampv : ratio);
+  int done = 0;
+  int prisk = p_check_risk(s, A, c->maintenance_margin);              /* :215 */
+  for (int i = 0; i < A; ++i)
+    if (risk[i] != ORC_GREEN && risk[i] != ORC_INSUFF_MARGIN) done = 1;
+  if (prisk != ORC_GREEN || p_equity(s, A) < 0.1 * c->init_cash) done = 1;
+
+  /* agent-side reward (offpolicy_q.py:152-164) */
+  double ar[MAXA];
+  agent_reward(s, A, prevVal, prevEq, tp, tu, tc, ar);
+  double ar_sum = orc_canon_sum(ar, A);
+
+  /* State.portfolio */
+  double port[MAXA + 1];
+  p_ledger_normed_full(s, A, port);
+
+  /* reward shaping, n = 1 (nstep_buffer.py; replay_buffer.py:68-80) */
+  int D = (c->reward_mode == ORC_REWARD_AGENT_PER_ASSET) ? A : 1;
+  double rin[MAXA];
+  if (c->reward_mode == ORC_REWARD_ENV_LOG) rin[0] = reward;
+  else if (c->reward_mode == ORC_REWARD_AGENT_SUM) rin[0] = ar_sum;
+  else for (int i = 0; i < A; ++i) rin[i] = ar[i];
+  double shaped[MAXA];
+  const double one = 1.0;
+  if (c->shaper == ORC_SHAPER_DSR) orc_dsr(rin, 1, D, &one, c->adaptation_rate, s->sA, s->sB, shaped);
+  else if (c->shaper == ORC_SHAPER_DDR) orc_ddr(rin, 1, D, &one, c->adaptation_rate, s->sA, s->sB, shaped);
+  else if (c->shaper == ORC_SHAPER_PPC) {  /* cosine_port_shaper :182-204 */
+    double cs = cosine_sim(port, c->desired_portfolio, A + 1);
+    for (int d = 0; d < D; ++d) shaped[d] = 1.0 * (rin[d] + c->cosine_temp * cs);
+  } else for (int d = 0; d < D; ++d) shaped[d] = rin[d];
+
+  /* outputs */
+  size_t eA = (size_t)e * A;
+  if (o->reward) o->reward[e] = reward;
+  if (o->agent_reward) {
+    if (D == 1) o->agent_reward[e] = rin[0];
+    else for (int i = 0; i < A; ++i) o->agent_reward[eA + i] = ar[i];
+  }
+  if (o->shaped) {
+    if (D == 1) o->shaped[e] = shaped[0];
+    else for (int i = 0; i < A; ++i) o->shaped[eA + i] = shaped[i];
+  }
+  if (o->done) o->done[e] = (uint8_t)done;
+  if (o->obs_price) for (int i = 0; i < A; ++i) o->obs_price[eA + i] = s->P[i];
+  if (o->obs_port) for (int i = 0; i <= A; ++i) o->obs_port[(size_t)e * (A + 1) + i] = port[i];
+  if (o->timestamp) o->timestamp[e] = s->ts;
+  for (int i = 0; i < A; ++i) {
+    if (o->tprice) o->tprice[eA + i] = tp[i];
+    if (o->tunits) o->tunits[eA + i] = tu[i];
+    if (o->tcost) o->tcost[eA + i] = tc[i];
+    if (o->risk) o->risk[eA + i] = (uint8_t)risk[i];
+  }
+  if (o->margin_call) o->margin_call[e] = (uint8_t)marginCall;
+
+  /* episode statistics */
+  s->ep_ret += reward;
+  s->ep_len += 1;
+  if (done) {
+    s->last_ret = s->ep_ret; s->last_len = s->ep_len; s->last_eq = currentEq;
+    s->n_done += 1; s->ep_ret = 0; s->ep_len = 0;
+  }
+  window_stream(b, e);                       /* agent streams next_state (:193) */
+  if (done && c->auto_reset) env_reset_one(b, e);  /* agent reset_state (:199-201) */
+}
+
+void orc_step(orc_batch *b, int kind, const double *units, const int32_t *asset_idx,
+              const orc_out *out) {
+  for (int e = 0; e < b->N; ++e) {
+    if (kind == ORC_STEP_UNITS) step_one(b, e, kind, units + (size_t)e * b->A, 0, 0., out);
+    else if (kind == ORC_STEP_SINGLE) step_one(b, e, kind, NULL, asset_idx[e], units[e], out);
+    else step_one(b, e, kind, NULL, 0, 0., out);
+  }
+}
+
+/* DQN.action_to_transaction -- dqn.py:160-179 */
+static void action_to_units_one(const orc_batch *b, int e, const int8_t *act, double *units) {
+  const orc_env *s = &b->envs[e];
+  int A = b->A;
+  double avM = p_available_margin(s, A, b->cfg.required_margin);
+  int half = b->cfg.action_atoms / 2;
+  for (int i = 0; i < A; ++i) {
+    double u = b->cfg.unit_size * avM / s->P[i];
+    double centered = (double)(act[i] - half);
+    units[i] = centered * u;
+    if (act[i] == 0) units[i] = (s->L[i] != 0) ? -s->L[i] : 0.;
+  }
+}
+
+void orc_action_to_units(orc_batch *b, const int8_t *actions, double *units) {
+  for (int e = 0; e < b->N; ++e)
+    action_to_units_one(b, e, actions + (size_t)e * b->A, units + (size_t)e * b->A);
+}
+
+static double *offs_d(double *p, size_t off) { return p ? p + off : NULL; }
+static uint8_t *offs_u8(uint8_t *p, size_t off) { return p ? p + off : NULL; }
+
+void orc_rollout(orc_batch *b, const int8_t *actions, int k_steps, const orc_out *out) {
+  int N = b->N, A = b->A;
+  int D = (b->cfg.reward_mode == ORC_REWARD_AGENT_PER_ASSET) ? A : 1;
+  double units[MAXA];
+  for (int k = 0; k < k_steps; ++k) {
+    size_t nA = (size_t)k * N * A, nN = (size_t)k * N;
+    orc_out o = *out;
+    o.reward = offs_d(out->reward, nN);
+    o.agent_reward = offs_d(out->agent_reward, nN * D);
+    o.shaped = offs_d(out->shaped, nN * D);
+    o.done = offs_u8(out->done, nN);
+    o.obs_price = offs_d(out->obs_price, nA);
+    o.obs_port = offs_d(out->obs_port, (size_t)k * N * (A + 1));
+    o.timestamp = out->timestamp ? out->timestamp + nN : NULL;
+    o.tprice = offs_d(out->tprice, nA);
+    o.tunits = offs_d(out->tunits, nA);
+    o.tcost = offs_d(out->tcost, nA);
+    o.risk = offs_u8(out->risk, nA);
+    o.margin_call = offs_u8(out->margin_call, nN);
+    for (int e = 0; e < N; ++e) {
+      action_to_units_one(b, e, actions + nA + (size_t)e * A, units);
+      step_one(b, e, ORC_STEP_UNITS, units, 0, 0., &o);
+    }
+  }
+}
+
+/* ---- state access -------------------------------------------------------- */
+
+void orc_get_field(const orc_batch *b, int field, double *out) {
+  for (int e = 0; e < b->N; ++e) {
+    const orc_env *s = &b->envs[e];
+    for (int i = 0; i < b->A; ++i) {
+      double v = 0.;
+      switch (field) {
+        case ORC_F_LEDGER: v = s->L[i]; break;
+        case ORC_F_MEP: v = s->mep[i]; break;
+        case ORC_F_BORROWED: v = s->Bm[i]; break;
+        case ORC_F_PRICE: v = s->P[i]; break;
+        case ORC_F_SINE_X: v = s->x[i]; break;
+        case ORC_F_OU_MEAN: v = s->ouMean[i]; break;
+        case ORC_F_DY: v = s->dY[i]; break;
+        case ORC_F_TLEN: v = s->tlen[i]; break;
+        case ORC_F_TRENDING: v = s->trending[i]; break;
+        case ORC_F_DIR: v = s->dir[i]; break;
+        case ORC_F_SHAPER_A: v = s->sA[i]; break;
+        case ORC_F_SHAPER_B: v = s->sB[i]; break;
+      }
+      out[(size_t)e * b->A + i] = v;
+    }
+  }
+}
+
+void orc_set_field(orc_batch *b, int field, const double *in) {
+  for (int e = 0; e < b->N; ++e) {
+    orc_env *s = &b->envs[e];
+    for (int i = 0; i < b->A; ++i) {
+      double v = in[(size_t)e * b->A + i];
+      switch (field) {
+        case ORC_F_LEDGER: s->L[i] = v; break;
+        case ORC_F_MEP: s->mep[i] = v; break;
+        case ORC_F_BORROWED: s->Bm[i] = v; break;
+        case ORC_F_PRICE: s->P[i] = v; break;
+        case ORC_F_SINE_X: s->x[i] = v; break;
+        case ORC_F_OU_MEAN: s->ouMean[i] = v; break;
+        case ORC_F_DY: s->dY[i] = v; break;
+        case ORC_F_TLEN: s->tlen[i] = (int32_t)v; break;
+        case ORC_F_TRENDING: s->trending[i] = (uint8_t)v; break;
+        case ORC_F_DIR: s->dir[i] = (int8_t)v; break;
+        case ORC_F_SHAPER_A: s->sA[i] = v; break;
+        case ORC_F_SHAPER_B: s->sB[i] = v; break;
+      }
+    }
+  }
+}
+
+void orc_get_scalar(const orc_batch *b, int which, double *out) {
+  const int A = b->A;
+  for (int e = 0; e < b->N; ++e) {
+    const orc_env *s = &b->envs[e];
+    double v = 0.;
+    switch (which) {
+      case ORC_S_CASH: v = s->cash; break;
+      case ORC_S_EQUITY: v = p_equity(s, A); break;
+      case ORC_S_PNL: v = p_pnl(s, A); break;
+      case ORC_S_BALANCE: v = p_balance(s, A); break;
+      case ORC_S_AVAILABLE_MARGIN: v = p_available_margin(s, A, b->cfg.required_margin); break;
+      case ORC_S_USED_MARGIN: v = p_used_margin(s, A, b->cfg.required_margin); break;
+      case ORC_S_BORROWED_MARGIN: v = p_borrowed_margin(s, A); break;
+      case ORC_S_BORROWED_ASSET_VALUE: v = p_borrowed_asset_value(s, A); break;
+      case ORC_S_ASSET_VALUE: v = p_asset_value(s, A); break;
+      case ORC_S_TIMESTAMP: v = (double)s->ts; break;
+      case ORC_S_CHECK_RISK: v = p_check_risk(s, A, b->cfg.maintenance_margin); break;
+      case ORC_S_SHAPER_A: v = s->sA[0]; break;
+      case ORC_S_SHAPER_B: v = s->sB[0]; break;
+      case ORC_S_EP_RET: v = s->ep_ret; break;
+      case ORC_S_EP_LEN: v = s->ep_len; break;
+      case ORC_S_LAST_RET: v = s->last_ret; break;
+      case ORC_S_LAST_LEN: v = s->last_len; break;
+      case ORC_S_LAST_EQUITY: v = s->last_eq; break;
+      case ORC_S_N_DONE: v = s->n_done; break;
+    }
+    out[e] = v;
+  }
+}
+
+void orc_set_cash(orc_batch *b, const double *cash) {
+  for (int e = 0; e < b->N; ++e) b->envs[e].cash = cash[e];
+}
+
+void orc_port_handle_transaction(orc_batch *b, int e, int asset, double tprice, double units,
+                                 double cost) {
+  p_handle_transaction(&b->envs[e], b->cfg.required_margin, asset, tprice, units, cost);
+}
+int orc_port_check_risk(const orc_batch *b, int e) {
+  return p_check_risk(&b->envs[e], b->A, b->cfg.maintenance_margin);
+}
+int orc_port_check_risk_order(const orc_batch *b, int e, int asset, double units) {
+  return p_check_risk_order(&b->envs[e], b->A, b->cfg.required_margin, b->cfg.maintenance_margin,
+                            asset, units);
+}
+void orc_port_ledger_normed_full(const orc_batch *b, int e, double *out) {
+  p_ledger_normed_full(&b->envs[e], b->A, out);
+}
+void orc_broker_handle_transaction(orc_batch *b, int e, int asset, double units, double *resp) {
+  int r;
+  b_handle_transaction(&b->cfg, &b->envs[e], b->A, asset, units, &resp[0], &resp[1], &resp[2], &r);
+  resp[3] = r;
+}
+
+/* ---- window output (StackerDiscrete.current_data, preprocessor.py:177-185) */
+
+void orc_window_stream(orc_batch *b) {
+  for (int e = 0; e < b->N; ++e) window_stream(b, e);
+}
+
+void orc_window(const orc_batch *b, double *price, double *port, uint64_t *ts) {
+  int W = b->cfg.window, A = b->A, R = 2 * A + 1;
+  if (W <= 0) return;
+  for (int e = 0; e < b->N; ++e) {
+    const orc_env *s = &b->envs[e];
+    int len = s->wlen;
+    double *xp = price ? price + (size_t)e * W * A : NULL;
+    /* rows oldest -> newest; an underfull deque yields len rows (rest zero) */
+    for (int w = 0; w < W; ++w) {
+      int valid = w < len;
+      int h = (s->whead - (len - 1) + w + W * 2) % W;
+      const double *row = s->ring + (size_t)h * R;
+      if (xp)
+        for (int i = 0; i < A; ++i) xp[(size_t)w * A + i] = valid ? row[i] : 0.;
+      if (port)
+        for (int i = 0; i <= A; ++i)
+          port[((size_t)e * W + w) * (A + 1) + i] = valid ? row[A + i] : 0.;
+      if (ts) ts[(size_t)e * W + w] = valid ? s->ring_ts[h] : 0;
+    }
+    if (!price) continue;
+    int nt = b->cfg.norm_type;
+    if (nt == ORC_NORM_LOG) {                       /* log_norm :79-81 */
+      for (int w = 0; w < len; ++w)
+        for (int i = 0; i < A; ++i) {
+          double v = xp[(size_t)w * A + i];
+          xp[(size_t)w * A + i] = log((v < 1e-5) ? 1e-5 : v);
+        }
+    } else if (nt == ORC_NORM_LOOKBACK || nt == ORC_NORM_LOOKBACK_LOG) { /* :63-66 */
+      for (int i = 0; i < A; ++i) {
+        double last = xp[(size_t)(len - 1) * A + i];
+        for (int w = 0; w < len; ++w) {
+          double v = xp[(size_t)w * A + i] / last;
+          xp[(size_t)w * A + i] = (nt == ORC_NORM_LOOKBACK_LOG) ? log(v) : v;
+        }
+      }
+    } else if (nt == ORC_NORM_STANDARD_NORMAL) {    /* standard_norm :83-92 */
+      for (int i = 0; i < A; ++i) {
+        double sum = 0.;
+        for (int w = 0; w < len; ++w) sum += xp[(size_t)w * A + i];
+        double mean = sum / len;
+        double ss = 0.;
+        for (int w = 0; w < len; ++w) {
+          double d = xp[(size_t)w * A + i] - mean;
+          ss += d * d;
+        }
+        double sd = sqrt(ss / len);
+        for (int w = 0; w < len; ++w) {
+          double v = (xp[(size_t)w * A + i] - mean) / sd;
+          if (v != v) v = 0.;                       /* np.nan_to_num */
+          else if (v == INFINITY) v = 1.7976931348623157e308;
+          else if (v == -INFINITY) v = -1.7976931348623157e308;
+          xp[(size_t)w * A + i] = v;
+        }
+      }
+    }
+  }
+}

@@ -1,0 +1,275 @@
+"""ctypes front-end of the C oracle (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module.  The product package (madigan_amd) never does.
+
+The config dictionary understood here is the same one madigan_amd's
+BatchedEnv takes (see madigan_amd/config.py), so a parity test builds both
+sides from one dict.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD = os.path.join(HERE, "_build")
+MAXA = 64
+
+GREEN, INSUFF_MARGIN, MARGIN_CALL, BLOWN_OUT = 0, 1, 2, 3
+SRC_EXTERNAL, SRC_SINE, SRC_OU, SRC_TRENDOU = 0, 1, 2, 3
+SHAPERS = {"none": 0, None: 0, "None": 0, "DSR": 1, "DDR": 2, "PPC": 3, "cosine": 3,
+           "cosine_similarity": 3, "cosine_port_shaper": 3}
+REWARD_MODES = {"env_log": 0, "agent_sum": 1, "agent_per_asset": 2}
+NORMS = {None: 0, "none": 0, "log": 1, "lookback": 2, "standard_normal": 3, "lookback_log": 4}
+STEP_NONE, STEP_UNITS, STEP_SINGLE = 0, 1, 2
+
+F_LEDGER, F_MEP, F_BORROWED, F_PRICE, F_SINE_X, F_OU_MEAN, F_DY, F_TLEN, F_TRENDING, F_DIR, \
+    F_SHAPER_A, F_SHAPER_B = range(12)
+S_NAMES = ["cash", "equity", "pnl", "balance", "availableMargin", "usedMargin", "borrowedMargin",
+           "borrowedAssetValue", "assetValue", "timestamp", "checkRisk", "shaperA", "shaperB",
+           "ep_ret", "ep_len", "last_ret", "last_len", "last_equity", "n_done"]
+
+
+class AssetSrc(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("pad_", C.c_int32), ("p", C.c_double * 12)]
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("n_envs", C.c_int32), ("n_assets", C.c_int32), ("env_offset", C.c_int64),
+        ("seed", C.c_uint64), ("init_cash", C.c_double), ("required_margin", C.c_double),
+        ("maintenance_margin", C.c_double), ("slippage_rel", C.c_double),
+        ("slippage_abs", C.c_double), ("tc_rel", C.c_double), ("tc_abs", C.c_double),
+        ("shaper", C.c_int32), ("reward_mode", C.c_int32), ("adaptation_rate", C.c_double),
+        ("cosine_temp", C.c_double), ("desired_portfolio", C.c_double * (MAXA + 1)),
+        ("window", C.c_int32), ("norm_type", C.c_int32), ("auto_reset", C.c_int32),
+        ("action_atoms", C.c_int32), ("unit_size", C.c_double),
+    ]
+
+
+class Out(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in (
+        "reward", "agent_reward", "shaped", "done", "obs_price", "obs_port", "timestamp",
+        "tprice", "tunits", "tcost", "risk", "margin_call")]
+
+
+_LIB = {}
+
+
+def build(fast: bool = False) -> str:
+    name = "libmadigan_oracle_fast.so" if fast else "libmadigan_oracle.so"
+    path = os.path.join(BUILD, name)
+    srcs = [os.path.join(HERE, f) for f in ("madigan_oracle.c", "madigan_oracle.h")]
+    if not os.path.exists(path) or any(os.path.getmtime(s) > os.path.getmtime(path) for s in srcs):
+        subprocess.run(["make", "-s", "-C", HERE, os.path.join("_build", name)], check=True)
+    return path
+
+
+def lib(fast: bool = False):
+    if fast not in _LIB:
+        L = C.CDLL(build(fast))
+        P = C.c_void_p
+        L.orc_create.restype = P
+        L.orc_create.argtypes = [C.POINTER(Config), C.POINTER(AssetSrc)]
+        L.orc_destroy.argtypes = [P]
+        L.orc_reset.argtypes = [P, P]
+        L.orc_step.argtypes = [P, C.c_int, P, P, C.POINTER(Out)]
+        L.orc_rollout.argtypes = [P, P, C.c_int, C.POINTER(Out)]
+        L.orc_action_to_units.argtypes = [P, P, P]
+        L.orc_set_prices.argtypes = [P, P]
+        L.orc_get_field.argtypes = [P, C.c_int, P]
+        L.orc_set_field.argtypes = [P, C.c_int, P]
+        L.orc_get_scalar.argtypes = [P, C.c_int, P]
+        L.orc_set_cash.argtypes = [P, P]
+        L.orc_port_handle_transaction.argtypes = [P, C.c_int, C.c_int, C.c_double, C.c_double,
+                                                  C.c_double]
+        L.orc_port_check_risk.argtypes = [P, C.c_int]
+        L.orc_port_check_risk.restype = C.c_int
+        L.orc_port_check_risk_order.argtypes = [P, C.c_int, C.c_int, C.c_double]
+        L.orc_port_check_risk_order.restype = C.c_int
+        L.orc_port_ledger_normed_full.argtypes = [P, C.c_int, P]
+        L.orc_broker_handle_transaction.argtypes = [P, C.c_int, C.c_int, C.c_double, P]
+        L.orc_window.argtypes = [P, P, P, P]
+        L.orc_window_stream.argtypes = [P]
+        for fn in (L.orc_dsr, L.orc_ddr):
+            fn.argtypes = [P, C.c_int, C.c_int, P, C.c_double, P, P, P]
+        L.orc_philox4x32_10.argtypes = [P, P, P]
+        for fn in (L.orc_log, L.orc_sin, L.orc_cos2pi):
+            fn.argtypes = [C.c_double]
+            fn.restype = C.c_double
+        L.orc_normal.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64]
+        L.orc_normal.restype = C.c_double
+        L.orc_uniform2.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64,
+                                   P, P]
+        L.orc_canon_sum.argtypes = [P, C.c_int]
+        L.orc_canon_sum.restype = C.c_double
+        _LIB[fast] = L
+    return _LIB[fast]
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def make_srcs(sources):
+    """sources: list of (kind, params) for each asset in order."""
+    arr = (AssetSrc * MAXA)()
+    for i, (kind, params) in enumerate(sources):
+        arr[i].kind = kind
+        for j, v in enumerate(params):
+            arr[i].p[j] = float(v)
+    return arr
+
+
+class OracleBatch:
+    """N independent reference Envs (one C object per env)."""
+
+    def __init__(self, cfg: dict, sources, fast: bool = False):
+        self.L = lib(fast)
+        c = Config()
+        self.N = c.n_envs = int(cfg["n_envs"])
+        self.A = c.n_assets = len(sources)
+        c.env_offset = int(cfg.get("env_offset", 0))
+        c.seed = int(cfg.get("seed", 0))
+        c.init_cash = float(cfg.get("init_cash", 1_000_000))
+        c.required_margin = float(cfg.get("required_margin", 1.0))
+        c.maintenance_margin = float(cfg.get("maintenance_margin", 0.25))
+        c.slippage_rel = float(cfg.get("slippage_rel", 0.0))
+        c.slippage_abs = float(cfg.get("slippage_abs", 0.0))
+        c.tc_rel = float(cfg.get("transaction_cost_rel", 0.0))
+        c.tc_abs = float(cfg.get("transaction_cost_abs", 0.0))
+        c.shaper = SHAPERS[cfg.get("reward_shaper", None)]
+        c.reward_mode = REWARD_MODES[cfg.get("reward_mode", "env_log")]
+        c.adaptation_rate = float(cfg.get("adaptation_rate", 0.001))
+        c.cosine_temp = float(cfg.get("cosine_temp", 0.0))
+        dp = cfg.get("desired_portfolio", [1.0] + [0.0] * self.A)
+        for i, v in enumerate(dp):
+            c.desired_portfolio[i] = float(v)
+        c.window = int(cfg.get("window", 0))
+        c.norm_type = NORMS[cfg.get("norm_type", None)]
+        c.auto_reset = int(cfg.get("auto_reset", 0))
+        c.action_atoms = int(cfg.get("action_atoms", 3))
+        c.unit_size = float(cfg.get("unit_size", 0.05))
+        self.cfg = c
+        self.W = c.window
+        self.D = self.A if c.reward_mode == 2 else 1
+        self._srcs = make_srcs(sources)
+        self.h = self.L.orc_create(C.byref(c), self._srcs)
+        if not self.h:
+            raise ValueError("orc_create rejected the configuration")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.orc_destroy(self.h)
+            self.h = None
+
+    # -- outputs ---------------------------------------------------------
+    def _alloc_out(self, K=None):
+        N, A, D = self.N, self.A, self.D
+        pre = () if K is None else (K,)
+        o = dict(
+            reward=np.zeros(pre + (N,)), agent_reward=np.zeros(pre + ((N,) if D == 1 else (N, A))),
+            shaped=np.zeros(pre + ((N,) if D == 1 else (N, A))), done=np.zeros(pre + (N,), np.uint8),
+            obs_price=np.zeros(pre + (N, A)), obs_port=np.zeros(pre + (N, A + 1)),
+            timestamp=np.zeros(pre + (N,), np.uint64), tprice=np.zeros(pre + (N, A)),
+            tunits=np.zeros(pre + (N, A)), tcost=np.zeros(pre + (N, A)),
+            risk=np.zeros(pre + (N, A), np.uint8), margin_call=np.zeros(pre + (N,), np.uint8))
+        s = Out(**{k: _ptr(v) for k, v in o.items()})
+        return o, s
+
+    def step(self, units=None, asset_idx=None):
+        o, s = self._alloc_out()
+        if units is None:
+            self.L.orc_step(self.h, STEP_NONE, None, None, C.byref(s))
+        elif asset_idx is None:
+            u = np.ascontiguousarray(units, dtype=np.float64).reshape(self.N, self.A)
+            self.L.orc_step(self.h, STEP_UNITS, _ptr(u), None, C.byref(s))
+        else:
+            u = np.ascontiguousarray(units, dtype=np.float64).reshape(self.N)
+            ix = np.ascontiguousarray(asset_idx, dtype=np.int32).reshape(self.N)
+            self.L.orc_step(self.h, STEP_SINGLE, _ptr(u), _ptr(ix), C.byref(s))
+        return o
+
+    def rollout(self, actions):
+        a = np.ascontiguousarray(actions, dtype=np.int8)
+        K = a.shape[0]
+        o, s = self._alloc_out(K)
+        self.L.orc_rollout(self.h, _ptr(a), K, C.byref(s))
+        return o
+
+    def action_to_units(self, actions):
+        a = np.ascontiguousarray(actions, dtype=np.int8).reshape(self.N, self.A)
+        u = np.zeros((self.N, self.A))
+        self.L.orc_action_to_units(self.h, _ptr(a), _ptr(u))
+        return u
+
+    def reset(self, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        self.L.orc_reset(self.h, _ptr(m))
+
+    def set_prices(self, prices):
+        p = np.ascontiguousarray(prices, dtype=np.float64).reshape(self.N, self.A)
+        self.L.orc_set_prices(self.h, _ptr(p))
+
+    # -- state -------------------------------------------------------------
+    def field(self, f):
+        out = np.zeros((self.N, self.A))
+        self.L.orc_get_field(self.h, f, _ptr(out))
+        return out
+
+    def set_field(self, f, values):
+        v = np.ascontiguousarray(np.broadcast_to(values, (self.N, self.A)), dtype=np.float64)
+        self.L.orc_set_field(self.h, f, _ptr(v))
+
+    def scalar(self, name):
+        out = np.zeros(self.N)
+        self.L.orc_get_scalar(self.h, S_NAMES.index(name), _ptr(out))
+        return out
+
+    def set_cash(self, cash):
+        v = np.ascontiguousarray(np.broadcast_to(cash, (self.N,)), dtype=np.float64)
+        self.L.orc_set_cash(self.h, _ptr(v))
+
+    def window(self):
+        W, N, A = self.W, self.N, self.A
+        price = np.zeros((N, W, A))
+        port = np.zeros((N, W, A + 1))
+        ts = np.zeros((N, W), np.uint64)
+        self.L.orc_window(self.h, _ptr(price), _ptr(port), _ptr(ts))
+        return price, port, ts
+
+    def window_stream(self):
+        self.L.orc_window_stream(self.h)
+
+    # Portfolio / Broker level hooks (env e)
+    def port_handle_transaction(self, e, asset, tprice, units, cost=0.0):
+        self.L.orc_port_handle_transaction(self.h, e, asset, tprice, units, cost)
+
+    def port_check_risk(self, e=0, asset=None, units=None):
+        if asset is None:
+            return self.L.orc_port_check_risk(self.h, e)
+        return self.L.orc_port_check_risk_order(self.h, e, asset, units)
+
+    def ledger_normed_full(self, e=0):
+        out = np.zeros(self.A + 1)
+        self.L.orc_port_ledger_normed_full(self.h, e, _ptr(out))
+        return out
+
+    def broker_handle_transaction(self, e, asset, units):
+        r = np.zeros(4)
+        self.L.orc_broker_handle_transaction(self.h, e, asset, units, _ptr(r))
+        return r
+
+
+def dsr(rewards, discounts, eta, A, B, ddr=False):
+    r = np.ascontiguousarray(rewards, dtype=np.float64)
+    L_, D = r.shape
+    d = np.ascontiguousarray(discounts, dtype=np.float64)
+    out = np.zeros(D)
+    fn = lib().orc_ddr if ddr else lib().orc_dsr
+    fn(_ptr(r), L_, D, _ptr(d), eta, _ptr(A), _ptr(B), _ptr(out))
+    return out

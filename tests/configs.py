@@ -1,0 +1,38 @@
+"""Shared workload definitions (BASELINE.json configs) for tests and bench."""
+from oracle import oracle as O
+
+SYNTH_KAT = {  # madigan/environments/cpp/tests/envTest.py:11-21
+    "data_source_type": "Synth",
+    "data_source_config": {"freq": [1., 0.3, 2., 0.5], "mu": [2., 2.1, 2.2, 2.3],
+                           "amp": [1., 1.2, 1.3, 1.0], "phase": [0., 1.0, 2., 1.],
+                           "dX": 0.01, "noise": 0.},
+}
+
+# C2: OU mu=10 theta=.08 phi=.04 per asset (scripts/ou_ddr_.001_nstep20.yaml:84-98)
+def ou_sources(A, mean=10.0, theta=0.08, phi=0.04):
+    return [(O.SRC_OU, [mean, theta, phi])] * A
+
+
+# C3: TrendOU (config.yaml:116-138)
+TRENDOU_P = [0.001, 100, 500, 0.001, 0.005, 5.0, 0.15, 0.04, 0.001, 0.99]
+
+
+def trendou_sources(A, params=None):
+    return [(O.SRC_TRENDOU, list(params or TRENDOU_P))] * A
+
+
+def sine_sources(freq, mu, amp, phase, dX=0.01, noise=0.0):
+    return [(O.SRC_SINE, [f, m, a, p, dX, noise]) for f, m, a, p in zip(freq, mu, amp, phase)]
+
+
+# C4: Composite = Synth(2) + OU(3) + TrendOU(3)
+def composite_sources():
+    return (sine_sources([1., 0.3], [2., 2.1], [1., 1.2], [0., 1.], 0.01, 0.0)
+            + [(O.SRC_OU, [10.0, 0.15, 0.04])] * 3 + trendou_sources(3))
+
+
+def spec_from_sources(sources):
+    """madigan_amd SourceSpec from the oracle's (kind, params) list."""
+    from madigan_amd.config import SourceSpec
+    return SourceSpec(kinds=[k for k, _ in sources], params=[list(map(float, p)) for _, p in sources],
+                      assets=[f"a{i}" for i in range(len(sources))])

@@ -223,10 +223,6 @@ typedef struct {
   double sA[MAXA], sB[MAXA];
   /* episode statistics */
   double ep_ret, ep_len, last_ret, last_len, last_eq, n_done;
-  /* StackerDiscrete deques (preprocessor.py:150-152) */
-  double *ring;          /* W rows of (A + A+1) */
-  uint64_t *ring_ts;
-  int wlen, whead;
 } orc_env;
 
 struct orc_batch {
@@ -235,6 +231,7 @@ struct orc_batch {
   int N, A;
   orc_env *envs;
   double *ext;  /* (N,A) external prices */
+  orc_ring ring; /* StackerDiscrete deques (preprocessor.py:150-152), F = A, P = A+1 */
 };
 
 /* ---- Portfolio valuation (Portfolio.cpp:170-235) ------------------------ */
@@ -453,6 +450,7 @@ static void src_init(orc_batch *b, int e) {
   orc_env *s = &b->envs[e];
   for (int i = 0; i < b->A; ++i) {
     const double *p = b->src[i].p;
+    s->dir[i] = 1;
     switch (b->src[i].kind) {
       case ORC_SRC_SINE: s->x[i] = p[3]; s->P[i] = 0.0; break;        /* :466 */
       case ORC_SRC_OU: s->P[i] = p[0]; break;                           /* :1128 */
@@ -475,23 +473,34 @@ static void env_init_accountants(orc_batch *b, int e) {
 
 /* ---- window (StackerDiscrete) ------------------------------------------- */
 
-static void window_stream(orc_batch *b, int e) {  /* preprocessor.py:172-175 */
-  int W = b->cfg.window;
-  if (W <= 0) return;
-  orc_env *s = &b->envs[e];
-  int A = b->A, R = 2 * A + 1;
-  int h = (s->whead + 1) % W;
-  double *row = s->ring + (size_t)h * R;
-  for (int i = 0; i < A; ++i) row[i] = s->P[i];
-  p_ledger_normed_full(s, A, row + A);
-  s->ring_ts[h] = s->ts;
-  s->whead = h;
-  if (s->wlen < W) s->wlen++;
+/* deque.append on env e's ring (preprocessor.py:172-175) */
+static void ring_push_one(const orc_ring *r, int e, const double *price, const double *port,
+                          uint64_t ts) {
+  int W = r->window, C = r->n_price + r->n_port;
+  int h = (r->head[e] + 1) % W;
+  double *row = r->ring + ((size_t)e * W + h) * C;
+  for (int i = 0; i < r->n_price; ++i) row[i] = price ? price[i] : 0.;
+  for (int i = 0; i < r->n_port; ++i) row[r->n_price + i] = port ? port[i] : 0.;
+  r->ring_ts[(size_t)e * W + h] = ts;
+  r->head[e] = h;
+  if (r->len[e] < W) r->len[e]++;
 }
 
-static void window_clear(orc_batch *b, int e) {  /* reset_state, preprocessor.py:196-199 */
-  b->envs[e].wlen = 0;
-  b->envs[e].whead = b->cfg.window > 0 ? b->cfg.window - 1 : 0;
+static void ring_clear_one(const orc_ring *r, int e) { /* reset_state, preprocessor.py:196-199 */
+  r->len[e] = 0;
+  r->head[e] = r->window - 1;
+}
+
+static void window_stream(orc_batch *b, int e) {
+  if (b->cfg.window <= 0) return;
+  orc_env *s = &b->envs[e];
+  double port[MAXA + 1];
+  p_ledger_normed_full(s, b->A, port);
+  ring_push_one(&b->ring, e, s->P, port, s->ts);
+}
+
+static void window_clear(orc_batch *b, int e) {
+  if (b->cfg.window > 0) ring_clear_one(&b->ring, e);
 }
 
 /* Agent reset: env.reset(); preprocessor.reset_state(); stream_state(state);
@@ -502,7 +511,7 @@ static void env_reset_one(orc_batch *b, int e) {
   if (b->cfg.window > 0) {
     window_clear(b, e);
     window_stream(b, e);
-    while (b->envs[e].wlen < b->cfg.window) {
+    while (b->ring.len[e] < b->cfg.window) {
       src_get_data(b, e);  /* Env::step() with no action: only the tick matters */
       window_stream(b, e);
     }
@@ -566,6 +575,17 @@ static double cosine_sim(const double *p, const double *q, int n) {
   return sum_full(pq, n) / (norm_p * norm_q);
 }
 
+/* cosine_port_shaper (nstep_buffer.py:182-204) over an n-step window:
+ * rewards (L,D), ports (L,P) = next_state.portfolio[-1] rows, target (P). */
+void orc_ppc(const double *rewards, const double *ports, int L, int D, int P, const double *target,
+             double temp, const double *discounts, double *out) {
+  for (int d = 0; d < D; ++d) out[d] = 0.0;
+  for (int k = 0; k < L; ++k) {
+    double cs = cosine_sim(ports + (size_t)k * P, target, P);
+    for (int d = 0; d < D; ++d) out[d] += discounts[k] * (rewards[k * D + d] + temp * cs);
+  }
+}
+
 /* ---- public API ---------------------------------------------------------- */
 
 orc_batch *orc_create(const orc_config *cfg, const orc_asset_src *srcs) {
@@ -578,11 +598,16 @@ orc_batch *orc_create(const orc_config *cfg, const orc_asset_src *srcs) {
   b->envs = (orc_env *)calloc((size_t)b->N, sizeof(orc_env));
   b->ext = (double *)calloc((size_t)b->N * b->A, sizeof(double));
   int W = cfg->window;
+  if (W > 0) {
+    orc_ring *r = &b->ring;
+    r->n_envs = b->N; r->n_price = b->A; r->n_port = b->A + 1; r->window = W;
+    r->norm_type = cfg->norm_type;
+    r->ring = (double *)calloc((size_t)b->N * W * (2 * b->A + 1), sizeof(double));
+    r->ring_ts = (uint64_t *)calloc((size_t)b->N * W, sizeof(uint64_t));
+    r->head = (int32_t *)calloc((size_t)b->N, sizeof(int32_t));
+    r->len = (int32_t *)calloc((size_t)b->N, sizeof(int32_t));
+  }
   for (int e = 0; e < b->N; ++e) {
-    if (W > 0) {
-      b->envs[e].ring = (double *)calloc((size_t)W * (2 * b->A + 1), sizeof(double));
-      b->envs[e].ring_ts = (uint64_t *)calloc((size_t)W, sizeof(uint64_t));
-    }
     window_clear(b, e);
     src_init(b, e);               /* Env::initMembers -> makeDataSource (Env.h:139-148) */
     env_init_accountants(b, e);   /* -> initAccountants (one getData) */
@@ -592,7 +617,7 @@ orc_batch *orc_create(const orc_config *cfg, const orc_asset_src *srcs) {
 
 void orc_destroy(orc_batch *b) {
   if (!b) return;
-  for (int e = 0; e < b->N; ++e) { free(b->envs[e].ring); free(b->envs[e].ring_ts); }
+  free(b->ring.ring); free(b->ring.ring_ts); free(b->ring.head); free(b->ring.len);
   free(b->envs);
   free(b->ext);
   free(b);
@@ -882,60 +907,75 @@ void orc_window_stream(orc_batch *b) {
   for (int e = 0; e < b->N; ++e) window_stream(b, e);
 }
 
-void orc_window(const orc_batch *b, double *price, double *port, uint64_t *ts) {
-  int W = b->cfg.window, A = b->A, R = 2 * A + 1;
-  if (W <= 0) return;
-  for (int e = 0; e < b->N; ++e) {
-    const orc_env *s = &b->envs[e];
-    int len = s->wlen;
-    double *xp = price ? price + (size_t)e * W * A : NULL;
-    /* rows oldest -> newest; an underfull deque yields len rows (rest zero) */
+void orc_ring_push(const orc_ring *r, const double *price, const double *port,
+                   const uint64_t *ts) {
+  for (int e = 0; e < r->n_envs; ++e)
+    ring_push_one(r, e, price ? price + (size_t)e * r->n_price : NULL,
+                  port ? port + (size_t)e * r->n_port : NULL, ts ? ts[e] : 0);
+}
+
+void orc_ring_clear(const orc_ring *r, const uint8_t *mask) {
+  for (int e = 0; e < r->n_envs; ++e)
+    if (!mask || mask[e]) ring_clear_one(r, e);
+}
+
+/* current_data for every env: rows oldest -> newest; an underfull deque yields
+ * len rows (the rest zero); normaliser on the price block only. */
+void orc_ring_gather(const orc_ring *r, double *price, double *port, uint64_t *ts) {
+  const int W = r->window, F = r->n_price, P = r->n_port, C = F + P;
+  for (int e = 0; e < r->n_envs; ++e) {
+    const int len = r->len[e];
+    const double *base = r->ring + (size_t)e * W * C;
+    double *xp = price ? price + (size_t)e * W * F : NULL;
     for (int w = 0; w < W; ++w) {
       int valid = w < len;
-      int h = (s->whead - (len - 1) + w + W * 2) % W;
-      const double *row = s->ring + (size_t)h * R;
+      int h = (r->head[e] - (len - 1) + w + W * 2) % W;
+      const double *row = base + (size_t)h * C;
       if (xp)
-        for (int i = 0; i < A; ++i) xp[(size_t)w * A + i] = valid ? row[i] : 0.;
+        for (int i = 0; i < F; ++i) xp[(size_t)w * F + i] = valid ? row[i] : 0.;
       if (port)
-        for (int i = 0; i <= A; ++i)
-          port[((size_t)e * W + w) * (A + 1) + i] = valid ? row[A + i] : 0.;
-      if (ts) ts[(size_t)e * W + w] = valid ? s->ring_ts[h] : 0;
+        for (int i = 0; i < P; ++i) port[((size_t)e * W + w) * P + i] = valid ? row[F + i] : 0.;
+      if (ts) ts[(size_t)e * W + w] = valid ? r->ring_ts[(size_t)e * W + h] : 0;
     }
-    if (!price) continue;
-    int nt = b->cfg.norm_type;
+    if (!xp || len == 0) continue;
+    int nt = r->norm_type;
     if (nt == ORC_NORM_LOG) {                       /* log_norm :79-81 */
       for (int w = 0; w < len; ++w)
-        for (int i = 0; i < A; ++i) {
-          double v = xp[(size_t)w * A + i];
-          xp[(size_t)w * A + i] = log((v < 1e-5) ? 1e-5 : v);
+        for (int i = 0; i < F; ++i) {
+          double v = xp[(size_t)w * F + i];
+          xp[(size_t)w * F + i] = log((v < 1e-5) ? 1e-5 : v);
         }
     } else if (nt == ORC_NORM_LOOKBACK || nt == ORC_NORM_LOOKBACK_LOG) { /* :63-66 */
-      for (int i = 0; i < A; ++i) {
-        double last = xp[(size_t)(len - 1) * A + i];
+      for (int i = 0; i < F; ++i) {
+        double last = xp[(size_t)(len - 1) * F + i];
         for (int w = 0; w < len; ++w) {
-          double v = xp[(size_t)w * A + i] / last;
-          xp[(size_t)w * A + i] = (nt == ORC_NORM_LOOKBACK_LOG) ? log(v) : v;
+          double v = xp[(size_t)w * F + i] / last;
+          xp[(size_t)w * F + i] = (nt == ORC_NORM_LOOKBACK_LOG) ? log(v) : v;
         }
       }
     } else if (nt == ORC_NORM_STANDARD_NORMAL) {    /* standard_norm :83-92 */
-      for (int i = 0; i < A; ++i) {
+      for (int i = 0; i < F; ++i) {
         double sum = 0.;
-        for (int w = 0; w < len; ++w) sum += xp[(size_t)w * A + i];
+        for (int w = 0; w < len; ++w) sum += xp[(size_t)w * F + i];
         double mean = sum / len;
         double ss = 0.;
         for (int w = 0; w < len; ++w) {
-          double d = xp[(size_t)w * A + i] - mean;
+          double d = xp[(size_t)w * F + i] - mean;
           ss += d * d;
         }
         double sd = sqrt(ss / len);
         for (int w = 0; w < len; ++w) {
-          double v = (xp[(size_t)w * A + i] - mean) / sd;
+          double v = (xp[(size_t)w * F + i] - mean) / sd;
           if (v != v) v = 0.;                       /* np.nan_to_num */
           else if (v == INFINITY) v = 1.7976931348623157e308;
           else if (v == -INFINITY) v = -1.7976931348623157e308;
-          xp[(size_t)w * A + i] = v;
+          xp[(size_t)w * F + i] = v;
         }
       }
     }
   }
+}
+
+void orc_window(const orc_batch *b, double *price, double *port, uint64_t *ts) {
+  if (b->cfg.window > 0) orc_ring_gather(&b->ring, price, port, ts);
 }

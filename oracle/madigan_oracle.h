@@ -100,6 +100,17 @@ typedef struct {
   uint8_t *margin_call;  /* (N) */
 } orc_out;
 
+/* StackerDiscrete deques of N envs: ring (N,W,F+P), ring_ts (N,W), head/len (N) */
+typedef struct {
+  int32_t n_envs, n_price, n_port, window, norm_type, pad_;
+  double *ring;
+  uint64_t *ring_ts;
+  int32_t *head, *len;
+} orc_ring;
+void orc_ring_push(const orc_ring *r, const double *price, const double *port, const uint64_t *ts);
+void orc_ring_clear(const orc_ring *r, const uint8_t *mask);
+void orc_ring_gather(const orc_ring *r, double *price, double *port, uint64_t *ts);
+
 typedef struct orc_batch orc_batch;
 
 orc_batch *orc_create(const orc_config *cfg, const orc_asset_src *srcs);
@@ -155,6 +166,9 @@ void orc_dsr(const double *rewards, int L, int D, const double *discounts,
              double eta, double *A, double *B, double *out);
 void orc_ddr(const double *rewards, int L, int D, const double *discounts,
              double eta, double *A, double *B, double *out);
+
+void orc_ppc(const double *rewards, const double *ports, int L, int D, int P, const double *target,
+             double temp, const double *discounts, double *out);
 
 /* RNG + deterministic math shared (by specification) with the device path */
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

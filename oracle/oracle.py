@@ -97,6 +97,7 @@ def lib(fast: bool = False):
         L.orc_window_stream.argtypes = [P]
         for fn in (L.orc_dsr, L.orc_ddr):
             fn.argtypes = [P, C.c_int, C.c_int, P, C.c_double, P, P, P]
+        L.orc_ppc.argtypes = [P, P, C.c_int, C.c_int, C.c_int, P, C.c_double, P, P]
         L.orc_philox4x32_10.argtypes = [P, P, P]
         for fn in (L.orc_log, L.orc_sin, L.orc_cos2pi):
             fn.argtypes = [C.c_double]
@@ -272,4 +273,24 @@ def dsr(rewards, discounts, eta, A, B, ddr=False):
     out = np.zeros(D)
     fn = lib().orc_ddr if ddr else lib().orc_dsr
     fn(_ptr(r), L_, D, _ptr(d), eta, _ptr(A), _ptr(B), _ptr(out))
+    return out
+
+
+def ppc(rewards, ports, target, temp, discounts):
+    r = np.ascontiguousarray(rewards, dtype=np.float64)
+    p = np.ascontiguousarray(ports, dtype=np.float64)
+    L_, D = r.shape
+    P = p.shape[1]
+    t = np.ascontiguousarray(target, dtype=np.float64)
+    d = np.ascontiguousarray(discounts, dtype=np.float64)
+    out = np.zeros(D)
+    lib().orc_ppc(_ptr(r), _ptr(p), L_, D, P, _ptr(t), float(temp), _ptr(d), _ptr(out))
+    return out
+
+
+def philox(ctr, key):
+    c = np.ascontiguousarray(ctr, dtype=np.uint32)
+    k = np.ascontiguousarray(key, dtype=np.uint32)
+    out = np.zeros(4, np.uint32)
+    lib().orc_philox4x32_10(_ptr(c), _ptr(k), _ptr(out))
     return out

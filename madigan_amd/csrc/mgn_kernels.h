@@ -63,18 +63,63 @@ __device__ __forceinline__ double tree(const double (&v)[M]) {
   }
 }
 
+// DPP lane moves (VALU latency, no LDS crossbar).  Controls (gfx9 / gfx950):
+// quad_perm = p0 | p1<<2 | p2<<4 | p3<<6, row_mirror 0x140, row_half_mirror
+// 0x141, row_newbcast:n 0x150+n (broadcast lane n of each 16-lane row).
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = dpp_i32<CTRL>(__double2loint(v));
+  const int hi = dpp_i32<CTRL>(__double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+
+// Segment all-reduce over S aligned lanes.  Every stage pairs each lane with a
+// lane of the sibling block, so every lane ends with the pairwise tree
+// ((v0+v1)+(v2+v3))+((v4+v5)+(v6+v7))... -- the canonical order.
 template <int S>
 __device__ __forceinline__ double seg_sum(double v) {
-#pragma unroll
-  for (int o = 1; o < S; o <<= 1) v = v + __shfl_xor(v, o, 64);
+  if constexpr (S >= 2) v = v + dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  if constexpr (S >= 4) v = v + dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  if constexpr (S >= 8) v = v + dpp_f64<0x141>(v);  // row_half_mirror
+  if constexpr (S >= 16) v = v + dpp_f64<0x140>(v); // row_mirror
+  if constexpr (S >= 32) v = v + __shfl_xor(v, 16, 64);
+  if constexpr (S >= 64) v = v + __shfl_xor(v, 32, 64);
   return v;
 }
 
 template <int S>
 __device__ __forceinline__ int seg_or(int v) {
-#pragma unroll
-  for (int o = 1; o < S; o <<= 1) v = v | __shfl_xor(v, o, 64);
+  if constexpr (S >= 2) v = v | dpp_i32<0xB1>(v);
+  if constexpr (S >= 4) v = v | dpp_i32<0x4E>(v);
+  if constexpr (S >= 8) v = v | dpp_i32<0x141>(v);
+  if constexpr (S >= 16) v = v | dpp_i32<0x140>(v);
+  if constexpr (S >= 32) v = v | __shfl_xor(v, 16, 64);
+  if constexpr (S >= 64) v = v | __shfl_xor(v, 32, 64);
   return v;
+}
+
+// Broadcast lane J of every S-lane segment to the segment (J compile-time).
+template <int S, int J>
+__device__ __forceinline__ double seg_bcast(double v) {
+  if constexpr (S == 1) {
+    return v;
+  } else if constexpr (S == 2) {
+    return dpp_f64<J | (J << 2) | ((2 + J) << 4) | ((2 + J) << 6)>(v);
+  } else if constexpr (S == 4) {
+    return dpp_f64<J * 0x55>(v);
+  } else if constexpr (S == 8) {
+    const double a = dpp_f64<0x150 + J>(v);
+    const double b = dpp_f64<0x150 + 8 + J>(v);
+    return (__lane_id() & 8) ? b : a;
+  } else if constexpr (S == 16) {
+    return dpp_f64<0x150 + J>(v);
+  } else {
+    return __shfl(v, (int)(__lane_id() & ~(S - 1)) + J, 64);
+  }
 }
 
 template <int M, int S>
@@ -297,6 +342,102 @@ __device__ __forceinline__ void store_lane(const Lane<M>& s, const KParams& p, i
   }
 }
 
+
+// One Broker round (Broker.cpp:124-142): asset i = J*M + MM, executed by the
+// owning lane J of every segment after a segment reduction of the portfolio
+// sums; the owner's new cash is then broadcast to its segment.
+template <int M, int S, int J, int MM>
+__device__ __forceinline__ void broker_round(Lane<M>& s, const KParams& p, double& cash,
+                                             const double (&uc)[M], double (&tp)[M],
+                                             double (&tu)[M], double (&tc)[M], int (&rk)[M],
+                                             int ls) {
+  const bool act = (ls == J) && (uc[MM] != 0.);
+  if (__ballot(act) == 0) return;
+  const Sums q = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
+  const double pnl = q.lp - q.ml;
+  const double balance = cash + q.sh;
+  const double availM = (balance + pnl) / p.reqM;
+  if (act) {
+    const double u = uc[MM];
+    const double cur = s.L[MM];
+    const double price = s.P[MM];
+    int risk;  // Portfolio::checkRisk(i, u), Portfolio.cpp:254-279
+    if (signbit(u) != signbit(cur)) {
+      risk = MGN_GREEN;
+      if (u > -1 * cur) {
+        const double excess = u + cur;
+        if (availM <= fabs(price * excess) || balance <= 0.) risk = MGN_INSUFF_MARGIN;
+      }
+    } else {
+      const double equity = (cash + q.lp) - q.b;
+      const double mr = p.mainM * pnl;
+      if ((equity <= -mr) || ((balance + pnl) <= -mr)) risk = MGN_MARGIN_CALL;
+      else if (availM <= fabs(price * u) || balance <= 0.) risk = MGN_INSUFF_MARGIN;
+      else risk = MGN_GREEN;
+    }
+    rk[MM] = risk;
+    if (risk == MGN_GREEN) {  // Broker.cpp:128-135
+      const double slippage = (price * p.slip_rel) + p.slip_abs;
+      const double tprice = u < 0 ? (price - slippage) : (price + slippage);
+      const double tcost = fabs(u * price) * p.tc_rel + p.tc_abs;
+      // Portfolio::handleTransaction, Portfolio.cpp:284-323
+      double units = u;
+      double cu = cur;
+      double me = s.mep[MM];
+      if (signbit(cu) != signbit(units)) {
+        if (fabs(units) > fabs(cu)) {
+          units += cu;
+          cash += cu * tprice;
+          cu = 0.;
+          me = tprice;
+        }
+      } else {
+        me += (tprice - me) * (units / (units + cu));
+      }
+      const double amt = tprice * units;
+      const double use = amt * p.reqM;
+      const double brw = amt - use;
+      double bm = s.Bm[MM];
+      bm += brw;
+      cash -= (use + tcost);
+      cu += units;
+      if (fabs(cu) < 0.000001) {
+        me = 0.;
+        if (bm > 0.) {
+          cash -= bm;
+          bm = 0.;
+        }
+      }
+      if (bm < 0.) {
+        cash -= bm;
+        bm = 0.;
+      }
+      s.L[MM] = cu;
+      s.mep[MM] = me;
+      s.Bm[MM] = bm;
+      tp[MM] = tprice;
+      tu[MM] = u;
+      tc[MM] = tcost;
+    }
+  }
+  cash = seg_bcast<S, J>(cash);
+}
+
+// Rounds in asset order i = 0..A-1 (Broker.cpp:149-155); J, MM compile-time.
+template <int M, int S, int I>
+struct Rounds {
+  static __device__ __forceinline__ void run(Lane<M>& s, const KParams& p, double& cash,
+                                             const double (&uc)[M], double (&tp)[M],
+                                             double (&tu)[M], double (&tc)[M], int (&rk)[M],
+                                             int ls) {
+    if constexpr (I < M * S) {
+      if (I >= p.A) return;
+      broker_round<M, S, I / M, I % M>(s, p, cash, uc, tp, tu, tc, rk, ls);
+      Rounds<M, S, I + 1>::run(s, p, cash, uc, tp, tu, tc, rk, ls);
+    }
+  }
+};
+
 // input selector
 enum { IN_NONE = 0, IN_UNITS = 1, IN_SINGLE = 2, IN_DISCRETE = 3 };
 
@@ -347,7 +488,6 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
   const int ls = tid % S;
   const int env = blockIdx.x * EPB + tid / S;
   if (env >= p.N) return;
-  const int seg_base = (int)(__lane_id()) - ls;
   const int A = p.A;
   const int D = p.D;
 
@@ -429,83 +569,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
       tc[m] = 0.;
       rk[m] = MGN_GREEN;
     }
-    for (int j = 0; j < S; ++j) {
-#pragma unroll
-      for (int m = 0; m < M; ++m) {
-        const int i = j * M + m;
-        if (i >= A) break;
-        const bool act = (ls == j) && (uc[m] != 0.);
-        if (__ballot(act) == 0) continue;
-        const Sums q = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
-        const double pnl = q.lp - q.ml;
-        const double balance = cash + q.sh;
-        const double availM = (balance + pnl) / p.reqM;
-        if (act) {
-          const double u = uc[m];
-          const double cur = s.L[m];
-          const double price = s.P[m];
-          int risk;  // Portfolio::checkRisk(i, u), Portfolio.cpp:254-279
-          if (signbit(u) != signbit(cur)) {
-            risk = MGN_GREEN;
-            if (u > -1 * cur) {
-              const double excess = u + cur;
-              if (availM <= fabs(price * excess) || balance <= 0.) risk = MGN_INSUFF_MARGIN;
-            }
-          } else {
-            const double equity = (cash + q.lp) - q.b;
-            const double mr = p.mainM * pnl;
-            if ((equity <= -mr) || ((balance + pnl) <= -mr)) risk = MGN_MARGIN_CALL;
-            else if (availM <= fabs(price * u) || balance <= 0.) risk = MGN_INSUFF_MARGIN;
-            else risk = MGN_GREEN;
-          }
-          rk[m] = risk;
-          if (risk == MGN_GREEN) {  // Broker.cpp:128-135
-            const double slippage = (price * p.slip_rel) + p.slip_abs;
-            const double tprice = u < 0 ? (price - slippage) : (price + slippage);
-            const double tcost = fabs(u * price) * p.tc_rel + p.tc_abs;
-            // Portfolio::handleTransaction, Portfolio.cpp:284-323
-            double units = u;
-            double cu = cur;
-            double me = s.mep[m];
-            if (signbit(cu) != signbit(units)) {
-              if (fabs(units) > fabs(cu)) {
-                units += cu;
-                cash += cu * tprice;
-                cu = 0.;
-                me = tprice;
-              }
-            } else {
-              me += (tprice - me) * (units / (units + cu));
-            }
-            const double amt = tprice * units;
-            const double use = amt * p.reqM;
-            const double brw = amt - use;
-            double bm = s.Bm[m];
-            bm += brw;
-            cash -= (use + tcost);
-            cu += units;
-            if (fabs(cu) < 0.000001) {
-              me = 0.;
-              if (bm > 0.) {
-                cash -= bm;
-                bm = 0.;
-              }
-            }
-            if (bm < 0.) {
-              cash -= bm;
-              bm = 0.;
-            }
-            s.L[m] = cu;
-            s.mep[m] = me;
-            s.Bm[m] = bm;
-            tp[m] = tprice;
-            tu[m] = u;
-            tc[m] = tcost;
-          }
-        }
-        cash = __shfl(cash, seg_base + j, 64);
-      }
-    }
+    Rounds<M, S, 0>::run(s, p, cash, uc, tp, tu, tc, rk, ls);
     // BrokerResponse.marginCall (Broker.cpp:156-157)
     int mcall = 0;
     if (in_kind != IN_NONE) {

@@ -1,0 +1,67 @@
+"""Multi-GPU sharding of the batched env (one process per GPU).
+
+Envs are independent (no cross-env term anywhere on the step), so
+N_total envs are split contiguously: rank r owns global envs
+[offset_r, offset_r + n_r).  The generators key their Philox streams by the
+global env index (``env_offset``), so a sharded run produces exactly the
+per-env trajectories of a single-device run.  The only collective is an
+all-gather of per-env episode statistics (RCCL over xGMI with the "nccl"
+backend; gloo in CPU tests), issued at log intervals, never per step.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+
+def shard(n_total: int, rank: int, world: int) -> Tuple[int, int]:
+    """(env_offset, n_local) of rank's contiguous slice; remainders go to the
+    lowest ranks so every rank's slice differs by at most one env."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank/world {rank}/{world}")
+    base, rem = divmod(int(n_total), world)
+    n_local = base + (1 if rank < rem else 0)
+    offset = rank * base + min(rank, rem)
+    return offset, n_local
+
+
+def allgather_episode_stats(stats, group=None):
+    """All-gather the (n_local, S) per-env episode statistics of every rank into
+    (n_total, S) in global env order.  Equal shard sizes use one
+    all_gather_into_tensor; ragged shards pad to the largest and trim."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return stats
+    world = dist.get_world_size(group)
+    n_local = torch.tensor([stats.shape[0]], dtype=torch.int64, device=stats.device)
+    sizes = [torch.zeros_like(n_local) for _ in range(world)]
+    dist.all_gather(sizes, n_local, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    n_max = max(sizes)
+    if stats.shape[0] < n_max:
+        pad = torch.zeros((n_max - stats.shape[0],) + tuple(stats.shape[1:]), dtype=stats.dtype,
+                          device=stats.device)
+        stats = torch.cat([stats, pad])
+    out = torch.empty((world * n_max,) + tuple(stats.shape[1:]), dtype=stats.dtype,
+                      device=stats.device)
+    dist.all_gather_into_tensor(out, stats.contiguous(), group=group)
+    if all(s == n_max for s in sizes):
+        return out
+    return torch.cat([out[r * n_max:r * n_max + sizes[r]] for r in range(world)])
+
+
+def summarize(stats):
+    """Episode summary over all envs from gathered (n_total, 4) statistics:
+    {last return, last length, last final equity, done count}."""
+    import torch
+    done = stats[:, 3] > 0
+    n = int(done.sum().item())
+    if n == 0:
+        return {"episodes": int(stats[:, 3].sum().item()), "mean_return": float("nan"),
+                "mean_length": float("nan"), "mean_final_equity": float("nan")}
+    return {"episodes": int(stats[:, 3].sum().item()),
+            "mean_return": float(stats[done, 0].mean().item()),
+            "mean_length": float(stats[done, 1].mean().item()),
+            "mean_final_equity": float(stats[done, 2].mean().item()),
+            "envs_with_episode": n, "std_return": float(torch.std(stats[done, 0]).item())
+            if n > 1 else 0.0}

@@ -294,3 +294,48 @@ def philox(ctr, key):
     out = np.zeros(4, np.uint32)
     lib().orc_philox4x32_10(_ptr(c), _ptr(k), _ptr(out))
     return out
+
+
+class RingStruct(C.Structure):
+    _fields_ = [("n_envs", C.c_int32), ("n_price", C.c_int32), ("n_port", C.c_int32),
+                ("window", C.c_int32), ("norm_type", C.c_int32), ("pad_", C.c_int32),
+                ("ring", C.c_void_p), ("ring_ts", C.c_void_p), ("head", C.c_void_p),
+                ("len", C.c_void_p)]
+
+
+class Ring:
+    """StackerDiscrete deques of N envs on numpy buffers (orc_ring_*)."""
+
+    def __init__(self, n_envs, n_price, n_port, window, norm_type=None):
+        self.L = lib()
+        for fn in (self.L.orc_ring_push, self.L.orc_ring_gather):
+            fn.argtypes = [C.POINTER(RingStruct), C.c_void_p, C.c_void_p, C.c_void_p]
+        self.L.orc_ring_clear.argtypes = [C.POINTER(RingStruct), C.c_void_p]
+        self.N, self.F, self.P, self.W = n_envs, n_price, n_port, window
+        self.ring = np.zeros((n_envs, window, n_price + n_port))
+        self.ts = np.zeros((n_envs, window), np.uint64)
+        self.head = np.full(n_envs, window - 1, np.int32)
+        self.len = np.zeros(n_envs, np.int32)
+        s = RingStruct()
+        s.n_envs, s.n_price, s.n_port, s.window = n_envs, n_price, n_port, window
+        s.norm_type = NORMS[norm_type]
+        s.ring, s.ring_ts = self.ring.ctypes.data, self.ts.ctypes.data
+        s.head, s.len = self.head.ctypes.data, self.len.ctypes.data
+        self.s = s
+
+    def push(self, price, port, ts):
+        p = np.ascontiguousarray(price, dtype=np.float64).reshape(self.N, self.F)
+        q = np.ascontiguousarray(port, dtype=np.float64).reshape(self.N, self.P)
+        t = np.ascontiguousarray(np.broadcast_to(ts, (self.N,)), dtype=np.uint64)
+        self.L.orc_ring_push(C.byref(self.s), _ptr(p), _ptr(q), _ptr(t))
+
+    def clear(self, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        self.L.orc_ring_clear(C.byref(self.s), _ptr(m))
+
+    def gather(self):
+        price = np.zeros((self.N, self.W, self.F))
+        port = np.zeros((self.N, self.W, self.P))
+        ts = np.zeros((self.N, self.W), np.uint64)
+        self.L.orc_ring_gather(C.byref(self.s), _ptr(price), _ptr(port), _ptr(ts))
+        return price, port, ts

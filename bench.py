@@ -41,16 +41,17 @@ def c3_kwargs():
                 unit_size=0.05, auto_reset=True, init_cash=1_000_000.0)
 
 
-def bytes_per_env_step(A: int, fuse: int, D: int = 1) -> float:
+def bytes_per_env_step(A: int, fuse: int, D: int = 1, agent_reward: bool = False) -> float:
     """Algorithmic HBM bytes of the fused step kernel per env-step.
 
-    per step: actions A*1 B read; outputs reward 8, agent_reward 8*D, shaped 8*D,
+    per step: actions A*1 B read; outputs reward 8, shaped 8*D (+ agent_reward 8*D when
+    requested; the C3 workload feeds the env log reward to DDR and does not),
     done 1, obs_price 8A, obs_port 8(A+1), timestamp 8, tprice/tunits/tcost 24A,
     risk A, marginCall 1.  Per launch (amortised over `fuse` steps): state read +
     write of L, meanEntry, borrowed, price, sine_x, ouMean, dY (7*8A), trend len
     4A + flags A, cash 8, timestamp 8, shaper A/B 16*D, running stats 16, plus
     the episode-stat counter read 8 and the stats row write 32."""
-    per_step = A + 8 + 16 * D + 1 + 8 * A + 8 * (A + 1) + 8 + 24 * A + A + 1
+    per_step = A + 8 + 8 * D * (2 if agent_reward else 1) + 1 + 8 * A + 8 * (A + 1) + 8 + 24 * A + A + 1
     state = 2 * (7 * 8 * A + 4 * A + A + 8 + 8 + 16 * D + 16) + 8 + 32
     return per_step + state / fuse
 
@@ -98,6 +99,7 @@ def main():
     ap.add_argument("--fuse", type=int, default=64)
     ap.add_argument("--n-envs", type=int, default=8192, help="envs per GPU")
     ap.add_argument("--assets", type=int, default=8)
+    ap.add_argument("--layout", type=int, default=0, help="assets per lane (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
@@ -119,9 +121,13 @@ def main():
     N, A, F = args.n_envs, args.assets, args.fuse
     spec = trendou_spec(*[[p] * A for p in TRENDOU_P])
     env = BatchedEnv(spec, N, device=dev, seed=0x6D6164 + 3, env_offset=rank * N, **c3_kwargs())
+    if args.layout:
+        env.lib.mgn_set_layout(env.h, args.layout)
     total = args.warmup + args.steps
     actions = env.generate_actions(total, seed=0x6D6164)
-    traj = env.alloc_traj(F)
+    traj = env.alloc_traj(F, fields=[f for f in ("reward", "shaped", "done", "obs_price", "obs_port",
+                                                 "timestamp", "tprice", "tunits", "tcost", "risk",
+                                                 "margin_call")])
     stream = torch.cuda.current_stream(dev)
 
     def run(k0: int, k1: int, ev=None):
@@ -186,6 +192,7 @@ def main():
                                    "auto-reset",
                        "n_envs_per_gpu": N, "n_assets": A, "window": 0,
                        "steps_per_launch": steps_per_launch,
+                       "assets_per_lane": int(env.lib.mgn_get_layout(env.h)),
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": achieved_gbs / PEAK_HBM_GBS,

@@ -197,6 +197,15 @@ int mgn_ring_clear(const mgn_ring *ring, const uint8_t *mask_dev, void *stream);
 /* current_data: price (N,W,n_price) normalised, port (N,W,n_port), ts (N,W) */
 int mgn_ring_gather(const mgn_ring *ring, double *price_dev, double *port_dev, uint64_t *ts_dev,
                     void *stream);
+/* Lane layout of the step kernels: assets held per lane (1, 2, 4, 8; 0 =
+ * automatic, the default).  Results are bit-identical for every layout (the
+ * canonical reduction tree does not depend on it); only speed changes. */
+int mgn_set_layout(mgn_env *env, int32_t assets_per_lane);
+int mgn_get_layout(const mgn_env *env);
+/* DIAGNOSTIC ONLY (timing ablations, outputs become wrong): bit 0 skips the
+ * Broker rounds, bit 1 the generators, bit 2 the output stores, bit 3 the
+ * logarithms of the agent reward.  Never set in product or parity runs. */
+int mgn_set_ablation(mgn_env *env, int32_t flags);
 /* synchronise the handle's stream */
 int mgn_synchronize(mgn_env *env);
 const char *mgn_last_error(const mgn_env *env);

@@ -97,6 +97,9 @@ SYMBOLS = {
     "mgn_ring_push": (C.c_int, [C.POINTER(Ring), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mgn_ring_clear": (C.c_int, [C.POINTER(Ring), C.c_void_p, C.c_void_p]),
     "mgn_ring_gather": (C.c_int, [C.POINTER(Ring), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mgn_set_layout": (C.c_int, [C.c_void_p, C.c_int32]),
+    "mgn_get_layout": (C.c_int, [C.c_void_p]),
+    "mgn_set_ablation": (C.c_int, [C.c_void_p, C.c_int32]),
     "mgn_synchronize": (C.c_int, [C.c_void_p]),
     "mgn_last_error": (C.c_char_p, [C.c_void_p]),
     "mgn_global_error": (C.c_char_p, []),

@@ -2,24 +2,30 @@
 
     python -m madigan_amd.build [--force]
 
-Strict IEEE binary64 on the device: -ffp-contract=off, no fast-math, so the
-kernels' arithmetic is the same sequence of correctly rounded operations the
-oracle evaluates.
+Translation units: mgn_api.hip (C ABI, window/action kernels) plus one
+mgn_launch_a<APAD>.hip per padded asset count with that APAD's (M, S)
+instantiations of the step kernels; they compile in parallel and link into
+one shared library.  Strict IEEE binary64 on the device: -ffp-contract=off, no
+fast-math, so the kernels evaluate the same sequence of correctly rounded
+operations as the oracle.
 """
 from __future__ import annotations
 
+import glob
 import os
 import shutil
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = os.path.join(HERE, "csrc", "mgn_api.hip")
-DEPS = [os.path.join(HERE, "csrc", f) for f in ("mgn_api.hip", "mgn_kernels.h", "mgn_math.h")] + [
-    os.path.join(ROOT, "include", "madigan_amd.h")]
+CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmadigan_hip.so")
+OBJ = os.path.join(HERE, "_obj")
 ARCH = os.environ.get("MADIGAN_OFFLOAD_ARCH", "gfx950")
+FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+         "-fno-fast-math", "-Wall"]
 
 
 def hipcc() -> str:
@@ -29,18 +35,44 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm toolchain required)")
 
 
+def sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def deps():
+    return sources() + glob.glob(os.path.join(CSRC, "*.h")) + [
+        os.path.join(ROOT, "include", "madigan_amd.h")]
+
+
 def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(d) > t for d in DEPS)
+    return any(os.path.getmtime(d) > t for d in deps())
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
     if not force and not needs_build():
         return OUT
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-fno-fast-math", "-Wall", "-o", OUT + ".tmp", SRC]
+    os.makedirs(OBJ, exist_ok=True)
+    cc = hipcc()
+    jobs = jobs or min(8, os.cpu_count() or 4)
+
+    def compile_one(src):
+        obj = os.path.join(OBJ, os.path.basename(src).replace(".hip", ".o"))
+        cmd = [cc, *FLAGS, "-c", "-o", obj, src]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {src}:\n{r.stderr}")
+        if r.stderr.strip() and verbose:
+            print(r.stderr, file=sys.stderr)
+        return obj
+
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, sources()))
+    cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -11,7 +11,8 @@
 #include <string>
 
 #include "../../include/madigan_amd.h"
-#include "mgn_kernels.h"
+#include "mgn_aux_kernels.h"
+#include "mgn_launch.h"
 
 namespace {
 
@@ -48,6 +49,8 @@ struct mgn_env {
   mgn_asset_source* src_dev;
   double* target_dev;
   std::string err;
+  int ablate = 0;
+  int m = 1;  // assets per lane
 };
 
 namespace {
@@ -158,6 +161,7 @@ mgn::KParams kparams(const mgn_env* e) {
   p.shaper = c.shaper; p.reward_mode = c.reward_mode; p.auto_reset = c.auto_reset;
   p.atoms = c.action_atoms; p.eta = c.adaptation_rate; p.cos_temp = c.cosine_temp;
   p.unit_size = c.unit_size;
+  p.ablate = e->ablate;
   const mgn_views& v = e->v;
   p.L = v.ledger; p.mep = v.mean_entry; p.Bm = v.borrowed; p.P = v.prices;
   p.sx = v.sine_x; p.oum = v.ou_mean; p.dy = v.trend_dy; p.tlen = v.trend_len; p.tfl = v.trend_flags;
@@ -168,50 +172,46 @@ mgn::KParams kparams(const mgn_env* e) {
   return p;
 }
 
-// dispatch on APAD with one asset per lane (M = 1, S = APAD)
-template <template <int, int> class F, typename... Args>
-void dispatch(int apad, Args&&... args) {
-  switch (apad) {
-    case 1: F<1, 1>::run(args...); break;
-    case 2: F<1, 2>::run(args...); break;
-    case 4: F<1, 4>::run(args...); break;
-    case 8: F<1, 8>::run(args...); break;
-    case 16: F<1, 16>::run(args...); break;
-    case 32: F<1, 32>::run(args...); break;
-    default: F<1, 64>::run(args...); break;
+template <typename Arg>
+void launch(void (*const* fns)(int, const Arg&), int apad, int m, const Arg& a) {
+  const int idx = apad <= 1 ? 0 : apad <= 2 ? 1 : apad <= 4 ? 2 : apad <= 8 ? 3 : apad <= 16 ? 4 : apad <= 32 ? 5 : 6;
+  fns[idx](m, a);
+}
+void (*const kStep[7])(int, const mgn::StepArgs&) = {mgn::launch_step_a1, mgn::launch_step_a2, mgn::launch_step_a4, mgn::launch_step_a8, mgn::launch_step_a16, mgn::launch_step_a32, mgn::launch_step_a64};
+void (*const kInit[7])(int, const mgn::InitArgs&) = {mgn::launch_init_a1, mgn::launch_init_a2, mgn::launch_init_a4, mgn::launch_init_a8, mgn::launch_init_a16, mgn::launch_init_a32, mgn::launch_init_a64};
+void (*const kVal[7])(int, const mgn::ValArgs&) = {mgn::launch_val_a1, mgn::launch_val_a2, mgn::launch_val_a4, mgn::launch_val_a8, mgn::launch_val_a16, mgn::launch_val_a32, mgn::launch_val_a64};
+
+void launch_step(const mgn_env* e, const mgn_traj& out, int in_kind, const double* units,
+                 const int32_t* aidx, const int8_t* act, int K);
+void launch_init(const mgn_env* e, int mode, const uint8_t* mask);
+void launch_val(const mgn_env* e, double* out);
+
+// Lane layout: as few lanes per env as keeps >= 2 waves per SIMD resident
+// (256 CUs x 4 SIMDs x 2), so large batches run thread-per-env-like (less
+// cross-lane work per env) and small batches spread each env over more lanes.
+int choose_m(int n_envs, int apad) {
+  int m = mgn::min_m(apad);
+  while (m < 8 && m < apad) {
+    const long long waves = (long long)n_envs * (apad / (2 * m)) / 64;
+    if (waves < 2048) break;
+    m *= 2;
   }
+  return m;
 }
 
-template <int M, int S>
-struct StepL {
-  static void run(const mgn_env* e, const mgn_traj& out, int in_kind, const double* units,
-                  const int32_t* aidx, const int8_t* act, int K) {
-    const int epb = mgn::BLOCK / S;
-    const int grid = (e->N + epb - 1) / epb;
-    hipLaunchKernelGGL((mgn::k_step<M, S>), dim3(grid), dim3(mgn::BLOCK), 0, e->stream, kparams(e),
-                       out, in_kind, units, aidx, act, K);
-  }
-};
-
-template <int M, int S>
-struct InitL {
-  static void run(const mgn_env* e, int mode, const uint8_t* mask) {
-    const int epb = mgn::BLOCK / S;
-    const int grid = (e->N + epb - 1) / epb;
-    hipLaunchKernelGGL((mgn::k_init_reset<M, S>), dim3(grid), dim3(mgn::BLOCK), 0, e->stream,
-                       kparams(e), mode, mask);
-  }
-};
-
-template <int M, int S>
-struct ValL {
-  static void run(const mgn_env* e, double* out) {
-    const int epb = mgn::BLOCK / S;
-    const int grid = (e->N + epb - 1) / epb;
-    hipLaunchKernelGGL((mgn::k_valuation<M, S>), dim3(grid), dim3(mgn::BLOCK), 0, e->stream,
-                       kparams(e), out);
-  }
-};
+void launch_step(const mgn_env* e, const mgn_traj& out, int in_kind, const double* units,
+                 const int32_t* aidx, const int8_t* act, int K) {
+  mgn::StepArgs a{kparams(e), out, in_kind, units, aidx, act, K, e->stream};
+  launch(kStep, e->apad, e->m, a);
+}
+void launch_init(const mgn_env* e, int mode, const uint8_t* mask) {
+  mgn::InitArgs a{kparams(e), mode, mask, e->stream};
+  launch(kInit, e->apad, e->m, a);
+}
+void launch_val(const mgn_env* e, double* out) {
+  mgn::ValArgs a{kparams(e), out, e->stream};
+  launch(kVal, e->apad, e->m, a);
+}
 
 mgn::RingDesc ring_desc(const mgn_env* e) {
   mgn::RingDesc r;
@@ -246,6 +246,7 @@ int mgn_create(const mgn_config* cfg, const mgn_asset_source* sources, void* str
   e->W = cfg->window > 0 ? cfg->window : 0;
   e->D = (cfg->reward_mode == MGN_REWARD_AGENT_PER_ASSET) ? e->A : 1;
   e->apad = next_pow2(e->A);
+  e->m = choose_m(e->N, e->apad);
   e->stream = (hipStream_t)stream;
   const Offsets o = plan(cfg);
   e->arena_bytes = o.total;
@@ -295,7 +296,7 @@ int mgn_create(const mgn_config* cfg, const mgn_asset_source* sources, void* str
     rc = check_hip(e, hipMemcpyAsync(e->target_dev, cfg->desired_portfolio, 8 * (e->A + 1),
                                      hipMemcpyHostToDevice, e->stream), "hipMemcpyAsync(target)");
   if (rc == MGN_OK) {
-    dispatch<InitL>(e->apad, e, 0, (const uint8_t*)nullptr);
+    launch_init(e, 0, nullptr);
     rc = check_hip(e, hipGetLastError(), "k_init_reset");
   }
   if (rc == MGN_OK) rc = check_hip(e, hipStreamSynchronize(e->stream), "hipStreamSynchronize");
@@ -331,7 +332,7 @@ int mgn_get_views(const mgn_env* e, mgn_views* views) {
 
 int mgn_reset(mgn_env* e, const uint8_t* mask_dev) {
   if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
-  dispatch<InitL>(e->apad, e, 1, mask_dev);
+  launch_init(e, 1, mask_dev);
   return check_hip(e, hipGetLastError(), "mgn_reset");
 }
 
@@ -344,7 +345,7 @@ int mgn_step(mgn_env* e, int32_t kind, const double* units_dev, const int32_t* a
   else return fail(e, MGN_ERR_CONFIG, "unknown step kind");
   if (in_kind != mgn::IN_NONE && !units_dev) return fail(e, MGN_ERR_ARG, "units pointer is null");
   if (in_kind == mgn::IN_SINGLE && !aidx_dev) return fail(e, MGN_ERR_ARG, "asset index pointer is null");
-  dispatch<StepL>(e->apad, e, e->v.out, in_kind, units_dev, aidx_dev, (const int8_t*)nullptr, 1);
+  launch_step(e, e->v.out, in_kind, units_dev, aidx_dev, nullptr, 1);
   return check_hip(e, hipGetLastError(), "mgn_step");
 }
 
@@ -352,8 +353,7 @@ int mgn_rollout(mgn_env* e, const int8_t* actions_dev, int32_t k_steps, const mg
   if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
   if (!actions_dev || !out) return fail(e, MGN_ERR_ARG, "null actions/out");
   if (k_steps < 1) return fail(e, MGN_ERR_LENGTH, "k_steps must be >= 1");
-  dispatch<StepL>(e->apad, e, *out, (int)mgn::IN_DISCRETE, (const double*)nullptr,
-                  (const int32_t*)nullptr, actions_dev, (int)k_steps);
+  launch_step(e, *out, mgn::IN_DISCRETE, nullptr, nullptr, actions_dev, (int)k_steps);
   return check_hip(e, hipGetLastError(), "mgn_rollout");
 }
 
@@ -361,8 +361,7 @@ int mgn_rollout_units(mgn_env* e, const double* units_dev, int32_t k_steps, cons
   if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
   if (!units_dev || !out) return fail(e, MGN_ERR_ARG, "null units/out");
   if (k_steps < 1) return fail(e, MGN_ERR_LENGTH, "k_steps must be >= 1");
-  dispatch<StepL>(e->apad, e, *out, (int)mgn::IN_UNITS, units_dev, (const int32_t*)nullptr,
-                  (const int8_t*)nullptr, (int)k_steps);
+  launch_step(e, *out, mgn::IN_UNITS, units_dev, nullptr, nullptr, (int)k_steps);
   return check_hip(e, hipGetLastError(), "mgn_rollout_units");
 }
 
@@ -413,7 +412,7 @@ int mgn_generate_actions(mgn_env* e, int8_t* actions_dev, int32_t k_steps, uint6
 
 int mgn_valuation(mgn_env* e, double* out_dev) {
   if (!e || !out_dev) return fail(e, MGN_ERR_ARG, "null handle/out");
-  dispatch<ValL>(e->apad, e, out_dev);
+  launch_val(e, out_dev);
   return check_hip(e, hipGetLastError(), "mgn_valuation");
 }
 
@@ -468,6 +467,28 @@ int mgn_ring_gather(const mgn_ring* r, double* price_dev, double* port_dev, uint
   hipLaunchKernelGGL(mgn::k_ring_gather, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, ring_from(r), price_dev, port_dev, ts_dev);
   return check_hip(nullptr, hipGetLastError(), "mgn_ring_gather");
+}
+
+int mgn_set_layout(mgn_env* e, int32_t assets_per_lane) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  if (assets_per_lane == 0) {
+    e->m = choose_m(e->N, e->apad);
+    return MGN_OK;
+  }
+  if (assets_per_lane != 1 && assets_per_lane != 2 && assets_per_lane != 4 && assets_per_lane != 8)
+    return fail(e, MGN_ERR_CONFIG, "assets_per_lane must be 0 (auto), 1, 2, 4 or 8");
+  int m = assets_per_lane < e->apad ? assets_per_lane : e->apad;
+  if (m < mgn::min_m(e->apad)) m = mgn::min_m(e->apad);
+  e->m = m;
+  return MGN_OK;
+}
+
+int mgn_get_layout(const mgn_env* e) { return e ? e->m : 0; }
+
+int mgn_set_ablation(mgn_env* e, int32_t flags) {
+  if (!e) return MGN_ERR_ARG;
+  e->ablate = flags;
+  return MGN_OK;
 }
 
 int mgn_synchronize(mgn_env* e) {

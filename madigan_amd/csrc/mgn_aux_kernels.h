@@ -1,0 +1,121 @@
+// mgn_aux_kernels.h -- non-templated kernels (window ring, action generator);
+// included by exactly one translation unit (mgn_api.hip).
+#pragma once
+
+#include "mgn_kernels.h"
+
+namespace mgn {
+
+// ---------------------------------------------------------------------------
+// Window kernels (StackerDiscrete, preprocessor.py:143-199).  Ring layout
+// (N, W, C) with C = F + P columns (price features then portfolio entries).
+struct RingDesc {
+  int N, F, Pn, W, norm;
+  double* ring;
+  uint64_t* ring_ts;
+  int32_t* head;
+  int32_t* len;
+};
+
+// stream_state: one thread per env (rare; the fused step writes its own rows)
+__global__ void k_ring_push(RingDesc r, const double* __restrict__ price,
+                            const double* __restrict__ port, const uint64_t* __restrict__ ts) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= r.N) return;
+  const int C = r.F + r.Pn;
+  const int h = (r.head[env] + 1) % r.W;
+  double* row = r.ring + ((size_t)env * r.W + h) * C;
+  for (int c = 0; c < r.F; ++c) row[c] = price ? price[(size_t)env * r.F + c] : 0.;
+  for (int c = 0; c < r.Pn; ++c) row[r.F + c] = port ? port[(size_t)env * r.Pn + c] : 0.;
+  r.ring_ts[(size_t)env * r.W + h] = ts ? ts[env] : 0;
+  r.head[env] = h;
+  if (r.len[env] < r.W) r.len[env] += 1;
+}
+
+__global__ void k_ring_clear(RingDesc r, const uint8_t* __restrict__ mask) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= r.N) return;
+  if (mask && !mask[env]) return;
+  r.head[env] = r.W - 1;
+  r.len[env] = 0;
+}
+
+// current_data: one thread per (env, column); rows oldest -> newest, norm on
+// price columns (log_norm :79-81, lookback :63-66, standard_norm :83-92).
+__global__ __launch_bounds__(BLOCK) void k_ring_gather(RingDesc r, double* __restrict__ price_out,
+                                                       double* __restrict__ port_out,
+                                                       uint64_t* __restrict__ ts_out) {
+  const int C = r.F + r.Pn;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (int64_t)r.N * C) return;
+  const int env = (int)(gid / C);
+  const int c = (int)(gid % C);
+  const int W = r.W;
+  const int len = r.len[env];
+  const int hd = r.head[env];
+  const double* base = r.ring + (size_t)env * W * C;
+  auto row_of = [&](int w) { return (hd - (len - 1) + w + 2 * W) % W; };
+  if (c >= r.F) {
+    const int pc = c - r.F;
+    if (port_out)
+      for (int w = 0; w < W; ++w)
+        port_out[((size_t)env * W + w) * r.Pn + pc] = (w < len) ? base[(size_t)row_of(w) * C + c] : 0.;
+    return;
+  }
+  if (c == 0 && ts_out)
+    for (int w = 0; w < W; ++w)
+      ts_out[(size_t)env * W + w] = (w < len) ? r.ring_ts[(size_t)env * W + row_of(w)] : 0;
+  if (!price_out) return;
+  double* o = price_out + (size_t)env * W * r.F + c;
+  const int nt = r.norm;
+  if (nt == MGN_NORM_STANDARD_NORMAL) {
+    double sum = 0.;
+    for (int w = 0; w < len; ++w) sum += base[(size_t)row_of(w) * C + c];
+    const double mean = sum / len;
+    double ss = 0.;
+    for (int w = 0; w < len; ++w) {
+      const double d = base[(size_t)row_of(w) * C + c] - mean;
+      ss += d * d;
+    }
+    const double sd = sqrt(ss / len);
+    for (int w = 0; w < W; ++w) {
+      double v = 0.;
+      if (w < len) {
+        v = (base[(size_t)row_of(w) * C + c] - mean) / sd;
+        if (v != v) v = 0.;
+        else if (v == __builtin_inf()) v = 1.7976931348623157e308;
+        else if (v == -__builtin_inf()) v = -1.7976931348623157e308;
+      }
+      o[(size_t)w * r.F] = v;
+    }
+    return;
+  }
+  const double last = (len > 0) ? base[(size_t)row_of(len - 1) * C + c] : 1.;
+  for (int w = 0; w < W; ++w) {
+    double v = 0.;
+    if (w < len) {
+      v = base[(size_t)row_of(w) * C + c];
+      if (nt == MGN_NORM_LOG) v = log((v < 1e-5) ? 1e-5 : v);
+      else if (nt == MGN_NORM_LOOKBACK) v = v / last;
+      else if (nt == MGN_NORM_LOOKBACK_LOG) v = log(v / last);
+    }
+    o[(size_t)w * r.F] = v;
+  }
+}
+
+// Philox discrete actions U{0..atoms-1}: counter (k, env, asset, 0xAC7)
+__global__ void k_gen_actions(int8_t* __restrict__ out, int K, int N, int A, int atoms,
+                              uint64_t seed, int64_t env_offset) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)K * N * A;
+  if (gid >= total) return;
+  const int a = (int)(gid % A);
+  const int64_t ke = gid / A;
+  const int env = (int)(ke % N);
+  const uint32_t k = (uint32_t)(ke / N);
+  const u4 x = philox4x32_10(k, (uint32_t)(env_offset + env), (uint32_t)a, 0xAC7u, (uint32_t)seed,
+                             (uint32_t)(seed >> 32));
+  out[gid] = (int8_t)(((uint64_t)x.x * (uint32_t)atoms) >> 32);
+}
+
+}  // namespace mgn

@@ -31,6 +31,7 @@ struct KParams {
   uint64_t seed;
   double init_cash, reqM, mainM, slip_rel, slip_abs, tc_rel, tc_abs;
   int shaper, reward_mode, auto_reset, atoms;
+  int ablate;  // diagnostic timing builds only (mgn_set_ablation); 0 in every real run
   double eta, cos_temp, unit_size;
   // state
   double *L, *mep, *Bm, *P, *sx, *oum, *dy;
@@ -524,20 +525,40 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
     cos_qn = sqrt(p.target[0] * p.target[0] + canon<M, S>(qq));
   }
 
+  // agent-side reward only when it is an output or feeds the shaper
+  const bool need_ar = (p.reward_mode != MGN_REWARD_ENV_LOG) || (out.agent_reward != nullptr);
+  // Portfolio sums of the current state.  They are carried from the previous
+  // step's post-getData sums (same inputs, so bit-identical to a recompute)
+  // and recomputed only after a reset.
+  Sums s0 = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
+  // discrete actions of the next step are prefetched one step ahead
+  int8_t act_next[M];
+  if (in_kind == IN_DISCRETE) {
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+      act_next[m] = s.valid[m] ? act_in[(size_t)env * A + s.asset[m]] : 0;
+  }
+
   for (int k = 0; k < K; ++k) {
     const size_t oN = (size_t)k * p.N, oNA = (size_t)k * p.N * A;
     // ---- action -> units for this lane's slots
     double uc[M];
-    Sums s0 = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
     const double prevEq = (cash + s0.lp) - s0.b;  // Env.h:208
     if (in_kind == IN_DISCRETE) {                  // dqn.py:160-179
       const double avM = ((cash + s0.sh) + (s0.lp - s0.ml)) / p.reqM;
       const int half = p.atoms / 2;
+      int8_t act_cur[M];
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        act_cur[m] = act_next[m];
+        if (k + 1 < K && s.valid[m])
+          act_next[m] = act_in[oNA + (size_t)p.N * A + (size_t)env * A + s.asset[m]];
+      }
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         uc[m] = 0.;
         if (!s.valid[m]) continue;
-        const int a = act_in[oNA + (size_t)env * A + s.asset[m]];
+        const int a = act_cur[m];
         const double u = p.unit_size * avM / s.P[m];
         uc[m] = (double)(a - half) * u;
         if (a == 0) uc[m] = (s.L[m] != 0) ? -s.L[m] : 0.;
@@ -569,7 +590,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
       tc[m] = 0.;
       rk[m] = MGN_GREEN;
     }
-    Rounds<M, S, 0>::run(s, p, cash, uc, tp, tu, tc, rk, ls);
+    if (!(p.ablate & 1)) Rounds<M, S, 0>::run(s, p, cash, uc, tp, tu, tc, rk, ls);
     // BrokerResponse.marginCall (Broker.cpp:156-157)
     int mcall = 0;
     if (in_kind != IN_NONE) {
@@ -578,7 +599,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
     }
 
     // ---- dataSource->getData()
-    gen_tick<M>(s, p, env, ts);
+    if (!(p.ablate & 2)) gen_tick<M>(s, p, env, ts);
     ts += 1;
 
     // ---- reward / done (Env.h:211-223)
@@ -603,14 +624,14 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
     double ar[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      if (!s.valid[m]) {
+      if (!s.valid[m] || !need_ar) {
         ar[m] = 0.;
         continue;
       }
       double v = (((s.L[m] * s.P[m]) - prevVal[m]) - (tu[m] * tp[m] + tc[m])) / prevEq;
       v += 1;
       v = (v < .35) ? .35 : v;
-      ar[m] = log(v);
+      ar[m] = (p.ablate & 8) ? v : log(v);
     }
     // ---- reward shaping
     double cos_term = 0.;
@@ -641,7 +662,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
     // ---- outputs
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      if (!s.valid[m]) continue;
+      if (!s.valid[m] || (p.ablate & 4)) continue;
       const size_t i = oNA + (size_t)env * A + s.asset[m];
       if (out.obs_price) out.obs_price[i] = s.P[m];
       if (out.tprice) out.tprice[i] = tp[m];
@@ -654,7 +675,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
         if (out.shaped) out.shaped[i] = shaped_v[m];
       }
     }
-    if (ls == 0) {
+    if (ls == 0 && !(p.ablate & 4)) {
       if (out.reward) out.reward[oN + env] = reward;
       if (out.done) out.done[oN + env] = done ? 1 : 0;
       if (out.timestamp) out.timestamp[oN + env] = ts;
@@ -682,7 +703,11 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
     }
     // ---- window + auto reset
     if (p.W > 0) ring_push<M, S>(s, p, env, ls, cash, ts, head, len);
-    if (done && p.auto_reset) env_reset<M, S>(s, p, env, ls, cash, ts, head, len);
+    s0 = q;
+    if (done && p.auto_reset) {
+      env_reset<M, S>(s, p, env, ls, cash, ts, head, len);
+      s0 = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
+    }
   }
 
   // ---- write back state
@@ -816,118 +841,6 @@ __global__ __launch_bounds__(BLOCK) void k_valuation(KParams p, double* __restri
   o[7] = bav;
   o[8] = q.lp;
   o[9] = margin_call(q, cash, p.mainM) ? (double)MGN_MARGIN_CALL : (double)MGN_GREEN;
-}
-
-// ---------------------------------------------------------------------------
-// Window kernels (StackerDiscrete, preprocessor.py:143-199).  Ring layout
-// (N, W, C) with C = F + P columns (price features then portfolio entries).
-struct RingDesc {
-  int N, F, Pn, W, norm;
-  double* ring;
-  uint64_t* ring_ts;
-  int32_t* head;
-  int32_t* len;
-};
-
-// stream_state: one thread per env (rare; the fused step writes its own rows)
-__global__ void k_ring_push(RingDesc r, const double* __restrict__ price,
-                            const double* __restrict__ port, const uint64_t* __restrict__ ts) {
-  const int env = blockIdx.x * blockDim.x + threadIdx.x;
-  if (env >= r.N) return;
-  const int C = r.F + r.Pn;
-  const int h = (r.head[env] + 1) % r.W;
-  double* row = r.ring + ((size_t)env * r.W + h) * C;
-  for (int c = 0; c < r.F; ++c) row[c] = price ? price[(size_t)env * r.F + c] : 0.;
-  for (int c = 0; c < r.Pn; ++c) row[r.F + c] = port ? port[(size_t)env * r.Pn + c] : 0.;
-  r.ring_ts[(size_t)env * r.W + h] = ts ? ts[env] : 0;
-  r.head[env] = h;
-  if (r.len[env] < r.W) r.len[env] += 1;
-}
-
-__global__ void k_ring_clear(RingDesc r, const uint8_t* __restrict__ mask) {
-  const int env = blockIdx.x * blockDim.x + threadIdx.x;
-  if (env >= r.N) return;
-  if (mask && !mask[env]) return;
-  r.head[env] = r.W - 1;
-  r.len[env] = 0;
-}
-
-// current_data: one thread per (env, column); rows oldest -> newest, norm on
-// price columns (log_norm :79-81, lookback :63-66, standard_norm :83-92).
-__global__ __launch_bounds__(BLOCK) void k_ring_gather(RingDesc r, double* __restrict__ price_out,
-                                                       double* __restrict__ port_out,
-                                                       uint64_t* __restrict__ ts_out) {
-  const int C = r.F + r.Pn;
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (int64_t)r.N * C) return;
-  const int env = (int)(gid / C);
-  const int c = (int)(gid % C);
-  const int W = r.W;
-  const int len = r.len[env];
-  const int hd = r.head[env];
-  const double* base = r.ring + (size_t)env * W * C;
-  auto row_of = [&](int w) { return (hd - (len - 1) + w + 2 * W) % W; };
-  if (c >= r.F) {
-    const int pc = c - r.F;
-    if (port_out)
-      for (int w = 0; w < W; ++w)
-        port_out[((size_t)env * W + w) * r.Pn + pc] = (w < len) ? base[(size_t)row_of(w) * C + c] : 0.;
-    return;
-  }
-  if (c == 0 && ts_out)
-    for (int w = 0; w < W; ++w)
-      ts_out[(size_t)env * W + w] = (w < len) ? r.ring_ts[(size_t)env * W + row_of(w)] : 0;
-  if (!price_out) return;
-  double* o = price_out + (size_t)env * W * r.F + c;
-  const int nt = r.norm;
-  if (nt == MGN_NORM_STANDARD_NORMAL) {
-    double sum = 0.;
-    for (int w = 0; w < len; ++w) sum += base[(size_t)row_of(w) * C + c];
-    const double mean = sum / len;
-    double ss = 0.;
-    for (int w = 0; w < len; ++w) {
-      const double d = base[(size_t)row_of(w) * C + c] - mean;
-      ss += d * d;
-    }
-    const double sd = sqrt(ss / len);
-    for (int w = 0; w < W; ++w) {
-      double v = 0.;
-      if (w < len) {
-        v = (base[(size_t)row_of(w) * C + c] - mean) / sd;
-        if (v != v) v = 0.;
-        else if (v == __builtin_inf()) v = 1.7976931348623157e308;
-        else if (v == -__builtin_inf()) v = -1.7976931348623157e308;
-      }
-      o[(size_t)w * r.F] = v;
-    }
-    return;
-  }
-  const double last = (len > 0) ? base[(size_t)row_of(len - 1) * C + c] : 1.;
-  for (int w = 0; w < W; ++w) {
-    double v = 0.;
-    if (w < len) {
-      v = base[(size_t)row_of(w) * C + c];
-      if (nt == MGN_NORM_LOG) v = log((v < 1e-5) ? 1e-5 : v);
-      else if (nt == MGN_NORM_LOOKBACK) v = v / last;
-      else if (nt == MGN_NORM_LOOKBACK_LOG) v = log(v / last);
-    }
-    o[(size_t)w * r.F] = v;
-  }
-}
-
-// Philox discrete actions U{0..atoms-1}: counter (k, env, asset, 0xAC7)
-__global__ void k_gen_actions(int8_t* __restrict__ out, int K, int N, int A, int atoms,
-                              uint64_t seed, int64_t env_offset) {
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t total = (int64_t)K * N * A;
-  if (gid >= total) return;
-  const int a = (int)(gid % A);
-  const int64_t ke = gid / A;
-  const int env = (int)(ke % N);
-  const uint32_t k = (uint32_t)(ke / N);
-  const u4 x = philox4x32_10(k, (uint32_t)(env_offset + env), (uint32_t)a, 0xAC7u, (uint32_t)seed,
-                             (uint32_t)(seed >> 32));
-  out[gid] = (int8_t)(((uint64_t)x.x * (uint32_t)atoms) >> 32);
 }
 
 }  // namespace mgn

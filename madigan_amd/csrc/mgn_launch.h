@@ -1,0 +1,50 @@
+// mgn_launch.h -- host-side launchers of the templated step kernels.  Each
+// padded asset count APAD has its own translation unit (mgn_launch_a<APAD>.hip)
+// so the (M, S) instantiations compile in parallel.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "mgn_kernels.h"
+
+namespace mgn {
+
+struct StepArgs {
+  KParams p;
+  mgn_traj out;
+  int in_kind;
+  const double* units;
+  const int32_t* aidx;
+  const int8_t* act;
+  int K;
+  hipStream_t stream;
+};
+struct InitArgs {
+  KParams p;
+  int mode;
+  const uint8_t* mask;
+  hipStream_t stream;
+};
+struct ValArgs {
+  KParams p;
+  double* out;
+  hipStream_t stream;
+};
+
+// smallest assets-per-lane with at most 16 lanes per env (DPP-only reductions)
+constexpr int min_m(int apad) { return apad > 16 ? apad / 16 : 1; }
+
+#define MGN_DECLARE_APAD(A)                          \
+  void launch_step_a##A(int m, const StepArgs& a);   \
+  void launch_init_a##A(int m, const InitArgs& a);   \
+  void launch_val_a##A(int m, const ValArgs& a);
+MGN_DECLARE_APAD(1)
+MGN_DECLARE_APAD(2)
+MGN_DECLARE_APAD(4)
+MGN_DECLARE_APAD(8)
+MGN_DECLARE_APAD(16)
+MGN_DECLARE_APAD(32)
+MGN_DECLARE_APAD(64)
+#undef MGN_DECLARE_APAD
+
+}  // namespace mgn

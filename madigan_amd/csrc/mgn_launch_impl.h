@@ -1,0 +1,58 @@
+// mgn_launch_impl.h -- defines the launchers for one APAD (included once per
+// mgn_launch_a<APAD>.hip).
+#pragma once
+
+#include "mgn_launch.h"
+
+namespace mgn {
+
+template <int M, int S>
+struct StepL {
+  static void run(const StepArgs& a) {
+    const int epb = BLOCK / S;
+    const int grid = (a.p.N + epb - 1) / epb;
+    hipLaunchKernelGGL((k_step<M, S>), dim3(grid), dim3(BLOCK), 0, a.stream, a.p, a.out, a.in_kind,
+                       a.units, a.aidx, a.act, a.K);
+  }
+};
+template <int M, int S>
+struct InitL {
+  static void run(const InitArgs& a) {
+    const int epb = BLOCK / S;
+    const int grid = (a.p.N + epb - 1) / epb;
+    hipLaunchKernelGGL((k_init_reset<M, S>), dim3(grid), dim3(BLOCK), 0, a.stream, a.p, a.mode,
+                       a.mask);
+  }
+};
+template <int M, int S>
+struct ValL {
+  static void run(const ValArgs& a) {
+    const int epb = BLOCK / S;
+    const int grid = (a.p.N + epb - 1) / epb;
+    hipLaunchKernelGGL((k_valuation<M, S>), dim3(grid), dim3(BLOCK), 0, a.stream, a.p, a.out);
+  }
+};
+
+// M in {1,2,4,8} clamped to [min_m(APAD), APAD]; S = APAD / M <= 16
+template <template <int, int> class F, int APAD, typename Arg>
+void dispatch_m(int m, const Arg& a) {
+  if constexpr (APAD >= 8) {
+    if (m >= 8) { F<8, APAD / 8>::run(a); return; }
+  }
+  if constexpr (APAD >= 4 && min_m(APAD) <= 4) {
+    if (m >= 4 || min_m(APAD) == 4) { F<4, APAD / 4>::run(a); return; }
+  }
+  if constexpr (APAD >= 2 && min_m(APAD) <= 2) {
+    if (m >= 2 || min_m(APAD) == 2) { F<2, APAD / 2>::run(a); return; }
+  }
+  if constexpr (min_m(APAD) == 1) F<1, APAD>::run(a);
+}
+
+}  // namespace mgn
+
+#define MGN_DEFINE_APAD(A)                                                                   \
+  namespace mgn {                                                                            \
+  void launch_step_a##A(int m, const StepArgs& a) { dispatch_m<StepL, A>(m, a); }            \
+  void launch_init_a##A(int m, const InitArgs& a) { dispatch_m<InitL, A>(m, a); }            \
+  void launch_val_a##A(int m, const ValArgs& a) { dispatch_m<ValL, A>(m, a); }               \
+  }

@@ -227,3 +227,30 @@ def test_sharded_equals_unsharded(gpu):
         hi.step()
     p = full.prices.cpu().numpy()
     assert_bits(np.concatenate([lo.prices.cpu().numpy(), hi.prices.cpu().numpy()]), p, "shards")
+
+
+@pytest.mark.parametrize("A", [3, 8, 16])
+def test_layouts_bit_identical(gpu, A):
+    """Every lane layout (assets per lane 1/2/4/8) evaluates the same canonical
+    tree, so all layouts produce identical bits."""
+    import ctypes as C
+    from madigan_amd import BatchedEnv
+    N, K = 200, 24
+    kw = dict(required_margin=0.1, maintenance_margin=1.0, transaction_cost_rel=0.02,
+              reward_shaper="DSR", reward_mode="agent_per_asset", auto_reset=True, seed=21)
+    spec = spec_from_sources(trendou_sources(A, [0.05, 3, 40, 0.001, 0.02, 5.0, 0.15, 0.04, 0.01, 0.99]))
+    ref = None
+    for m in (1, 2, 4, 8):
+        g = BatchedEnv(spec, N, **kw)
+        g.lib.mgn_set_layout(g.h, m)
+        acts = g.generate_actions(K, seed=4)
+        out = {k: v.cpu().numpy() for k, v in g.rollout(acts).items()}
+        out["ledger"] = g.ledger.cpu().numpy()
+        if ref is None:
+            ref = out
+            continue
+        for k, v in out.items():
+            if v.dtype == np.float64:
+                assert_bits(v, ref[k], f"M={m} {k}")
+            else:
+                assert np.array_equal(v, ref[k]), f"M={m} {k}"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # profiling recipe (run on the GPU box from the repo root)
 set -o pipefail
-cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo; cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT

@@ -162,6 +162,7 @@ mgn::KParams kparams(const mgn_env* e) {
   p.atoms = c.action_atoms; p.eta = c.adaptation_rate; p.cos_temp = c.cosine_temp;
   p.unit_size = c.unit_size;
   p.ablate = e->ablate;
+  p.reqm_one = (c.required_margin == 1.0) ? 1 : 0;
   const mgn_views& v = e->v;
   p.L = v.ledger; p.mep = v.mean_entry; p.Bm = v.borrowed; p.P = v.prices;
   p.sx = v.sine_x; p.oum = v.ou_mean; p.dy = v.trend_dy; p.tlen = v.trend_len; p.tfl = v.trend_flags;

@@ -31,6 +31,7 @@ struct KParams {
   uint64_t seed;
   double init_cash, reqM, mainM, slip_rel, slip_abs, tc_rel, tc_abs;
   int shaper, reward_mode, auto_reset, atoms;
+  int reqm_one;  // required_margin == 1.0
   int ablate;  // diagnostic timing builds only (mgn_set_ablation); 0 in every real run
   double eta, cos_temp, unit_size;
   // state
@@ -187,8 +188,9 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
     const int kind = s.kind[m];
     if (kind == MGN_SRC_TRENDOU) {
       double y = s.P[m];
+      const Draw d = draw0(p.seed, genv, (uint32_t)a, tick);
       if (s.tfl[m] & 1) {
-        const double n = normal(p.seed, genv, (uint32_t)a, 0, tick) * q[8] + 0.0;
+        const double n = d.z * q[8] + 0.0;
         const double dir = (s.tfl[m] & 2) ? -1.0 : 1.0;
         y += y * (s.dy[m] * dir + n);
         s.tlen[m] -= 1;
@@ -199,32 +201,30 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
         y = (0.01 < y) ? y : 0.01;
         if (y <= .1) s.tfl[m] &= ~2;
       } else {
-        const double n = normal(p.seed, genv, (uint32_t)a, 0, tick) * q[7] + 0.0;
+        const double n = d.z * q[7] + 0.0;
         const double ou_noise = y * n;
         const double ou_rev = q[6] * (s.oum[m] - y);
         y += ou_rev + ou_noise;
-        double u_trend, u_dir;
-        uniform2(p.seed, genv, (uint32_t)a, 1, tick, u_trend, u_dir);
-        if (u_trend < q[0]) {
+        if (d.ut < q[0]) {  // regime switch (DataSource.cpp:1484-1489)
           double u_len, u_dy;
-          uniform2(p.seed, genv, (uint32_t)a, 2, tick, u_len, u_dy);
+          uniform2(p.seed, genv, (uint32_t)a, 1, tick, u_len, u_dy);
           const int32_t lo = (int32_t)q[1], hi = (int32_t)q[2];
           int32_t len = lo + (int32_t)(u_len * (double)(hi - lo + 1));
           if (len > hi) len = hi;
           s.tlen[m] = len;
           s.dy[m] = (q[4] - q[3]) * u_dy + q[3];
-          s.tfl[m] = (uint8_t)(1 | ((u_dir < 0.5) ? 2 : 0));
+          s.tfl[m] = (uint8_t)(1 | (d.dbit ? 2 : 0));
         }
       }
       s.P[m] = y;
     } else if (kind == MGN_SRC_OU) {
-      const double z = normal(p.seed, genv, (uint32_t)a, 0, tick) * 1.0 + 0.0;
+      const double z = draw0(p.seed, genv, (uint32_t)a, tick).z * 1.0 + 0.0;
       double x = s.P[m];
       x += (q[1] * (q[0] - x)) + q[0] * q[2] * z;
       s.P[m] = x;
     } else if (kind == MGN_SRC_SINE) {
       double noise = 0.0;
-      if (q[5] != 0.0) noise = normal(p.seed, genv, (uint32_t)a, 0, tick) * q[5] + 0.0;
+      if (q[5] != 0.0) noise = draw0(p.seed, genv, (uint32_t)a, tick).z * q[5] + 0.0;
       const double PI2 = 3.141592653589793238463 * 2;
       s.P[m] = noise + q[1] + q[2] * det_sin(PI2 * s.sx[m] * q[0]);
       s.sx[m] += q[4];
@@ -344,87 +344,85 @@ __device__ __forceinline__ void store_lane(const Lane<M>& s, const KParams& p, i
 }
 
 
-// One Broker round (Broker.cpp:124-142): asset i = J*M + MM, executed by the
+// x / required_margin; x / 1.0 == x exactly in IEEE, so the common
+// required_margin == 1 case skips the division with identical bits.
+__device__ __forceinline__ double div_reqm(double x, const KParams& p) {
+  double r;
+  if (p.reqm_one) r = x;
+  else r = x / p.reqM;
+  return r;
+}
+
+// One Broker round (Broker.cpp:124-142): asset i = J*M + MM, decided by the
 // owning lane J of every segment after a segment reduction of the portfolio
-// sums; the owner's new cash is then broadcast to its segment.
+// sums; the owner's new cash is then broadcast to its segment.  Written as
+// straight-line predicated code (every branch of Portfolio::checkRisk and
+// Portfolio::handleTransaction is evaluated and the taken one selected), so the
+// round has no divergent control flow; the selected values are exactly the
+// ones the reference's branches produce.
 template <int M, int S, int J, int MM>
 __device__ __forceinline__ void broker_round(Lane<M>& s, const KParams& p, double& cash,
                                              const double (&uc)[M], double (&tp)[M],
                                              double (&tu)[M], double (&tc)[M], int (&rk)[M],
                                              int ls) {
   const bool act = (ls == J) && (uc[MM] != 0.);
-  if (__ballot(act) == 0) return;
   const Sums q = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
   const double pnl = q.lp - q.ml;
   const double balance = cash + q.sh;
-  const double availM = (balance + pnl) / p.reqM;
-  if (act) {
-    const double u = uc[MM];
-    const double cur = s.L[MM];
-    const double price = s.P[MM];
-    int risk;  // Portfolio::checkRisk(i, u), Portfolio.cpp:254-279
-    if (signbit(u) != signbit(cur)) {
-      risk = MGN_GREEN;
-      if (u > -1 * cur) {
-        const double excess = u + cur;
-        if (availM <= fabs(price * excess) || balance <= 0.) risk = MGN_INSUFF_MARGIN;
-      }
-    } else {
-      const double equity = (cash + q.lp) - q.b;
-      const double mr = p.mainM * pnl;
-      if ((equity <= -mr) || ((balance + pnl) <= -mr)) risk = MGN_MARGIN_CALL;
-      else if (availM <= fabs(price * u) || balance <= 0.) risk = MGN_INSUFF_MARGIN;
-      else risk = MGN_GREEN;
-    }
-    rk[MM] = risk;
-    if (risk == MGN_GREEN) {  // Broker.cpp:128-135
-      const double slippage = (price * p.slip_rel) + p.slip_abs;
-      const double tprice = u < 0 ? (price - slippage) : (price + slippage);
-      const double tcost = fabs(u * price) * p.tc_rel + p.tc_abs;
-      // Portfolio::handleTransaction, Portfolio.cpp:284-323
-      double units = u;
-      double cu = cur;
-      double me = s.mep[MM];
-      if (signbit(cu) != signbit(units)) {
-        if (fabs(units) > fabs(cu)) {
-          units += cu;
-          cash += cu * tprice;
-          cu = 0.;
-          me = tprice;
-        }
-      } else {
-        me += (tprice - me) * (units / (units + cu));
-      }
-      const double amt = tprice * units;
-      const double use = amt * p.reqM;
-      const double brw = amt - use;
-      double bm = s.Bm[MM];
-      bm += brw;
-      cash -= (use + tcost);
-      cu += units;
-      if (fabs(cu) < 0.000001) {
-        me = 0.;
-        if (bm > 0.) {
-          cash -= bm;
-          bm = 0.;
-        }
-      }
-      if (bm < 0.) {
-        cash -= bm;
-        bm = 0.;
-      }
-      s.L[MM] = cu;
-      s.mep[MM] = me;
-      s.Bm[MM] = bm;
-      tp[MM] = tprice;
-      tu[MM] = u;
-      tc[MM] = tcost;
-    }
-  }
-  cash = seg_bcast<S, J>(cash);
+  const double availM = div_reqm(balance + pnl, p);
+  const double u = uc[MM];
+  const double cur = s.L[MM];
+  const double price = s.P[MM];
+  // Portfolio::checkRisk(i, u), Portfolio.cpp:254-279
+  const bool opp = signbit(u) != signbit(cur);
+  const bool rev = u > -1 * cur;
+  const double excess = u + cur;
+  const bool insuff_opp = rev && ((availM <= fabs(price * excess)) || (balance <= 0.));
+  const double equity = (cash + q.lp) - q.b;
+  const double mr = p.mainM * pnl;
+  const bool mc = (equity <= -mr) || ((balance + pnl) <= -mr);
+  const bool insuff_same = (availM <= fabs(price * u)) || (balance <= 0.);
+  const int risk = opp ? (insuff_opp ? MGN_INSUFF_MARGIN : MGN_GREEN)
+                       : (mc ? MGN_MARGIN_CALL : (insuff_same ? MGN_INSUFF_MARGIN : MGN_GREEN));
+  // Broker.cpp:128-135 and Portfolio::handleTransaction, Portfolio.cpp:284-323
+  const double slippage = (price * p.slip_rel) + p.slip_abs;
+  const double tprice = u < 0 ? (price - slippage) : (price + slippage);
+  const double tcost = fabs(u * price) * p.tc_rel + p.tc_abs;
+  const bool close = opp && (fabs(u) > fabs(cur));
+  const double units = close ? u + cur : u;
+  const double c1 = close ? cash + cur * tprice : cash;
+  const double cu1 = close ? 0. : cur;
+  const double me0 = s.mep[MM];
+  const double me_avg = me0 + (tprice - me0) * (u / (u + cur));
+  const double me1 = close ? tprice : (opp ? me0 : me_avg);
+  const double amt = tprice * units;
+  const double use = amt * p.reqM;
+  const double brw = amt - use;
+  const double bm0 = s.Bm[MM];
+  const double bm1 = bm0 + brw;
+  const double c2 = c1 - (use + tcost);
+  const double cu2 = cu1 + units;
+  const bool closed = fabs(cu2) < 0.000001;
+  const double me2 = closed ? 0. : me1;
+  const bool repay = closed && (bm1 > 0.);
+  const double c3 = repay ? c2 - bm1 : c2;
+  const double bm2 = repay ? 0. : bm1;
+  const bool neg = bm2 < 0.;
+  const double c4 = neg ? c3 - bm2 : c3;
+  const double bm3 = neg ? 0. : bm2;
+  const bool go = act && (risk == MGN_GREEN);
+  rk[MM] = act ? risk : rk[MM];
+  s.L[MM] = go ? cu2 : cur;
+  s.mep[MM] = go ? me2 : me0;
+  s.Bm[MM] = go ? bm3 : bm0;
+  tp[MM] = go ? tprice : tp[MM];
+  tu[MM] = go ? u : tu[MM];
+  tc[MM] = go ? tcost : tc[MM];
+  cash = seg_bcast<S, J>(go ? c4 : cash);
 }
 
-// Rounds in asset order i = 0..A-1 (Broker.cpp:149-155); J, MM compile-time.
+// Rounds in asset order i = 0..APAD-1 (Broker.cpp:149-155); padding slots
+// i >= A carry units 0 and change nothing.
 template <int M, int S, int I>
 struct Rounds {
   static __device__ __forceinline__ void run(Lane<M>& s, const KParams& p, double& cash,
@@ -432,7 +430,6 @@ struct Rounds {
                                              double (&tu)[M], double (&tc)[M], int (&rk)[M],
                                              int ls) {
     if constexpr (I < M * S) {
-      if (I >= p.A) return;
       broker_round<M, S, I / M, I % M>(s, p, cash, uc, tp, tu, tc, rk, ls);
       Rounds<M, S, I + 1>::run(s, p, cash, uc, tp, tu, tc, rk, ls);
     }
@@ -539,174 +536,200 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
       act_next[m] = s.valid[m] ? act_in[(size_t)env * A + s.asset[m]] : 0;
   }
 
-  for (int k = 0; k < K; ++k) {
+  // Per-segment state machine: a segment either steps (k < K) or runs the
+  // source ticks of an auto-reset (Env::reset's getData + initialize_history,
+  // `pending` of them), so one inlined getData serves both paths.
+  int k = 0;
+  int pending = 0;
+  while (true) {
+    const bool stepping = (pending == 0) && (k < K);
+    const bool ticking = stepping || (pending > 0);
+    if (__ballot(ticking) == 0) break;
     const size_t oN = (size_t)k * p.N, oNA = (size_t)k * p.N * A;
-    // ---- action -> units for this lane's slots
-    double uc[M];
-    const double prevEq = (cash + s0.lp) - s0.b;  // Env.h:208
-    if (in_kind == IN_DISCRETE) {                  // dqn.py:160-179
-      const double avM = ((cash + s0.sh) + (s0.lp - s0.ml)) / p.reqM;
-      const int half = p.atoms / 2;
-      int8_t act_cur[M];
-#pragma unroll
-      for (int m = 0; m < M; ++m) {
-        act_cur[m] = act_next[m];
-        if (k + 1 < K && s.valid[m])
-          act_next[m] = act_in[oNA + (size_t)p.N * A + (size_t)env * A + s.asset[m]];
-      }
-#pragma unroll
-      for (int m = 0; m < M; ++m) {
-        uc[m] = 0.;
-        if (!s.valid[m]) continue;
-        const int a = act_cur[m];
-        const double u = p.unit_size * avM / s.P[m];
-        uc[m] = (double)(a - half) * u;
-        if (a == 0) uc[m] = (s.L[m] != 0) ? -s.L[m] : 0.;
-      }
-    } else if (in_kind == IN_UNITS) {
-#pragma unroll
-      for (int m = 0; m < M; ++m)
-        uc[m] = s.valid[m] ? units_in[oNA + (size_t)env * A + s.asset[m]] : 0.;
-    } else if (in_kind == IN_SINGLE) {
-      const int ai = aidx_in[env];
-      const double u = units_in[oN + env];
-#pragma unroll
-      for (int m = 0; m < M; ++m) uc[m] = (s.valid[m] && s.asset[m] == ai) ? u : 0.;
-    } else {
-#pragma unroll
-      for (int m = 0; m < M; ++m) uc[m] = 0.;
-    }
-    double prevVal[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) prevVal[m] = s.L[m] * s.P[m];
-
-    // ---- Broker::handleTransaction(units): serial rounds over assets
-    double tp[M], tu[M], tc[M];
+    double uc[M], prevVal[M], tp[M], tu[M], tc[M];
     int rk[M];
+    double prevEq = 0.;
+    int mcall = 0;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       tp[m] = 0.;
       tu[m] = 0.;
       tc[m] = 0.;
       rk[m] = MGN_GREEN;
+      uc[m] = 0.;
     }
-    if (!(p.ablate & 1)) Rounds<M, S, 0>::run(s, p, cash, uc, tp, tu, tc, rk, ls);
-    // BrokerResponse.marginCall (Broker.cpp:156-157)
-    int mcall = 0;
-    if (in_kind != IN_NONE) {
-      const Sums q = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
-      mcall = margin_call(q, cash, p.mainM) ? 1 : 0;
-    }
-
-    // ---- dataSource->getData()
-    if (!(p.ablate & 2)) gen_tick<M>(s, p, env, ts);
-    ts += 1;
-
-    // ---- reward / done (Env.h:211-223)
-    const Sums q = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
-    const double curEq = (cash + q.lp) - q.b;
-    const double ratio = curEq / prevEq;
-    const double clampv = (in_kind == IN_SINGLE) ? 0.01 : 0.3;
-    const double reward = log((ratio < clampv) ? clampv : ratio);
-    int bad = 0;
+    if (stepping) {
+      // ---- action -> units for this lane's slots
+      prevEq = (cash + s0.lp) - s0.b;  // Env.h:208
+      if (in_kind == IN_DISCRETE) {     // dqn.py:160-179
+        const double avM = div_reqm((cash + s0.sh) + (s0.lp - s0.ml), p);
+        const int half = p.atoms / 2;
+        int8_t act_cur[M];
 #pragma unroll
-    for (int m = 0; m < M; ++m) bad |= (rk[m] != MGN_GREEN && rk[m] != MGN_INSUFF_MARGIN) ? 1 : 0;
-    bad = seg_or<S>(bad);
-    const bool done = bad || margin_call(q, cash, p.mainM) || (curEq < 0.1 * p.init_cash);
-
-    // ---- State.portfolio = ledgerNormedFull (Portfolio.cpp:150-155)
-    const double port0 = (cash - q.b) / curEq;
-    double portA[M];
+        for (int m = 0; m < M; ++m) {
+          act_cur[m] = act_next[m];
+          if (k + 1 < K && s.valid[m])
+            act_next[m] = act_in[oNA + (size_t)p.N * A + (size_t)env * A + s.asset[m]];
+        }
 #pragma unroll
-    for (int m = 0; m < M; ++m) portA[m] = (s.L[m] * s.P[m]) / curEq;
-
-    // ---- agent-side per-asset reward (offpolicy_q.py:152-164)
-    double ar[M];
+        for (int m = 0; m < M; ++m) {
+          if (!s.valid[m]) continue;
+          const int a = act_cur[m];
+          const double u = p.unit_size * avM / s.P[m];
+          uc[m] = (double)(a - half) * u;
+          if (a == 0) uc[m] = (s.L[m] != 0) ? -s.L[m] : 0.;
+        }
+      } else if (in_kind == IN_UNITS) {
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-      if (!s.valid[m] || !need_ar) {
-        ar[m] = 0.;
-        continue;
+        for (int m = 0; m < M; ++m)
+          uc[m] = s.valid[m] ? units_in[oNA + (size_t)env * A + s.asset[m]] : 0.;
+      } else if (in_kind == IN_SINGLE) {
+        const int ai = aidx_in[env];
+        const double u = units_in[oN + env];
+#pragma unroll
+        for (int m = 0; m < M; ++m) uc[m] = (s.valid[m] && s.asset[m] == ai) ? u : 0.;
       }
-      double v = (((s.L[m] * s.P[m]) - prevVal[m]) - (tu[m] * tp[m] + tc[m])) / prevEq;
-      v += 1;
-      v = (v < .35) ? .35 : v;
-      ar[m] = (p.ablate & 8) ? v : log(v);
+#pragma unroll
+      for (int m = 0; m < M; ++m) prevVal[m] = s.L[m] * s.P[m];
+      // ---- Broker::handleTransaction(units): serial rounds over assets
+      if (in_kind != IN_NONE && !(p.ablate & 1)) Rounds<M, S, 0>::run(s, p, cash, uc, tp, tu, tc, rk, ls);
+      // BrokerResponse.marginCall (Broker.cpp:156-157)
+      if (in_kind != IN_NONE) {
+        const Sums q = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
+        mcall = margin_call(q, cash, p.mainM) ? 1 : 0;
+      }
     }
-    // ---- reward shaping
-    double cos_term = 0.;
-    if (p.shaper == MGN_SHAPER_PPC) {
-      double pp[M], pq[M];
+    if (ticking) {
+      // ---- dataSource->getData()
+      if (!(p.ablate & 2)) gen_tick<M>(s, p, env, ts);
+      ts += 1;
+    }
+    if (stepping) {
+      // ---- reward / done (Env.h:211-223)
+      const Sums q = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
+      const double curEq = (cash + q.lp) - q.b;
+      const double ratio = curEq / prevEq;
+      const double clampv = (in_kind == IN_SINGLE) ? 0.01 : 0.3;
+      const double reward = log((ratio < clampv) ? clampv : ratio);
+      int bad = 0;
+#pragma unroll
+      for (int m = 0; m < M; ++m) bad |= (rk[m] != MGN_GREEN && rk[m] != MGN_INSUFF_MARGIN) ? 1 : 0;
+      bad = seg_or<S>(bad);
+      const bool done = bad || margin_call(q, cash, p.mainM) || (curEq < 0.1 * p.init_cash);
+
+      // ---- State.portfolio = ledgerNormedFull (Portfolio.cpp:150-155)
+      const double port0 = (cash - q.b) / curEq;
+      double portA[M];
+#pragma unroll
+      for (int m = 0; m < M; ++m) portA[m] = (s.L[m] * s.P[m]) / curEq;
+
+      // ---- agent-side per-asset reward (offpolicy_q.py:152-164)
+      double ar[M];
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        const double qv = s.valid[m] ? p.target[1 + s.asset[m]] : 0.;
-        const double pv = s.valid[m] ? portA[m] : 0.;
-        pp[m] = pv * pv;
-        pq[m] = pv * qv;
+        if (!s.valid[m] || !need_ar) {
+          ar[m] = 0.;
+          continue;
+        }
+        double v = (((s.L[m] * s.P[m]) - prevVal[m]) - (tu[m] * tp[m] + tc[m])) / prevEq;
+        v += 1;
+        v = (v < .35) ? .35 : v;
+        ar[m] = (p.ablate & 8) ? v : log(v);
       }
-      const double np_ = sqrt(port0 * port0 + canon<M, S>(pp));
-      const double dot = port0 * p.target[0] + canon<M, S>(pq);
-      cos_term = p.cos_temp * (dot / (np_ * cos_qn));
-    }
-    double shaped_s = 0., rin_s = 0.;
-    double shaped_v[M];
-    if (D == 1) {
-      rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
-      shaped_s = shape(p.shaper, rin_s, shA[0], shB[0], p.eta, cos_term);
-    } else {
+      // ---- reward shaping
+      double cos_term = 0.;
+      if (p.shaper == MGN_SHAPER_PPC) {
+        double pp[M], pq[M];
 #pragma unroll
-      for (int m = 0; m < M; ++m)
-        shaped_v[m] = s.valid[m] ? shape(p.shaper, ar[m], shA[m], shB[m], p.eta, cos_term) : 0.;
-    }
-
-    // ---- outputs
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      if (!s.valid[m] || (p.ablate & 4)) continue;
-      const size_t i = oNA + (size_t)env * A + s.asset[m];
-      if (out.obs_price) out.obs_price[i] = s.P[m];
-      if (out.tprice) out.tprice[i] = tp[m];
-      if (out.tunits) out.tunits[i] = tu[m];
-      if (out.tcost) out.tcost[i] = tc[m];
-      if (out.risk) out.risk[i] = (uint8_t)rk[m];
-      if (out.obs_port) out.obs_port[(size_t)k * p.N * (A + 1) + (size_t)env * (A + 1) + 1 + s.asset[m]] = portA[m];
-      if (D != 1) {
-        if (out.agent_reward) out.agent_reward[i] = ar[m];
-        if (out.shaped) out.shaped[i] = shaped_v[m];
+        for (int m = 0; m < M; ++m) {
+          const double qv = s.valid[m] ? p.target[1 + s.asset[m]] : 0.;
+          const double pv = s.valid[m] ? portA[m] : 0.;
+          pp[m] = pv * pv;
+          pq[m] = pv * qv;
+        }
+        const double np_ = sqrt(port0 * port0 + canon<M, S>(pp));
+        const double dot = port0 * p.target[0] + canon<M, S>(pq);
+        cos_term = p.cos_temp * (dot / (np_ * cos_qn));
       }
-    }
-    if (ls == 0 && !(p.ablate & 4)) {
-      if (out.reward) out.reward[oN + env] = reward;
-      if (out.done) out.done[oN + env] = done ? 1 : 0;
-      if (out.timestamp) out.timestamp[oN + env] = ts;
-      if (out.margin_call) out.margin_call[oN + env] = (uint8_t)mcall;
-      if (out.obs_port) out.obs_port[(size_t)k * p.N * (A + 1) + (size_t)env * (A + 1)] = port0;
+      double shaped_s = 0., rin_s = 0.;
+      double shaped_v[M];
       if (D == 1) {
-        if (out.agent_reward) out.agent_reward[oN + env] = rin_s;
-        if (out.shaped) out.shaped[oN + env] = shaped_s;
+        rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
+        shaped_s = shape(p.shaper, rin_s, shA[0], shB[0], p.eta, cos_term);
+      } else {
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+          shaped_v[m] = s.valid[m] ? shape(p.shaper, ar[m], shA[m], shB[m], p.eta, cos_term) : 0.;
       }
-    }
 
-    // ---- episode statistics
-    ep_ret += reward;
-    ep_len += 1;
-    if (done) {
-      if (ls == 0) {
-        double* st = p.epstats + (size_t)env * 4;
-        st[0] = ep_ret;
-        st[1] = ep_len;
-        st[2] = curEq;
-        st[3] = st[3] + 1;
+      // ---- outputs
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        if (!s.valid[m] || (p.ablate & 4)) continue;
+        const size_t i = oNA + (size_t)env * A + s.asset[m];
+        if (out.obs_price) out.obs_price[i] = s.P[m];
+        if (out.tprice) out.tprice[i] = tp[m];
+        if (out.tunits) out.tunits[i] = tu[m];
+        if (out.tcost) out.tcost[i] = tc[m];
+        if (out.risk) out.risk[i] = (uint8_t)rk[m];
+        if (out.obs_port) out.obs_port[(size_t)k * p.N * (A + 1) + (size_t)env * (A + 1) + 1 + s.asset[m]] = portA[m];
+        if (D != 1) {
+          if (out.agent_reward) out.agent_reward[i] = ar[m];
+          if (out.shaped) out.shaped[i] = shaped_v[m];
+        }
       }
-      ep_ret = 0;
-      ep_len = 0;
-    }
-    // ---- window + auto reset
-    if (p.W > 0) ring_push<M, S>(s, p, env, ls, cash, ts, head, len);
-    s0 = q;
-    if (done && p.auto_reset) {
-      env_reset<M, S>(s, p, env, ls, cash, ts, head, len);
-      s0 = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
+      if (ls == 0 && !(p.ablate & 4)) {
+        if (out.reward) out.reward[oN + env] = reward;
+        if (out.done) out.done[oN + env] = done ? 1 : 0;
+        if (out.timestamp) out.timestamp[oN + env] = ts;
+        if (out.margin_call) out.margin_call[oN + env] = (uint8_t)mcall;
+        if (out.obs_port) out.obs_port[(size_t)k * p.N * (A + 1) + (size_t)env * (A + 1)] = port0;
+        if (D == 1) {
+          if (out.agent_reward) out.agent_reward[oN + env] = rin_s;
+          if (out.shaped) out.shaped[oN + env] = shaped_s;
+        }
+      }
+
+      // ---- episode statistics
+      ep_ret += reward;
+      ep_len += 1;
+      if (done) {
+        if (ls == 0) {
+          double* st = p.epstats + (size_t)env * 4;
+          st[0] = ep_ret;
+          st[1] = ep_len;
+          st[2] = curEq;
+          st[3] = st[3] + 1;
+        }
+        ep_ret = 0;
+        ep_len = 0;
+      }
+      // ---- window; agent reset (offpolicy_q.py:199-201)
+      if (p.W > 0) ring_push<M, S>(s, p, env, ls, cash, ts, head, len);
+      s0 = q;
+      k += 1;
+      if (done && p.auto_reset) {
+        // Env::reset (Env.h:181-187): source reset + fresh Broker; its getData
+        // and initialize_history's no-action ticks run as pending ticks
+        src_reset<M>(s, p);
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          s.L[m] = 0.;
+          s.mep[m] = 0.;
+          s.Bm[m] = 0.;
+        }
+        cash = p.init_cash;
+        if (p.W > 0) {
+          len = 0;
+          head = p.W - 1;
+        }
+        pending = p.W > 0 ? p.W : 1;
+      }
+    } else if (pending > 0) {
+      // ---- a reset tick: stream the State (preprocessor.py:172-194)
+      if (p.W > 0) ring_push<M, S>(s, p, env, ls, cash, ts, head, len);
+      pending -= 1;
+      if (pending == 0) s0 = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
     }
   }
 

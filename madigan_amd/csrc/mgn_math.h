@@ -4,7 +4,7 @@
 // the wall clock (madigan/environments/cpp/DataSource.cpp:472, :1131, :1407),
 // so its streams cannot be replayed.  This framework's variates are a fixed
 // specification instead: Philox4x32-10 keyed by (seed), counter
-// (tick, env, asset|slot<<16), Box-Muller on 53-bit uniforms, with fdlibm's
+// (tick, env, asset|slot<<16), Box-Muller (53-bit radius, 32-bit angle), with fdlibm's
 // log/sin/cos kernels evaluated in plain IEEE binary64 (compiled with
 // -ffp-contract=off) so every host restatement reproduces the device bits.
 #pragma once
@@ -23,25 +23,29 @@ __device__ __forceinline__ u4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c
                                             uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t lo0 = 0xD2511F53u * c0;
-    const uint32_t hi0 = __umulhi(0xD2511F53u, c0);
-    const uint32_t lo1 = 0xCD9E8D57u * c2;
-    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2);
-    const uint32_t n0 = hi1 ^ c1 ^ k0;
-    const uint32_t n2 = hi0 ^ c3 ^ k1;
-    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    // one v_mad_u64_u32 per product gives both halves
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
   return u4{c0, c1, c2, c3};
 }
 
+__device__ __forceinline__ u4 block(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot,
+                                    uint64_t tick) {
+  return philox4x32_10((uint32_t)tick, (uint32_t)env, asset | (slot << 16),
+                       (uint32_t)(tick >> 32) ^ (uint32_t)(env >> 32), (uint32_t)seed,
+                       (uint32_t)(seed >> 32));
+}
+
 // two 53-bit integers from one Philox block
 __device__ __forceinline__ void draw53(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot,
                                        uint64_t tick, uint64_t& a, uint64_t& b) {
-  const u4 x = philox4x32_10((uint32_t)tick, (uint32_t)env, asset | (slot << 16),
-                             (uint32_t)(tick >> 32) ^ (uint32_t)(env >> 32), (uint32_t)seed,
-                             (uint32_t)(seed >> 32));
+  const u4 x = block(seed, env, asset, slot, tick);
   a = (((uint64_t)x.y << 32) | x.x) >> 11;
   b = (((uint64_t)x.w << 32) | x.z) >> 11;
 }
@@ -157,14 +161,28 @@ __device__ __noinline__ double det_sin(double x) {
   return (q >= 2) ? -v : v;
 }
 
-// standard normal: Box-Muller on one Philox block
-__device__ __forceinline__ double normal(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot,
-                                         uint64_t tick) {
-  uint64_t a, b;
-  draw53(seed, env, asset, slot, tick, a, b);
+constexpr double TWO_M32 = 2.3283064365386962890625e-10;
+
+// Variates of one (env, asset, tick) from its slot-0 block x0..x3:
+//   u1 = ((x1:x0 >> 11) + 1) 2^-53 in (0,1],  u2 = x2 2^-32 in [0,1)
+//   z  = sqrt(-2 log u1) cos(2 pi u2)            (Box-Muller)
+//   ut = x3 2^-32 in [0,1)                        (TrendOU regime switch)
+//   dbit = x0 & 1                                 (TrendOU direction, a bit u1 drops)
+struct Draw {
+  double z, ut;
+  uint32_t dbit;
+};
+
+__device__ __forceinline__ Draw draw0(uint64_t seed, uint64_t env, uint32_t asset, uint64_t tick) {
+  const u4 x = block(seed, env, asset, 0, tick);
+  const uint64_t a = (((uint64_t)x.y << 32) | x.x) >> 11;
   const double u1 = (double)(a + 1) * TWO_M53;
-  const double u2 = (double)b * TWO_M53;
-  return sqrt(-2.0 * det_log(u1)) * det_cos2pi(u2);
+  const double u2 = (double)x.z * TWO_M32;
+  Draw d;
+  d.z = sqrt(-2.0 * det_log(u1)) * det_cos2pi(u2);
+  d.ut = (double)x.w * TWO_M32;
+  d.dbit = x.x & 1u;
+  return d;
 }
 
 }  // namespace mgn

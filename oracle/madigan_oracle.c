@@ -181,13 +181,33 @@ double orc_sin(double x) {
   }
 }
 
-/* Box-Muller on one Philox block: z = sqrt(-2 log u1) cos(2 pi u2), u1 in (0,1]. */
-double orc_normal(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot, uint64_t tick) {
-  uint64_t a, b;
-  draw(seed, env, asset, slot, tick, &a, &b);
+static const double TWO_M32 = 2.3283064365386962890625e-10; /* 2^-32 */
+
+/* Variates of one (env, asset, tick) from its slot-0 Philox block x0..x3:
+ *   u1 = ((x1:x0 >> 11) + 1) 2^-53 in (0,1],  u2 = x2 2^-32 in [0,1)
+ *   z  = sqrt(-2 log u1) cos(2 pi u2)           (Box-Muller)
+ *   ut = x3 2^-32                                (TrendOU regime-switch uniform)
+ *   dbit = x0 & 1                                (TrendOU direction; u1 drops it) */
+void orc_draw0(uint64_t seed, uint64_t env, uint32_t asset, uint64_t tick, double *z, double *ut,
+               uint32_t *dbit) {
+  uint32_t ctr[4] = {(uint32_t)tick, (uint32_t)env, asset,
+                     (uint32_t)(tick >> 32) ^ (uint32_t)(env >> 32)};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t x[4];
+  orc_philox4x32_10(ctr, key, x);
+  uint64_t a = (((uint64_t)x[1] << 32) | x[0]) >> 11;
   double u1 = (double)(a + 1) * TWO_M53;
-  double u2 = (double)b * TWO_M53;
-  return sqrt(-2.0 * orc_log(u1)) * orc_cos2pi(u2);
+  double u2 = (double)x[2] * TWO_M32;
+  *z = sqrt(-2.0 * orc_log(u1)) * orc_cos2pi(u2);
+  *ut = (double)x[3] * TWO_M32;
+  *dbit = x[0] & 1u;
+}
+
+double orc_normal(uint64_t seed, uint64_t env, uint32_t asset, uint64_t tick) {
+  double z, ut;
+  uint32_t b;
+  orc_draw0(seed, env, asset, tick, &z, &ut, &b);
+  return z;
 }
 
 /* Canonical reduction: pairwise tree over v[0..n-1], padded with +0.0 to the
@@ -376,14 +396,14 @@ static void src_get_data(orc_batch *b, int e) {
     switch (b->src[i].kind) {
       case ORC_SRC_SINE: { /* Synth::getData, DataSource.cpp:535-543 */
         double noise = 0.0;
-        if (p[5] != 0.0) noise = orc_normal(seed, genv, (uint32_t)i, 0, tick) * p[5] + 0.0;
+        if (p[5] != 0.0) noise = orc_normal(seed, genv, (uint32_t)i, tick) * p[5] + 0.0;
         const double PI2 = 3.141592653589793238463 * 2;
         s->P[i] = noise + p[1] + p[2] * orc_sin(PI2 * s->x[i] * p[0]);
         s->x[i] += p[4];
         break;
       }
       case ORC_SRC_OU: { /* OU::getData, DataSource.cpp:1173-1180 */
-        double z = orc_normal(seed, genv, (uint32_t)i, 0, tick) * 1.0 + 0.0;
+        double z = orc_normal(seed, genv, (uint32_t)i, tick) * 1.0 + 0.0;
         double x = s->P[i];
         x += (p[1] * (p[0] - x)) + p[0] * p[2] * z;
         s->P[i] = x;
@@ -391,8 +411,11 @@ static void src_get_data(orc_batch *b, int e) {
       }
       case ORC_SRC_TRENDOU: { /* TrendOU::getData, DataSource.cpp:1457-1493 */
         double y = s->P[i];
+        double z, u_trend;
+        uint32_t dbit;
+        orc_draw0(seed, genv, (uint32_t)i, tick, &z, &u_trend, &dbit);
         if (s->trending[i]) {
-          double n = orc_normal(seed, genv, (uint32_t)i, 0, tick) * p[8] + 0.0;
+          double n = z * p[8] + 0.0;
           y += y * (s->dY[i] * (double)s->dir[i] + n);
           s->tlen[i] -= 1;
           if (s->tlen[i] == 0) {
@@ -402,17 +425,15 @@ static void src_get_data(orc_batch *b, int e) {
           y = (0.01 < y) ? y : 0.01;   /* std::max(0.01, y) */
           if (y <= .1) s->dir[i] = 1;
         } else {
-          double n = orc_normal(seed, genv, (uint32_t)i, 0, tick) * p[7] + 0.0;
+          double n = z * p[7] + 0.0;
           double ou_noise = y * n;
           double ou_reverting_component = p[6] * (s->ouMean[i] - y);
           y += ou_reverting_component + ou_noise;
-          double u_trend, u_dir;
-          orc_uniform2(seed, genv, (uint32_t)i, 1, tick, &u_trend, &u_dir);
           if (u_trend < p[0]) {
             double u_len, u_dy;
-            orc_uniform2(seed, genv, (uint32_t)i, 2, tick, &u_len, &u_dy);
+            orc_uniform2(seed, genv, (uint32_t)i, 1, tick, &u_len, &u_dy);
             s->trending[i] = 1;
-            s->dir[i] = (u_dir < 0.5) ? -1 : 1;
+            s->dir[i] = dbit ? -1 : 1;
             int32_t lo = (int32_t)p[1], hi = (int32_t)p[2];
             int32_t len = lo + (int32_t)(u_len * (double)(hi - lo + 1));
             if (len > hi) len = hi;

@@ -175,7 +175,9 @@ void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t ou
 double orc_log(double x);
 double orc_sin(double x);
 double orc_cos2pi(double u);
-double orc_normal(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot, uint64_t tick);
+double orc_normal(uint64_t seed, uint64_t env, uint32_t asset, uint64_t tick);
+void orc_draw0(uint64_t seed, uint64_t env, uint32_t asset, uint64_t tick, double *z, double *ut,
+               uint32_t *dbit);
 void orc_uniform2(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot, uint64_t tick,
                   double *u0, double *u1);
 double orc_canon_sum(const double *v, int n);

@@ -102,7 +102,8 @@ def lib(fast: bool = False):
         for fn in (L.orc_log, L.orc_sin, L.orc_cos2pi):
             fn.argtypes = [C.c_double]
             fn.restype = C.c_double
-        L.orc_normal.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64]
+        L.orc_normal.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64]
+        L.orc_draw0.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, P, P, P]
         L.orc_normal.restype = C.c_double
         L.orc_uniform2.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64,
                                    P, P]

@@ -1,0 +1,95 @@
+"""The random-variate specification and the generators' statistics.
+
+The reference seeds std::default_random_engine from the wall clock
+(DataSource.cpp:472, :1131, :1407), so its draws cannot be replayed: generator
+parity with the reference is distributional ("parity unpinned" bitwise), and
+bitwise between the oracle and the HIP kernels (tests/test_gpu_parity.py).
+These tests pin the specification itself: Philox4x32-10 against the Random123
+known-answer vectors, the fdlibm log/sin/cos against libm, the variates'
+moments, and each generator's statistics against its reference formula.
+"""
+import ctypes as C
+import math
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.configs import ou_sources, trendou_sources
+
+
+@pytest.mark.parametrize("ctr,key,expect", [  # Random123 kat_vectors, philox4x32 10 rounds
+    ([0, 0, 0, 0], [0, 0], [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]),
+    ([0xffffffff] * 4, [0xffffffff] * 2, [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]),
+    ([0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344], [0xa4093822, 0x299f31d0],
+     [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]),
+])
+def test_philox_kat(ctr, key, expect):
+    assert list(O.philox(ctr, key)) == expect
+
+
+def test_fdlibm_accuracy_vs_libm():
+    L = O.lib()
+    rng = np.random.default_rng(0)
+    for x in rng.uniform(1e-300, 1.0, 5000):
+        assert abs(L.orc_log(x) - math.log(x)) <= 2 * np.spacing(abs(math.log(x)))
+    for x in np.concatenate([rng.uniform(-1e5, 1e5, 5000), np.arange(1, 200) * math.pi]):
+        assert abs(L.orc_sin(x) - math.sin(x)) <= 2e-16 + 2 * np.spacing(abs(math.sin(x)))
+    for u in rng.uniform(0, 1, 5000):
+        assert abs(L.orc_cos2pi(u) - math.cos(2 * math.pi * u)) < 1e-15
+
+
+def test_variates_moments():
+    L = O.lib()
+    z, ut = np.zeros(200_000), np.zeros(200_000)
+    bit = np.zeros(200_000, np.uint32)
+    zz, uu, bb = C.c_double(), C.c_double(), C.c_uint32()
+    for i in range(200_000):
+        L.orc_draw0(11, i % 1000, i // 1000 % 8, i // 8000, C.byref(zz), C.byref(uu), C.byref(bb))
+        z[i], ut[i], bit[i] = zz.value, uu.value, bb.value
+    assert abs(z.mean()) < 0.01 and abs(z.std() - 1) < 0.01
+    assert abs(np.mean(z ** 4) - 3) < 0.1        # normal kurtosis
+    assert abs(ut.mean() - 0.5) < 0.005 and ut.min() >= 0 and ut.max() < 1
+    assert abs(bit.mean() - 0.5) < 0.01
+    assert abs(np.corrcoef(z[:-1], z[1:])[0, 1]) < 0.01
+
+
+def test_ou_stationary_moments():
+    """x += theta(mu-x) + mu*phi*N(0,1) (DataSource.cpp:1173-1180): stationary
+    mean mu, variance (mu phi)^2 / (1 - (1-theta)^2)."""
+    mu, theta, phi = 10.0, 0.08, 0.04
+    b = O.OracleBatch(dict(n_envs=400, seed=3), ou_sources(2, mu, theta, phi))
+    for _ in range(200):
+        b.step()
+    xs = []
+    for _ in range(300):
+        b.step()
+        xs.append(b.field(O.F_PRICE).copy())
+    x = np.array(xs)
+    var = (mu * phi) ** 2 / (1 - (1 - theta) ** 2)
+    assert abs(x.mean() - mu) < 0.05
+    assert abs(x.var() / var - 1) < 0.05
+
+
+def test_trendou_regime_switching_rate():
+    """Trend starts with probability trendProb per OU-regime tick and lasts
+    U{min..max} ticks (DataSource.cpp:1457-1493)."""
+    p = [0.01, 5, 15, 0.001, 0.005, 5.0, 0.15, 0.04, 0.001, 0.99]
+    b = O.OracleBatch(dict(n_envs=500, seed=7), trendou_sources(4, p))
+    starts = 0
+    ou_ticks = 0
+    lens = []
+    prev = b.field(O.F_TRENDING)
+    for _ in range(400):
+        ou_ticks += int((prev == 0).sum())
+        b.step()
+        cur = b.field(O.F_TRENDING)
+        new = (prev == 0) & (cur == 1)
+        starts += int(new.sum())
+        lens.extend(b.field(O.F_TLEN)[new].tolist())
+        prev = cur
+    rate = starts / ou_ticks
+    assert abs(rate - 0.01) < 0.001
+    assert min(lens) >= 5 and max(lens) <= 15 and abs(np.mean(lens) - 10) < 0.3
+    dirs = b.field(O.F_DIR)
+    assert set(np.unique(dirs)) <= {-1.0, 1.0}

@@ -13,4 +13,4 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAIT_ANY --output-format csv -d $OUT/pmc3 -o pmc3 -- $B > $OUT/pmc3.log 2>&1 || { echo "pmc3 failed"; tail -20 $OUT/pmc3.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc4 -o pmc4 -- $B > $OUT/pmc4.log 2>&1 || { echo "pmc4 failed"; tail -20 $OUT/pmc4.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc5 -o pmc5 -- $B > $OUT/pmc5.log 2>&1 || { echo "pmc5 failed"; tail -20 $OUT/pmc5.log; exit 1; }
-find $OUT -name "*.csv" | head -30
+find $OUT -name "*.csv"

@@ -793,30 +793,45 @@ void orc_action_to_units(orc_batch *b, const int8_t *actions, double *units) {
 static double *offs_d(double *p, size_t off) { return p ? p + off : NULL; }
 static uint8_t *offs_u8(uint8_t *p, size_t off) { return p ? p + off : NULL; }
 
-void orc_rollout(orc_batch *b, const int8_t *actions, int k_steps, const orc_out *out) {
+static orc_out out_at_step(const orc_batch *b, const orc_out *out, int k) {
   int N = b->N, A = b->A;
   int D = (b->cfg.reward_mode == ORC_REWARD_AGENT_PER_ASSET) ? A : 1;
-  double units[MAXA];
-  for (int k = 0; k < k_steps; ++k) {
-    size_t nA = (size_t)k * N * A, nN = (size_t)k * N;
-    orc_out o = *out;
-    o.reward = offs_d(out->reward, nN);
-    o.agent_reward = offs_d(out->agent_reward, nN * D);
-    o.shaped = offs_d(out->shaped, nN * D);
-    o.done = offs_u8(out->done, nN);
-    o.obs_price = offs_d(out->obs_price, nA);
-    o.obs_port = offs_d(out->obs_port, (size_t)k * N * (A + 1));
-    o.timestamp = out->timestamp ? out->timestamp + nN : NULL;
-    o.tprice = offs_d(out->tprice, nA);
-    o.tunits = offs_d(out->tunits, nA);
-    o.tcost = offs_d(out->tcost, nA);
-    o.risk = offs_u8(out->risk, nA);
-    o.margin_call = offs_u8(out->margin_call, nN);
-    for (int e = 0; e < N; ++e) {
-      action_to_units_one(b, e, actions + nA + (size_t)e * A, units);
+  size_t nA = (size_t)k * N * A, nN = (size_t)k * N;
+  orc_out o = *out;
+  o.reward = offs_d(out->reward, nN);
+  o.agent_reward = offs_d(out->agent_reward, nN * D);
+  o.shaped = offs_d(out->shaped, nN * D);
+  o.done = offs_u8(out->done, nN);
+  o.obs_price = offs_d(out->obs_price, nA);
+  o.obs_port = offs_d(out->obs_port, (size_t)k * N * (A + 1));
+  o.timestamp = out->timestamp ? out->timestamp + nN : NULL;
+  o.tprice = offs_d(out->tprice, nA);
+  o.tunits = offs_d(out->tunits, nA);
+  o.tcost = offs_d(out->tcost, nA);
+  o.risk = offs_u8(out->risk, nA);
+  o.margin_call = offs_u8(out->margin_call, nN);
+  return o;
+}
+
+/* Envs are independent, so each env runs its k steps on its own; with
+ * threads > 1 the envs are split statically over OpenMP threads (CPU
+ * baseline on all host cores; results identical to threads == 1). */
+void orc_rollout_mt(orc_batch *b, const int8_t *actions, int k_steps, const orc_out *out,
+                    int threads) {
+  int N = b->N, A = b->A;
+#pragma omp parallel for schedule(static) num_threads(threads > 0 ? threads : 1) if (threads > 1)
+  for (int e = 0; e < N; ++e) {
+    double units[MAXA];
+    for (int k = 0; k < k_steps; ++k) {
+      orc_out o = out_at_step(b, out, k);
+      action_to_units_one(b, e, actions + (size_t)k * N * A + (size_t)e * A, units);
       step_one(b, e, ORC_STEP_UNITS, units, 0, 0., &o);
     }
   }
+}
+
+void orc_rollout(orc_batch *b, const int8_t *actions, int k_steps, const orc_out *out) {
+  orc_rollout_mt(b, actions, k_steps, out, 1);
 }
 
 /* ---- state access -------------------------------------------------------- */

@@ -124,6 +124,8 @@ void orc_step(orc_batch *b, int kind, const double *units, const int32_t *asset_
 /* K fused steps driven by discrete actions (K,N,A) int8 through
  * action_to_transaction (dqn.py:160-179); out arrays are (K, ...). */
 void orc_rollout(orc_batch *b, const int8_t *actions, int k_steps, const orc_out *out);
+void orc_rollout_mt(orc_batch *b, const int8_t *actions, int k_steps, const orc_out *out,
+                    int threads);
 /* dqn.py:160-179 on the current state: actions (N,A) -> units (N,A) */
 void orc_action_to_units(orc_batch *b, const int8_t *actions, double *units);
 /* external prices for the next getData (N,A), ORC_SRC_EXTERNAL assets */

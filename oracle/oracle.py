@@ -79,6 +79,7 @@ def lib(fast: bool = False):
         L.orc_reset.argtypes = [P, P]
         L.orc_step.argtypes = [P, C.c_int, P, P, C.POINTER(Out)]
         L.orc_rollout.argtypes = [P, P, C.c_int, C.POINTER(Out)]
+        L.orc_rollout_mt.argtypes = [P, P, C.c_int, C.POINTER(Out), C.c_int]
         L.orc_action_to_units.argtypes = [P, P, P]
         L.orc_set_prices.argtypes = [P, P]
         L.orc_get_field.argtypes = [P, C.c_int, P]
@@ -196,11 +197,13 @@ class OracleBatch:
             self.L.orc_step(self.h, STEP_SINGLE, _ptr(u), _ptr(ix), C.byref(s))
         return o
 
-    def rollout(self, actions):
+    def rollout(self, actions, threads=1):
+        """K discrete-action steps; threads > 1 splits the envs over OpenMP
+        threads (identical results)."""
         a = np.ascontiguousarray(actions, dtype=np.int8)
         K = a.shape[0]
         o, s = self._alloc_out(K)
-        self.L.orc_rollout(self.h, _ptr(a), K, C.byref(s))
+        self.L.orc_rollout_mt(self.h, _ptr(a), K, C.byref(s), int(threads))
         return o
 
     def action_to_units(self, actions):

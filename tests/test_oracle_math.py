@@ -93,3 +93,19 @@ def test_trendou_regime_switching_rate():
     assert min(lens) >= 5 and max(lens) <= 15 and abs(np.mean(lens) - 10) < 0.3
     dirs = b.field(O.F_DIR)
     assert set(np.unique(dirs)) <= {-1.0, 1.0}
+
+
+def test_rollout_threads_identical():
+    """The all-cores CPU baseline (OpenMP over envs) computes the same
+    trajectories as the single-threaded oracle."""
+    p = [0.01, 5, 15, 0.001, 0.005, 5.0, 0.15, 0.04, 0.001, 0.99]
+    cfg = dict(n_envs=64, seed=5, transaction_cost_rel=0.02, slippage_rel=1e-4,
+               maintenance_margin=0.25, required_margin=1.0, reward_shaper="DDR",
+               adaptation_rate=0.001, unit_size=0.05, auto_reset=1)
+    acts = np.random.default_rng(1).integers(0, 3, (40, 64, 3)).astype(np.int8)
+    outs = []
+    for threads in (1, 4):
+        b = O.OracleBatch(dict(cfg), trendou_sources(3, p))
+        outs.append(b.rollout(acts, threads=threads))
+    for k in outs[0]:
+        np.testing.assert_array_equal(outs[0][k], outs[1][k])

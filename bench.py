@@ -110,6 +110,13 @@ def cpu_baseline(n_envs: int, A: int, budget_s: float = 12.0):
                        f"oracle/madigan_oracle.c built -O3 -march=x86-64-v3 -ffast-math")
 
 
+def kernel_name(env, A: int) -> str:
+    m = int(env.lib.mgn_get_layout(env.h))
+    apad = 1 << max(0, (A - 1).bit_length())
+    rq1 = "true" if env.cfg.required_margin == 1.0 else "false"
+    return f"mgn::k_step<{m},{apad // m},{rq1}>"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -120,6 +127,9 @@ def main():
     ap.add_argument("--assets", type=int, default=8)
     ap.add_argument("--layout", type=int, default=0, help="assets per lane (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sweep", action="store_true",
+                    help="also time 1/16/64/256 steps per launch (separate launches; keep it off "
+                         "when profiling, so the kernel's rocprof average is the headline's)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
 
@@ -198,6 +208,26 @@ def main():
     value = world * N * args.steps / elapsed
     episodes = int(gathered[:, 3].sum().item())
 
+    # steps fused per launch (K in {1, 16, 256} beside the headline);
+    # outside the timed region, rank 0 only
+    sweep = {}
+    if rank == 0 and args.sweep:
+        big = env.alloc_traj(256, fields=list(traj.keys()))
+        for K in (1, 16, 64, 256):
+            reps = max(2, 512 // K)
+            s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            out = {kk: v[:K] for kk, v in big.items()}
+            env.rollout(actions[:K], out=out)  # warm
+            s_ev.record(stream)
+            for r in range(reps):
+                env.rollout(actions[:K], out=out)
+            e_ev.record(stream)
+            torch.cuda.synchronize()
+            us = s_ev.elapsed_time(e_ev) * 1e3 / (reps * K)
+            b = bytes_per_env_step(A, K, env.D)
+            sweep[str(K)] = {"us_per_step": us, "env_steps_per_s": N / us * 1e6,
+                             "bytes_per_env_step": b, "achieved_GBs": N * b / us / 1e3}
+
     if rank == 0:
         workload = f"C3_trendou_{N}x{A}_fuse{steps_per_launch}"
         traffic = load_pmc_traffic(workload)
@@ -215,10 +245,12 @@ def main():
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": achieved_gbs / PEAK_HBM_GBS,
-                         "traffic": traffic, "kernel": f"mgn::k_step<1,{A}>",
+                         "traffic": traffic, "kernel": kernel_name(env, A),
                          "bytes_per_env_step": bpes, "avg_launch_us": avg_launch_s * 1e6},
             "episodes_completed": episodes,
         }
+        if sweep:
+            res["fusion_sweep"] = sweep
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(N, A, args.cpu_budget)
         print(json.dumps(res))

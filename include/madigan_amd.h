@@ -38,8 +38,9 @@
 extern "C" {
 #endif
 
-#define MGN_ABI_VERSION 1
+#define MGN_ABI_VERSION 2
 #define MGN_MAX_ASSETS 64
+#define MGN_MAX_NSTEP 64
 
 /* status codes; the Python layer maps them to the reference's exceptions */
 enum {
@@ -85,7 +86,7 @@ typedef struct {
   double maintenance_margin;
   double slippage_rel, slippage_abs;
   double tc_rel, tc_abs;
-  int32_t shaper;              /* MGN_SHAPER_* (n-step = 1) */
+  int32_t shaper;              /* MGN_SHAPER_* */
   int32_t reward_mode;         /* MGN_REWARD_* : raw reward fed to the shaper */
   double adaptation_rate;      /* DSR/DDR eta */
   double cosine_temp;          /* PPC alpha */
@@ -95,6 +96,10 @@ typedef struct {
   int32_t auto_reset;          /* reset done envs inside the step kernel */
   int32_t action_atoms;        /* discrete actions for mgn_rollout */
   double unit_size;            /* unit_size_proportion_avM */
+  int32_t nstep;               /* n-step return length (nstep_return), 1..MGN_MAX_NSTEP;
+                                  NStepBuffer semantics, nstep_buffer.py:315-356 */
+  int32_t pad2_;
+  double discount;             /* gamma of the n-step aggregation */
 } mgn_config;
 
 /* Per-step outputs.  For mgn_step they are the handle's buffers (see views);
@@ -102,7 +107,8 @@ typedef struct {
 typedef struct {
   double *reward;        /* (N)            env log reward                 */
   double *agent_reward;  /* (N) or (N,A)   offpolicy_q.py:152-164         */
-  double *shaped;        /* (N) or (N,A)   shaper output                  */
+  double *shaped;        /* (N[,n][,A])    shaped rewards popped this step, in
+                            pop order (n-step: (N,n) or (N,n,A); n == 1: (N) or (N,A)) */
   uint8_t *done;         /* (N)                                           */
   double *obs_price;     /* (N,A)          State.price                    */
   double *obs_port;      /* (N,A+1)        State.portfolio                */
@@ -112,6 +118,7 @@ typedef struct {
   double *tcost;         /* (N,A)                                         */
   uint8_t *risk;         /* (N,A)          RiskInfo                       */
   uint8_t *margin_call;  /* (N)                                           */
+  uint8_t *n_shaped;     /* (N)            number of shaped rewards popped (n-step) */
 } mgn_traj;
 
 /* Device pointers into the handle's arena (row-major, env-major). */
@@ -135,8 +142,10 @@ typedef struct {
   double *win_price, *win_port;                      /* (N,W,A), (N,W,A+1) gathered window */
   uint64_t *win_ts;                                  /* (N,W) */
   uint8_t *reset_mask;                               /* (N) staging for mgn_reset */
+  double *nstep_ring;                                /* (N,n,D) NStepBuffer rewards */
+  int32_t *nstep_len, *nstep_head;                   /* (N) fill count, oldest index */
   mgn_traj out;                                      /* mgn_step outputs */
-  int32_t n_envs, n_assets, window, reward_dim;
+  int32_t n_envs, n_assets, window, reward_dim, nstep, pad_;
 } mgn_views;
 
 /* Stand-alone StackerDiscrete ring (preprocessor.py:143-199), caller-owned

@@ -12,7 +12,8 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmadigan_hip.so")
 MAX_ASSETS = 64
-ABI_VERSION = 1
+ABI_VERSION = 2
+MAX_NSTEP = 64
 
 # status codes -> the reference's exception types (DataTypes.h:36-46, pybind11)
 OK, ERR_CONFIG, ERR_INDEX, ERR_LENGTH, ERR_DEVICE, ERR_ARG = range(6)
@@ -43,11 +44,12 @@ class Config(C.Structure):
         ("cosine_temp", C.c_double), ("desired_portfolio", C.c_double * (MAX_ASSETS + 1)),
         ("window", C.c_int32), ("norm_type", C.c_int32), ("auto_reset", C.c_int32),
         ("action_atoms", C.c_int32), ("unit_size", C.c_double),
+        ("nstep", C.c_int32), ("pad2_", C.c_int32), ("discount", C.c_double),
     ]
 
 
 TRAJ_FIELDS = ("reward", "agent_reward", "shaped", "done", "obs_price", "obs_port", "timestamp",
-               "tprice", "tunits", "tcost", "risk", "margin_call")
+               "tprice", "tunits", "tcost", "risk", "margin_call", "n_shaped")
 
 
 class Traj(C.Structure):
@@ -58,13 +60,13 @@ VIEW_PTR_FIELDS = ("ledger", "mean_entry", "borrowed", "prices", "sine_x", "ou_m
                    "trend_len", "trend_flags", "cash", "timestamp", "shaper_a", "shaper_b",
                    "ep_stats", "episode_stats", "ext_prices", "units", "asset_idx", "ring",
                    "ring_ts", "ring_head", "ring_len", "win_price", "win_port", "win_ts",
-                   "reset_mask")
+                   "reset_mask", "nstep_ring", "nstep_len", "nstep_head")
 
 
 class Views(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in VIEW_PTR_FIELDS] + [
         ("out", Traj), ("n_envs", C.c_int32), ("n_assets", C.c_int32), ("window", C.c_int32),
-        ("reward_dim", C.c_int32)]
+        ("reward_dim", C.c_int32), ("nstep", C.c_int32), ("pad_", C.c_int32)]
 
 
 class Ring(C.Structure):

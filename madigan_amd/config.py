@@ -191,7 +191,8 @@ def build_config(spec: SourceSpec, *, n_envs: int, init_cash: float = 1_000_000.
                  reward_shaper=None, reward_mode: str = "env_log", adaptation_rate: float = 0.001,
                  cosine_temp: float = 0.0, desired_portfolio=None, window: int = 0,
                  norm_type=None, auto_reset: bool = False, action_atoms: int = 3,
-                 unit_size: float = 0.05, seed: int = 0, env_offset: int = 0):
+                 unit_size: float = 0.05, seed: int = 0, env_offset: int = 0,
+                 nstep_return: int = 1, discount: float = 0.99):
     A = spec.n_assets
     if A < 1 or A > L.MAX_ASSETS:
         raise ValueError(f"n_assets must be in [1, {L.MAX_ASSETS}], got {A}")
@@ -221,6 +222,10 @@ def build_config(spec: SourceSpec, *, n_envs: int, init_cash: float = 1_000_000.
     c.auto_reset = 1 if auto_reset else 0
     c.action_atoms = int(action_atoms)
     c.unit_size = float(unit_size)
+    if not 1 <= int(nstep_return) <= L.MAX_NSTEP:
+        raise ConfigError(f"nstep_return must be in [1, {L.MAX_NSTEP}], got {nstep_return}")
+    c.nstep = int(nstep_return)  # config.py:126 (Agent/Model spec)
+    c.discount = float(discount)  # config.py:154
     srcs = (L.AssetSource * A)()
     for i, (k, p) in enumerate(zip(spec.kinds, spec.params)):
         srcs[i].kind = k

@@ -5,6 +5,7 @@
 // except in mgn_create's parameter upload and mgn_synchronize.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -48,6 +49,7 @@ struct mgn_env {
   mgn_views v;
   mgn_asset_source* src_dev;
   double* target_dev;
+  double* disc_dev;  // (n) gamma^i
   std::string err;
   int ablate = 0;
   int m = 1;  // assets per lane
@@ -58,7 +60,8 @@ namespace {
 struct Offsets {
   size_t L, mep, Bm, P, sx, oum, dy, tlen, tfl, cash, ts, sA, sB, ep, epstats, ext, units, aidx,
       ring, ring_ts, rhead, rlen, wprice, wport, wts, mask, reward, areward, shaped, done, obsp,
-      obsport, obsts, tprice, tunits, tcost, risk, mcall, src, target;
+      obsport, obsts, tprice, tunits, tcost, risk, mcall, nshaped, nring, nlen, nhead, disc, src,
+      target;
   size_t total;
 };
 
@@ -66,6 +69,7 @@ Offsets plan(const mgn_config* c) {
   const size_t N = (size_t)c->n_envs, A = (size_t)c->n_assets;
   const size_t W = (size_t)(c->window > 0 ? c->window : 0);
   const size_t D = (c->reward_mode == MGN_REWARD_AGENT_PER_ASSET) ? A : 1;
+  const size_t n = (size_t)(c->nstep > 0 ? c->nstep : 1);
   Layout l;
   Offsets o;
   o.L = l.add(N * A * 8);
@@ -96,7 +100,7 @@ Offsets plan(const mgn_config* c) {
   o.mask = l.add(N);
   o.reward = l.add(N * 8);
   o.areward = l.add(N * D * 8);
-  o.shaped = l.add(N * D * 8);
+  o.shaped = l.add(N * n * D * 8);
   o.done = l.add(N);
   o.obsp = l.add(N * A * 8);
   o.obsport = l.add(N * (A + 1) * 8);
@@ -106,6 +110,11 @@ Offsets plan(const mgn_config* c) {
   o.tcost = l.add(N * A * 8);
   o.risk = l.add(N * A);
   o.mcall = l.add(N);
+  o.nshaped = l.add(N);
+  o.nring = l.add(n > 1 ? N * n * D * 8 : 0);
+  o.nlen = l.add(N * 4);
+  o.nhead = l.add(N * 4);
+  o.disc = l.add(n * 8);
   o.src = l.add(A * sizeof(mgn_asset_source));
   o.target = l.add((A + 1) * 8);
   o.total = l.total;
@@ -137,6 +146,10 @@ int validate(const mgn_config* c, const mgn_asset_source* s, std::string& msg) {
     return MGN_ERR_CONFIG;
   }
   if (c->norm_type < 0 || c->norm_type > MGN_NORM_LOOKBACK_LOG) { msg = "unknown norm_type"; return MGN_ERR_CONFIG; }
+  if (c->nstep < 1 || c->nstep > MGN_MAX_NSTEP) {
+    msg = "nstep_return must be in [1, 64]";
+    return MGN_ERR_CONFIG;
+  }
   for (int i = 0; i < c->n_assets; ++i) {
     const int k = s[i].kind;
     if (k < MGN_SRC_EXTERNAL || k > MGN_SRC_TRENDOU) {
@@ -170,6 +183,8 @@ mgn::KParams kparams(const mgn_env* e) {
   p.ep = v.ep_stats; p.epstats = v.episode_stats; p.ext = v.ext_prices;
   p.ring = v.ring; p.ring_ts = v.ring_ts; p.rhead = v.ring_head; p.rlen = v.ring_len;
   p.src = e->src_dev; p.target = e->target_dev;
+  p.nstep = c.nstep; p.nring = v.nstep_ring; p.nlen = v.nstep_len; p.nhead = v.nstep_head;
+  p.disc = e->disc_dev;
   return p;
 }
 
@@ -285,9 +300,17 @@ int mgn_create(const mgn_config* cfg, const mgn_asset_source* sources, void* str
   v.out.timestamp = (uint64_t*)(b + o.obsts); v.out.tprice = (double*)(b + o.tprice);
   v.out.tunits = (double*)(b + o.tunits); v.out.tcost = (double*)(b + o.tcost);
   v.out.risk = (uint8_t*)(b + o.risk); v.out.margin_call = (uint8_t*)(b + o.mcall);
+  v.out.n_shaped = (uint8_t*)(b + o.nshaped);
+  v.nstep_ring = cfg->nstep > 1 ? (double*)(b + o.nring) : nullptr;
+  v.nstep_len = (int32_t*)(b + o.nlen); v.nstep_head = (int32_t*)(b + o.nhead);
   v.n_envs = e->N; v.n_assets = e->A; v.window = e->W; v.reward_dim = e->D;
+  v.nstep = cfg->nstep; v.pad_ = 0;
   e->src_dev = (mgn_asset_source*)(b + o.src);
   e->target_dev = (double*)(b + o.target);
+  e->disc_dev = (double*)(b + o.disc);
+  // discounts gamma^i = math.pow(gamma, i) (nstep_buffer.py:328), host libm pow
+  double disc[MGN_MAX_NSTEP];
+  for (int i = 0; i < cfg->nstep; ++i) disc[i] = std::pow(cfg->discount, (double)i);
 
   int rc = check_hip(e, hipMemsetAsync(e->arena, 0, o.total, e->stream), "hipMemsetAsync");
   if (rc == MGN_OK)
@@ -296,6 +319,9 @@ int mgn_create(const mgn_config* cfg, const mgn_asset_source* sources, void* str
   if (rc == MGN_OK)
     rc = check_hip(e, hipMemcpyAsync(e->target_dev, cfg->desired_portfolio, 8 * (e->A + 1),
                                      hipMemcpyHostToDevice, e->stream), "hipMemcpyAsync(target)");
+  if (rc == MGN_OK)
+    rc = check_hip(e, hipMemcpyAsync(e->disc_dev, disc, 8 * cfg->nstep, hipMemcpyHostToDevice,
+                                     e->stream), "hipMemcpyAsync(discounts)");
   if (rc == MGN_OK) {
     launch_init(e, 0, nullptr);
     rc = check_hip(e, hipGetLastError(), "k_init_reset");

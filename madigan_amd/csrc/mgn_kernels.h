@@ -49,6 +49,11 @@ struct KParams {
   int32_t *rhead, *rlen;
   const mgn_asset_source *src;  // (A)
   const double *target;         // (A+1)
+  // NStepBuffer (n > 1): ring (N,n,D), fill count / oldest index (N), gamma^i (n)
+  int nstep;
+  double *nring;
+  int32_t *nlen, *nhead;
+  const double *disc;
 };
 
 // ---------------------------------------------------------------------------
@@ -68,15 +73,16 @@ __device__ __forceinline__ double tree(const double (&v)[M]) {
 // DPP lane moves (VALU latency, no LDS crossbar).  Controls (gfx9 / gfx950):
 // quad_perm = p0 | p1<<2 | p2<<4 | p3<<6, row_mirror 0x140, row_half_mirror
 // 0x141, row_newbcast:n 0x150+n (broadcast lane n of each 16-lane row).
+// Every control used here reads an in-range lane, so bound_ctrl is set and no
+// "old" value has to be materialized; row_newbcast moves 64 bits in one
+// v_mov_b64_dpp.
 template <int CTRL>
 __device__ __forceinline__ int dpp_i32(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+  return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xF, 0xF, true);
 }
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
-  const int lo = dpp_i32<CTRL>(__double2loint(v));
-  const int hi = dpp_i32<CTRL>(__double2hiint(v));
-  return __hiloint2double(hi, lo);
+  return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xF, 0xF, true);
 }
 
 // Segment all-reduce over S aligned lanes.  Every stage pairs each lane with a
@@ -344,6 +350,12 @@ __device__ __forceinline__ void store_lane(const Lane<M>& s, const KParams& p, i
 }
 
 
+template <typename T>
+__device__ __forceinline__ T in_vgpr(T x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 // x / required_margin; x / 1.0 == x exactly in IEEE, so the common
 // required_margin == 1 case skips the division with identical bits.
 __device__ __forceinline__ double div_reqm(double x, const KParams& p) {
@@ -436,6 +448,257 @@ struct Rounds {
   }
 };
 
+// ---------------------------------------------------------------------------
+// Broker rounds, exchange form (APAD <= 16).
+//
+// Everything in one round except the risk check and the cash update depends
+// only on that round's own asset (its units, ledger, price): the transaction
+// price, cost, new ledger / mean entry / borrowed, the cash increments and the
+// four portfolio-sum leaves before and after the order.  Each lane computes
+// those for its own slots in parallel and publishes them to LDS (OrderRec).
+// The serial chain then runs redundantly in every lane of the segment, in
+// registers: risk check against the current sums, select the leaf, and update
+// the canonical pairwise tree along one leaf-to-root path (nodes whose leaves
+// are all decided are final; nodes with none decided keep their pre-order
+// value).  Every node is the same sum of the same two children as in the full
+// tree, so the sums are bit-identical to recomputing the canonical tree after
+// each order (and to the oracle).
+struct alignas(16) OrderRec {
+  double pre[4];   // leaves {L*P, mep*L, L*(mep*[L<0]), Bm} before the order
+  double post[4];  // the same leaves if the order executes
+  double aPX;      // |price*excess| (reversal) or |price*units| (same side)
+  double X1;       // close ? L*tprice : -0.0   (cash += X1 is exact when not closing)
+  double y;        // usedMargin + cost
+  double Z;        // borrowed repaid / negative-borrow cleared, else +0.0
+  uint32_t act, need_mc, need_insuff, pad;
+};
+template <int APAD>
+struct alignas(16) EnvRecs {
+  OrderRec r[APAD];
+  double pad[2];  // 16 B skew: the segments of a wave read distinct LDS banks
+};
+
+// heap-indexed canonical tree over APAD leaves: node K (1-based) spans
+// leaves [lo(K), hi(K)); leaves are nodes APAD..2APAD-1
+constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x / 2); }
+template <int APAD, int K>
+struct Node {
+  static constexpr int depth = ilog2(K);
+  static constexpr int span = APAD >> depth;
+  static constexpr int lo = (K - (1 << depth)) * span;
+  static constexpr int hi = lo + span;
+};
+
+// value of node K once leaves 0..R are decided (fin) and the rest are not (pre)
+template <int APAD, int K, int R>
+__device__ __forceinline__ double node_val(const double (&pre)[2 * APAD],
+                                           const double (&fin)[2 * APAD]) {
+  if constexpr (Node<APAD, K>::hi - 1 <= R) {
+    return fin[K];
+  } else if constexpr (Node<APAD, K>::lo > R) {
+    return pre[K];
+  } else {
+    return node_val<APAD, 2 * K, R>(pre, fin) + node_val<APAD, 2 * K + 1, R>(pre, fin);
+  }
+}
+
+// leaf R decided: finalize every ancestor whose last leaf is R
+template <int APAD, int K, int R>
+__device__ __forceinline__ void finalize_up(double (&fin)[2 * APAD]) {
+  if constexpr (K >= 1) {
+    if constexpr (Node<APAD, K>::hi - 1 == R) {
+      fin[K] = fin[2 * K] + fin[2 * K + 1];
+      finalize_up<APAD, K / 2, R>(fin);
+    }
+  }
+}
+
+template <int APAD, int K>
+__device__ __forceinline__ void build_pre(double (&pre)[2 * APAD]) {
+  if constexpr (K >= 2) {
+    pre[K] = pre[2 * K] + pre[2 * K + 1];
+    build_pre<APAD, K - 1>(pre);
+  }
+}
+
+using d2 = double __attribute__((ext_vector_type(2)));
+using v4u = uint32_t __attribute__((ext_vector_type(4)));
+
+// the per-round part of one OrderRec, as vector loads
+struct RoundIn {
+  d2 post01, post23, ax1, yz;
+  v4u fl;
+};
+template <int APAD>
+__device__ __forceinline__ RoundIn load_round(const EnvRecs<APAD>& er, int i) {
+  const d2* rv = reinterpret_cast<const d2*>(&er.r[i]);
+  RoundIn r;
+  r.post01 = rv[2];
+  r.post23 = rv[3];
+  r.ax1 = rv[4];
+  r.yz = rv[5];
+  r.fl = *reinterpret_cast<const v4u*>(&er.r[i].act);
+  return r;
+}
+
+// Portfolio::checkRisk(i, u) (Portfolio.cpp:254-279) + Broker cash update
+// (Broker.cpp:128-135, Portfolio.cpp:284-323) for round I; RQ1: required
+// margin == 1 (x / 1.0 == x, division skipped with identical bits).  The next
+// round's record is loaded before this round computes (LDS latency hidden),
+// and the logic is straight-line (no short-circuit branches).
+template <int M, int S, bool RQ1, int I>
+struct XRounds {
+  static constexpr int APAD = M * S;
+  static __device__ __forceinline__ void run(const EnvRecs<APAD>& er, const RoundIn& r,
+                                             const KParams& p, double& cash,
+                                             const double (&s0)[4], double (&pre)[4][2 * APAD],
+                                             double (&fin)[4][2 * APAD], bool (&go_own)[M],
+                                             int (&rk)[M], int& any_mc, int ls) {
+    if constexpr (I < APAD) {
+      RoundIn nxt;
+      if constexpr (I + 1 < APAD) nxt = load_round<APAD>(er, I + 1);
+      const double post[4] = {r.post01.x, r.post01.y, r.post23.x, r.post23.y};
+      double R[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if constexpr (I == 0) R[q] = s0[q];
+        else R[q] = node_val<APAD, 1, I - 1>(pre[q], fin[q]);
+      }
+      const double pnl = R[0] - R[1];
+      const double balance = cash + R[2];
+      const double bp = balance + pnl;
+      const double availM = RQ1 ? bp : bp / p.reqM;
+      const double equity = (cash + R[0]) - R[3];
+      const double mr = p.mainM * pnl;
+      const int mc = (r.fl.y != 0) & ((equity <= -mr) | (bp <= -mr));
+      const int insuff = (r.fl.z != 0) & ((availM <= r.ax1.x) | (balance <= 0.));
+      const int go = (r.fl.x != 0) & !mc & !insuff;
+      any_mc |= (r.fl.x != 0) & mc;
+      const double c4 = ((cash + r.ax1.y) - r.yz.x) - r.yz.y;
+      cash = go ? c4 : cash;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        fin[q][APAD + I] = go ? post[q] : pre[q][APAD + I];
+        finalize_up<APAD, (APAD + I) / 2, I>(fin[q]);
+      }
+      const int risk = mc ? MGN_MARGIN_CALL : (insuff ? MGN_INSUFF_MARGIN : MGN_GREEN);
+      const bool own = ls == I / M;
+      go_own[I % M] = own ? (go != 0) : go_own[I % M];
+      rk[I % M] = (own & (r.fl.x != 0)) ? risk : rk[I % M];
+      if constexpr (I + 1 < APAD)
+        XRounds<M, S, RQ1, I + 1>::run(er, nxt, p, cash, s0, pre, fin, go_own, rk, any_mc, ls);
+    }
+  }
+};
+
+// The whole Broker::handleTransaction(units) (Broker.cpp:144-158) for the
+// lane's segment, exchange form.  On return the lane's slots hold the new
+// ledger, tp/tu/tc/rk the responses, `after` the canonical sums of the
+// post-transaction portfolio, and any_mc whether any order of the segment
+// was refused with MARGIN_CALL (the env's done condition, Env.h:216-218).
+template <int M, int S, bool RQ1>
+__device__ __forceinline__ void broker_x(Lane<M>& s, const KParams& p, EnvRecs<M * S>& er,
+                                         double& cash, const Sums& s0, const double (&uc)[M],
+                                         double (&tp)[M], double (&tu)[M], double (&tc)[M],
+                                         int (&rk)[M], int ls, Sums& after, int& any_mc) {
+  constexpr int APAD = M * S;
+  double cu2[M], me2[M], bm3[M], tpr[M], tco[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const double u = uc[m];
+    const double cur = s.L[m];
+    const double price = s.P[m];
+    const double me0 = s.mep[m];
+    const double bm0 = s.Bm[m];
+    const bool opp = signbit(u) != signbit(cur);
+    const bool rev = u > -1 * cur;
+    const double excess = u + cur;
+    const double slippage = (price * p.slip_rel) + p.slip_abs;
+    const double tprice = u < 0 ? (price - slippage) : (price + slippage);
+    const double tcost = fabs(u * price) * p.tc_rel + p.tc_abs;
+    const bool close = opp && (fabs(u) > fabs(cur));
+    const double units = close ? u + cur : u;
+    const double cu1 = close ? 0. : cur;
+    double me1;
+    if (close) me1 = tprice;
+    else if (opp) me1 = me0;
+    else me1 = me0 + (tprice - me0) * (u / (u + cur));
+    const double amt = tprice * units;
+    const double use = amt * p.reqM;
+    const double brw = amt - use;
+    const double bm1 = bm0 + brw;
+    const double c2l = cu1 + units;
+    const bool closed = fabs(c2l) < 0.000001;
+    const bool repay = closed && (bm1 > 0.);
+    const bool neg = !repay && (bm1 < 0.);
+    cu2[m] = c2l;
+    me2[m] = closed ? 0. : me1;
+    bm3[m] = (repay || neg) ? 0. : bm1;
+    tpr[m] = tprice;
+    tco[m] = tcost;
+    OrderRec& r = er.r[ls * M + m];
+    const double mk0 = (cur < 0.) ? 1.0 : 0.0;
+    r.pre[0] = cur * price;
+    r.pre[1] = me0 * cur;
+    r.pre[2] = cur * (me0 * mk0);
+    r.pre[3] = bm0;
+    const double mk1 = (cu2[m] < 0.) ? 1.0 : 0.0;
+    r.post[0] = cu2[m] * price;
+    r.post[1] = me2[m] * cu2[m];
+    r.post[2] = cu2[m] * (me2[m] * mk1);
+    r.post[3] = bm3[m];
+    r.aPX = opp ? fabs(price * excess) : fabs(price * u);
+    r.X1 = close ? cur * tprice : -0.0;
+    r.y = use + tcost;
+    r.Z = (repay || neg) ? bm1 : 0.0;
+    const bool act = u != 0.;
+    r.act = act;
+    r.need_mc = !opp;
+    r.need_insuff = !opp || rev;
+    r.pad = 0;
+  }
+  // the segment's records are written by its own lanes: wave-scope ordering
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+  double pre[4][2 * APAD], fin[4][2 * APAD];
+#pragma unroll
+  for (int a = 0; a < APAD; ++a) {
+    const d2* rv = reinterpret_cast<const d2*>(&er.r[a]);
+    const d2 p01 = rv[0], p23 = rv[1];
+    pre[0][APAD + a] = p01.x;
+    pre[1][APAD + a] = p01.y;
+    pre[2][APAD + a] = p23.x;
+    pre[3][APAD + a] = p23.y;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) build_pre<APAD, APAD - 1>(pre[q]);
+  const double s0a[4] = {s0.lp, s0.ml, s0.sh, s0.b};
+  bool go_own[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) go_own[m] = false;
+  XRounds<M, S, RQ1, 0>::run(er, load_round<APAD>(er, 0), p, cash, s0a, pre, fin, go_own, rk,
+                             any_mc, ls);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const bool go = go_own[m];
+    s.L[m] = go ? cu2[m] : s.L[m];
+    s.mep[m] = go ? me2[m] : s.mep[m];
+    s.Bm[m] = go ? bm3[m] : s.Bm[m];
+    tp[m] = go ? tpr[m] : tp[m];
+    tu[m] = go ? uc[m] : tu[m];
+    tc[m] = go ? tco[m] : tc[m];
+  }
+  after.lp = fin[0][1];
+  after.ml = fin[1][1];
+  after.sh = fin[2][1];
+  after.b = fin[3][1];
+}
+
 // input selector
 enum { IN_NONE = 0, IN_UNITS = 1, IN_SINGLE = 2, IN_DISCRETE = 3 };
 
@@ -449,8 +712,14 @@ __device__ __forceinline__ double dsr_one(double r, double A, double B) {
   return (B * dA - (A * dB) / 2) / (a * sqrt(a) + 1.1920928955078125e-07);
 }
 __device__ __forceinline__ double ddr_one(double r, double A, double B) {
-  if (r > 0.) return (r - A / 2) / (sqrt(B) + 1.1920928955078125e-07);
-  return (B * (r - A / 2) - (A * (r * r)) / 2) / (B * sqrt(B) + 1.1920928955078125e-07);  // B^(3/2)
+  // r > 0: (r - A/2) / (sqrt(B) + eps); else (B(r - A/2) - A r^2/2) / (B^(3/2) + eps),
+  // B^(3/2) as B*sqrt(B); one division with the branch's operands selected
+  const double sB = sqrt(B);
+  const double h = r - A / 2;
+  const bool pos = r > 0.;
+  const double num = pos ? h : (B * h - (A * (r * r)) / 2);
+  const double den = (pos ? sB : B * sB) + 1.1920928955078125e-07;
+  return num / den;
 }
 __device__ __forceinline__ double clip1(double v) { return v < -1. ? -1. : (v > 1. ? 1. : v); }
 
@@ -475,16 +744,82 @@ __device__ __forceinline__ double shape(int shaper, double r, double& A, double&
   return r;
 }
 
+// NStepBuffer.add + pop_nstep_sarsd for reward column d of one env
+// (nstep_buffer.py:315-356 as replay_buffer.py:68-80 drives it): append v; pop
+// once if the buffer is full, every entry if done.  A pop aggregates the
+// whole buffer (L entries, discounts gamma^0..gamma^(L-1)): DSR/DDR
+// clip(sum_k gamma^k f(r_k; A, B) / L) and then A, B from the oldest reward
+// (:62-91, :128-162); PPC / none: sum_k gamma^k v_k, v = r (+ temp*cos for
+// PPC, stored at add time) (:182-204, :23-27).  Ring (n, D) per env, oldest
+// at `head`; out: the env's (n, D) row of this step, zero after the pops.
+__device__ __forceinline__ void nstep_column(const KParams& p, double* out, int env, int d, int D,
+                                          double v, bool done, int len, int head, double& A,
+                                          double& B) {
+  const int n = p.nstep;
+  double* ring = p.nring + (size_t)env * n * D;
+  ring[(size_t)((head + len) % n) * D + d] = v;
+  len += 1;
+  const bool sr = p.shaper == MGN_SHAPER_DSR || p.shaper == MGN_SHAPER_DDR;
+  int pops = 0;
+  while (len >= n || (done && len > 0)) {
+    double acc = 0.0;
+    for (int k = 0; k < len; ++k) {
+      const double r = ring[(size_t)((head + k) % n) * D + d];
+      double f = r;
+      if (p.shaper == MGN_SHAPER_DSR) f = dsr_one(r, A, B);
+      else if (p.shaper == MGN_SHAPER_DDR) f = ddr_one(r, A, B);
+      acc += p.disc[k] * f;
+    }
+    double res = acc;
+    if (sr) {
+      res = clip1(acc / len);
+      const double r0 = ring[(size_t)head * D + d];
+      A += p.eta * (r0 - A);
+      if (p.shaper == MGN_SHAPER_DSR) {
+        B += p.eta * (r0 * r0 - B);
+      } else {
+        double m = r0 < 0. ? r0 : 0.;
+        if (r0 != r0) m = r0;
+        B += p.eta * (m * m - B);
+      }
+    }
+    if (out) out[(size_t)pops * D + d] = res;
+    head = (head + 1) % n;
+    len -= 1;
+    pops += 1;
+    if (!done && len < n) break;
+  }
+  if (out)
+    for (int j = pops; j < n; ++j) out[(size_t)j * D + d] = 0.;
+}
+
 // ---------------------------------------------------------------------------
 // The fused step kernel: K consecutive Env steps per launch, state held in
 // registers between steps.  in_kind selects Env::step() / step(units) /
 // step(assetIdx, units) / discrete actions via action_to_transaction.
-template <int M, int S>
+// RQ1: required_margin == 1.0, where x / required_margin == x exactly and the
+// divisions are skipped.  NST: n-step aggregation (nstep > 1) compiled in.
+template <int M, int S, bool RQ1, bool NST>
 __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_kind,
                                                 const double* __restrict__ units_in,
                                                 const int32_t* __restrict__ aidx_in,
                                                 const int8_t* __restrict__ act_in, int K) {
+  // loop-invariant fp64 parameters live in VGPRs: the kernel is SGPR-bound
+  // (pointers), and an SGPR spill costs a v_readlane per use in the loop
+  p.init_cash = in_vgpr(p.init_cash);
+  p.reqM = in_vgpr(p.reqM);
+  p.mainM = in_vgpr(p.mainM);
+  p.slip_rel = in_vgpr(p.slip_rel);
+  p.slip_abs = in_vgpr(p.slip_abs);
+  p.tc_rel = in_vgpr(p.tc_rel);
+  p.tc_abs = in_vgpr(p.tc_abs);
+  p.eta = in_vgpr(p.eta);
+  p.cos_temp = in_vgpr(p.cos_temp);
+  p.unit_size = in_vgpr(p.unit_size);
   constexpr int EPB = BLOCK / S;  // envs per block
+  // exchange-form Broker rounds (LDS: M * 28 KB per block)
+  constexpr bool XCH = (M * S <= 16) && (M <= 2) && (S >= 2);
+  __shared__ EnvRecs<XCH ? M * S : 1> recs[XCH ? EPB : 1];
   const int tid = threadIdx.x;
   const int ls = tid % S;
   const int env = blockIdx.x * EPB + tid / S;
@@ -508,6 +843,11 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
     }
   }
   double ep_ret = p.ep[(size_t)env * 2], ep_len = p.ep[(size_t)env * 2 + 1];
+  int32_t nlen = 0, nhead = 0;  // NStepBuffer fill count / oldest index (n > 1)
+  if constexpr (NST) {
+    nlen = p.nlen[env];
+    nhead = p.nhead[env];
+  }
   int32_t head = 0, len = 0;
   if (p.W > 0) {
     head = p.rhead[env];
@@ -553,6 +893,8 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
     int rk[M];
     double prevEq = 0.;
     int mcall = 0;
+    Sums sa = s0;  // canonical sums after the Broker (ledger unchanged: s0)
+    int any_mc = 0;  // exchange form: some order refused with MARGIN_CALL
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       tp[m] = 0.;
@@ -565,7 +907,8 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
       // ---- action -> units for this lane's slots
       prevEq = (cash + s0.lp) - s0.b;  // Env.h:208
       if (in_kind == IN_DISCRETE) {     // dqn.py:160-179
-        const double avM = div_reqm((cash + s0.sh) + (s0.lp - s0.ml), p);
+        const double bp = (cash + s0.sh) + (s0.lp - s0.ml);
+        const double avM = RQ1 ? bp : bp / p.reqM;
         const int half = p.atoms / 2;
         int8_t act_cur[M];
 #pragma unroll
@@ -595,11 +938,17 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
 #pragma unroll
       for (int m = 0; m < M; ++m) prevVal[m] = s.L[m] * s.P[m];
       // ---- Broker::handleTransaction(units): serial rounds over assets
-      if (in_kind != IN_NONE && !(p.ablate & 1)) Rounds<M, S, 0>::run(s, p, cash, uc, tp, tu, tc, rk, ls);
-      // BrokerResponse.marginCall (Broker.cpp:156-157)
       if (in_kind != IN_NONE) {
-        const Sums q = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
-        mcall = margin_call(q, cash, p.mainM) ? 1 : 0;
+        if constexpr (XCH) {
+          if (!(p.ablate & 1)) {
+            broker_x<M, S, RQ1>(s, p, recs[tid / S], cash, s0, uc, tp, tu, tc, rk, ls, sa, any_mc);
+          }
+        } else {
+          if (!(p.ablate & 1)) Rounds<M, S, 0>::run(s, p, cash, uc, tp, tu, tc, rk, ls);
+          sa = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
+        }
+        // BrokerResponse.marginCall (Broker.cpp:156-157)
+        mcall = margin_call(sa, cash, p.mainM) ? 1 : 0;
       }
     }
     if (ticking) {
@@ -608,16 +957,27 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
       ts += 1;
     }
     if (stepping) {
-      // ---- reward / done (Env.h:211-223)
-      const Sums q = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
+      // ---- reward / done (Env.h:211-223).  Only the L*P sum sees the new
+      // prices; the ledger sums are the ones after the Broker.
+      Sums q = sa;
+      {
+        double tlp[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) tlp[m] = s.L[m] * s.P[m];
+        q.lp = canon<M, S>(tlp);
+      }
       const double curEq = (cash + q.lp) - q.b;
       const double ratio = curEq / prevEq;
       const double clampv = (in_kind == IN_SINGLE) ? 0.01 : 0.3;
       const double reward = log((ratio < clampv) ? clampv : ratio);
       int bad = 0;
+      if constexpr (XCH) {
+        bad = any_mc;  // every lane saw every round's risk
+      } else {
 #pragma unroll
-      for (int m = 0; m < M; ++m) bad |= (rk[m] != MGN_GREEN && rk[m] != MGN_INSUFF_MARGIN) ? 1 : 0;
-      bad = seg_or<S>(bad);
+        for (int m = 0; m < M; ++m) bad |= (rk[m] != MGN_GREEN && rk[m] != MGN_INSUFF_MARGIN) ? 1 : 0;
+        bad = seg_or<S>(bad);
+      }
       const bool done = bad || margin_call(q, cash, p.mainM) || (curEq < 0.1 * p.init_cash);
 
       // ---- State.portfolio = ledgerNormedFull (Portfolio.cpp:150-155)
@@ -656,13 +1016,38 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
       }
       double shaped_s = 0., rin_s = 0.;
       double shaped_v[M];
-      if (D == 1) {
-        rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
-        shaped_s = shape(p.shaper, rin_s, shA[0], shB[0], p.eta, cos_term);
-      } else {
+      constexpr bool nst = NST;
+      if (D == 1) rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
+      if constexpr (!NST) {
+        if (D == 1) {
+          shaped_s = shape(p.shaper, rin_s, shA[0], shB[0], p.eta, cos_term);
+        } else {
 #pragma unroll
-        for (int m = 0; m < M; ++m)
-          shaped_v[m] = s.valid[m] ? shape(p.shaper, ar[m], shA[m], shB[m], p.eta, cos_term) : 0.;
+          for (int m = 0; m < M; ++m)
+            shaped_v[m] = s.valid[m] ? shape(p.shaper, ar[m], shA[m], shB[m], p.eta, cos_term) : 0.;
+        }
+      } else {
+        // NStepBuffer add + pops (replay_buffer.py:68-80); every lane tracks the
+        // segment's fill count / oldest index, column owners touch the ring
+        const int n = p.nstep;
+        const int L1 = nlen + 1;
+        const int pops = done ? L1 : (L1 >= n ? 1 : 0);
+        const bool ppc = p.shaper == MGN_SHAPER_PPC;
+        double* row = (out.shaped && !(p.ablate & 4)) ? out.shaped + (oN + env) * (size_t)n * D : nullptr;
+        if (D == 1) {
+          if (ls == 0)
+            nstep_column(p, row, env, 0, 1, ppc ? rin_s + cos_term : rin_s, done, nlen, nhead,
+                         shA[0], shB[0]);
+        } else {
+#pragma unroll
+          for (int m = 0; m < M; ++m)
+            if (s.valid[m])
+              nstep_column(p, row, env, s.asset[m], D, ppc ? ar[m] + cos_term : ar[m], done, nlen,
+                           nhead, shA[m], shB[m]);
+        }
+        if (ls == 0 && out.n_shaped && !(p.ablate & 4)) out.n_shaped[oN + env] = (uint8_t)pops;
+        nhead = (nhead + pops) % n;
+        nlen = L1 - pops;
       }
 
       // ---- outputs
@@ -678,7 +1063,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
         if (out.obs_port) out.obs_port[(size_t)k * p.N * (A + 1) + (size_t)env * (A + 1) + 1 + s.asset[m]] = portA[m];
         if (D != 1) {
           if (out.agent_reward) out.agent_reward[i] = ar[m];
-          if (out.shaped) out.shaped[i] = shaped_v[m];
+          if (out.shaped && !nst) out.shaped[i] = shaped_v[m];
         }
       }
       if (ls == 0 && !(p.ablate & 4)) {
@@ -686,10 +1071,11 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
         if (out.done) out.done[oN + env] = done ? 1 : 0;
         if (out.timestamp) out.timestamp[oN + env] = ts;
         if (out.margin_call) out.margin_call[oN + env] = (uint8_t)mcall;
+        if (!NST && out.n_shaped) out.n_shaped[oN + env] = 1;
         if (out.obs_port) out.obs_port[(size_t)k * p.N * (A + 1) + (size_t)env * (A + 1)] = port0;
         if (D == 1) {
           if (out.agent_reward) out.agent_reward[oN + env] = rin_s;
-          if (out.shaped) out.shaped[oN + env] = shaped_s;
+          if (out.shaped && !nst) out.shaped[oN + env] = shaped_s;
         }
       }
 
@@ -746,6 +1132,10 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
     if (p.W > 0) {
       p.rhead[env] = head;
       p.rlen[env] = len;
+    }
+    if constexpr (NST) {
+      p.nlen[env] = nlen;
+      p.nhead[env] = nhead;
     }
     if (D == 1) {
       p.sA[env] = shA[0];

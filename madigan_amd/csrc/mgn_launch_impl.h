@@ -11,8 +11,18 @@ struct StepL {
   static void run(const StepArgs& a) {
     const int epb = BLOCK / S;
     const int grid = (a.p.N + epb - 1) / epb;
-    hipLaunchKernelGGL((k_step<M, S>), dim3(grid), dim3(BLOCK), 0, a.stream, a.p, a.out, a.in_kind,
-                       a.units, a.aidx, a.act, a.K);
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, a.stream, a.p, a.out, a.in_kind,
+                         a.units, a.aidx, a.act, a.K);
+    };
+    const bool nst = a.p.nstep > 1;
+    if (a.p.reqm_one) {
+      if (nst) go(k_step<M, S, true, true>);
+      else go(k_step<M, S, true, false>);
+    } else {
+      if (nst) go(k_step<M, S, false, true>);
+      else go(k_step<M, S, false, false>);
+    }
   }
 };
 template <int M, int S>

@@ -31,7 +31,7 @@ VALUATION_FIELDS = ("cash", "equity", "pnl", "balance", "availableMargin", "used
 
 StepOutput = namedtuple("StepOutput", ["reward", "done", "obs_price", "obs_port", "timestamp",
                                        "tprice", "tunits", "tcost", "risk", "margin_call",
-                                       "shaped", "agent_reward"])
+                                       "shaped", "agent_reward", "n_shaped"])
 
 
 def _torch():
@@ -125,12 +125,15 @@ class BatchedEnv:
                  reward_shaper=None, reward_mode: str = "env_log",
                  adaptation_rate: float = 0.001, cosine_temp: float = 0.0,
                  desired_portfolio=None, window: int = 0, norm_type=None,
-                 auto_reset: bool = False, action_atoms: int = 3, unit_size: float = 0.05):
+                 auto_reset: bool = False, action_atoms: int = 3, unit_size: float = 0.05,
+                 nstep_return: int = 1, discount: float = 0.99):
         torch = _torch()
         self.lib = L.load()
         if not torch.cuda.is_available():
             raise RuntimeError("madigan_amd needs a ROCm GPU (gfx950); there is no CPU fallback")
         self.device = torch.device(device if device is not None else "cuda")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.spec = spec
         self.cfg, self._srcs = build_config(
             spec, n_envs=n_envs, init_cash=init_cash, required_margin=required_margin,
@@ -140,7 +143,7 @@ class BatchedEnv:
             reward_mode=reward_mode, adaptation_rate=adaptation_rate, cosine_temp=cosine_temp,
             desired_portfolio=desired_portfolio, window=window, norm_type=norm_type,
             auto_reset=auto_reset, action_atoms=action_atoms, unit_size=unit_size, seed=seed,
-            env_offset=env_offset)
+            env_offset=env_offset, nstep_return=nstep_return, discount=discount)
         self.N = int(n_envs)
         self.A = spec.n_assets
         self.W = int(window)
@@ -158,6 +161,7 @@ class BatchedEnv:
         L.check(self.lib.mgn_get_views(self.h, C.byref(v)), self.h)
         self._v = v
         self.D = v.reward_dim
+        self.nstep = v.nstep
         self._build_views()
         self._val = torch.empty((self.N, 10), dtype=torch.float64, device=self.device)
 
@@ -209,10 +213,11 @@ class BatchedEnv:
             timestamp=self._t(o.timestamp, i64, (N,)), tprice=self._t(o.tprice, f64, NA),
             tunits=self._t(o.tunits, f64, NA), tcost=self._t(o.tcost, f64, NA),
             risk=self._t(o.risk, u8, NA), margin_call=self._t(o.margin_call, u8, (N,)),
-            shaped=self._t(o.shaped, f64, Dsh), agent_reward=self._t(o.agent_reward, f64, Dsh))
+            shaped=self._t(o.shaped, f64, self._shaped_shape()),
+            agent_reward=self._t(o.agent_reward, f64, Dsh), n_shaped=self._t(o.n_shaped, u8, (N,)))
         # the whole step-output block is contiguous in the arena: one D2H copy
         lo = o.reward - self.arena.data_ptr()
-        hi = o.margin_call - self.arena.data_ptr() + N
+        hi = o.n_shaped - self.arena.data_ptr() + N
         self._out_span = (lo, hi)
 
     def __del__(self):
@@ -279,19 +284,48 @@ class BatchedEnv:
                                       C.c_void_p(ix.data_ptr())), self.h)
         return self.out
 
-    def alloc_traj(self, k_steps: int, fields=None):
-        """(K, ...) device buffers for rollout outputs (None fields are skipped)."""
+    def _shaped_shape(self) -> tuple:
+        N, A, D, n = self.N, self.A, self.D, self.nstep
+        col = (N,) if D == 1 else (N, A)
+        return col if n == 1 else ((N, n) if D == 1 else (N, n, A))
+
+    def _traj_shapes(self, K: int) -> dict:
         torch = _torch()
-        K, N, A, D = k_steps, self.N, self.A, self.D
-        shapes = dict(reward=((K, N), torch.float64), agent_reward=(((K, N) if D == 1 else (K, N, A)), torch.float64),
-                      shaped=(((K, N) if D == 1 else (K, N, A)), torch.float64), done=((K, N), torch.uint8),
-                      obs_price=((K, N, A), torch.float64), obs_port=((K, N, A + 1), torch.float64),
-                      timestamp=((K, N), torch.int64), tprice=((K, N, A), torch.float64),
-                      tunits=((K, N, A), torch.float64), tcost=((K, N, A), torch.float64),
-                      risk=((K, N, A), torch.uint8), margin_call=((K, N), torch.uint8))
+        N, A, D, n = self.N, self.A, self.D, self.nstep
+        col = (N,) if D == 1 else (N, A)
+        sh = col if n == 1 else ((N, n) if D == 1 else (N, n, A))
+        return dict(reward=((K, N), torch.float64), agent_reward=((K,) + col, torch.float64),
+                    shaped=((K,) + sh, torch.float64), done=((K, N), torch.uint8),
+                    obs_price=((K, N, A), torch.float64), obs_port=((K, N, A + 1), torch.float64),
+                    timestamp=((K, N), torch.int64), tprice=((K, N, A), torch.float64),
+                    tunits=((K, N, A), torch.float64), tcost=((K, N, A), torch.float64),
+                    risk=((K, N, A), torch.uint8), margin_call=((K, N), torch.uint8),
+                    n_shaped=((K, N), torch.uint8))
+
+    def alloc_traj(self, k_steps: int, fields=None):
+        """(K, ...) device buffers for rollout outputs (None fields are skipped).
+        shaped is (K,N[,A]) for n == 1 and (K,N,n[,A]) for n-step, with
+        n_shaped (K,N) the number of entries popped per step."""
+        torch = _torch()
         fields = L.TRAJ_FIELDS if fields is None else fields
-        return {k: torch.empty(s, dtype=dt, device=self.device) for k, (s, dt) in shapes.items()
-                if k in fields}
+        return {k: torch.empty(s, dtype=dt, device=self.device)
+                for k, (s, dt) in self._traj_shapes(k_steps).items() if k in fields}
+
+    def _check_traj(self, out: dict, K: int) -> None:
+        """Every output the kernel will write must hold K steps of its field."""
+        shapes = self._traj_shapes(K)
+        for k, v in out.items():
+            if v is None:
+                continue
+            if k not in shapes:
+                raise ValueError(f"unknown output field {k!r}")
+            s, dt = shapes[k]
+            n = 1
+            for d in s:
+                n *= d
+            if v.dtype != dt or v.device != self.device or not v.is_contiguous() or v.numel() < n:
+                raise ValueError(f"output {k!r} must be a contiguous {dt} tensor on {self.device} "
+                                 f"with >= {n} elements {s}, got {tuple(v.shape)} {v.dtype}")
 
     @staticmethod
     def _traj_struct(out: dict) -> L.Traj:
@@ -311,6 +345,7 @@ class BatchedEnv:
             raise ValueError(f"actions must be (K, {self.N}, {self.A}), got {tuple(actions.shape)}")
         K = int(actions.shape[0])
         out = self.alloc_traj(K) if out is None else out
+        self._check_traj(out, K)
         t = self._traj_struct(out)
         L.check(self.lib.mgn_rollout(self.h, C.c_void_p(actions.data_ptr()), K, C.byref(t)), self.h)
         return out
@@ -319,8 +354,11 @@ class BatchedEnv:
         """K fused Env::step(units) from units (K,N,A) fp64."""
         torch = _torch()
         u = torch.as_tensor(units).to(self.device, torch.float64).contiguous()
+        if u.dim() != 3 or u.shape[1] != self.N or u.shape[2] != self.A:
+            raise ValueError(f"units must be (K, {self.N}, {self.A}), got {tuple(u.shape)}")
         K = int(u.shape[0])
         out = self.alloc_traj(K) if out is None else out
+        self._check_traj(out, K)
         t = self._traj_struct(out)
         L.check(self.lib.mgn_rollout_units(self.h, C.c_void_p(u.data_ptr()), K, C.byref(t)), self.h)
         return out
@@ -377,7 +415,8 @@ class BatchedEnv:
             return blob[off:off + n].view(dtype).reshape(shape)
         Dsh = (N,) if D == 1 else (N, A)
         return dict(reward=arr(o.reward, np.float64, (N,)), agent_reward=arr(o.agent_reward, np.float64, Dsh),
-                    shaped=arr(o.shaped, np.float64, Dsh), done=arr(o.done, np.uint8, (N,)),
+                    shaped=arr(o.shaped, np.float64, self._shaped_shape()),
+                    n_shaped=arr(o.n_shaped, np.uint8, (N,)), done=arr(o.done, np.uint8, (N,)),
                     obs_price=arr(o.obs_price, np.float64, (N, A)),
                     obs_port=arr(o.obs_port, np.float64, (N, A + 1)),
                     timestamp=arr(o.timestamp, np.uint64, (N,)), tprice=arr(o.tprice, np.float64, (N, A)),
@@ -770,6 +809,11 @@ def make_batched_env(config, n_envs: int, **kw) -> BatchedEnv:
     norm = _cfg_get(pconf, "norm", False)
     norm_type = kw.pop("norm_type", _cfg_get(pconf, "norm_type", None) if norm else None)
     shaper = kw.pop("reward_shaper", _cfg_get(rconf, "reward_shaper", None))
+    aconf = _cfg_get(config, "agent_config") or {}
+    nstep = int(kw.pop("nstep_return", _cfg_get(aconf, "nstep_return", 1) or 1))
+    discount = float(kw.pop("discount", _cfg_get(aconf, "discount", 0.99)))
+    unit = kw.pop("unit_size", _cfg_get(aconf, "unit_size_proportion_avM", 0.05))
+    atoms = int(kw.pop("action_atoms", _cfg_get(aconf, "action_atoms", 3) or 3))
     return BatchedEnv(
         spec, n_envs, init_cash=_cfg_get(config, "init_cash", 1_000_000.0),
         required_margin=_cfg_get(config, "required_margin", 1.0),
@@ -782,7 +826,8 @@ def make_batched_env(config, n_envs: int, **kw) -> BatchedEnv:
         cosine_temp=_cfg_get(rconf, "cosine_temp", 0.0),
         desired_portfolio=_cfg_get(rconf, "desired_portfolio", None) if shaper in (
             "cosine", "cosine_similarity", "cosine_port_shaper") else None,
-        window=window, norm_type=norm_type, **kw)
+        window=window, norm_type=norm_type, nstep_return=nstep, discount=discount,
+        unit_size=unit, action_atoms=atoms, **kw)
 
 
 def get_env_info(env: Env) -> dict:

@@ -252,6 +252,11 @@ struct orc_batch {
   orc_env *envs;
   double *ext;  /* (N,A) external prices */
   orc_ring ring; /* StackerDiscrete deques (preprocessor.py:150-152), F = A, P = A+1 */
+  /* NStepBuffer per env (nstep_buffer.py:315-356), oldest first: (N, n, D) values
+   * (raw reward; PPC: reward + temp*cos), fill count (N), discounts gamma^i */
+  double *nring;
+  int32_t *nlen;
+  double disc[ORC_MAX_NSTEP];
 };
 
 /* ---- Portfolio valuation (Portfolio.cpp:170-235) ------------------------ */
@@ -611,6 +616,7 @@ void orc_ppc(const double *rewards, const double *ports, int L, int D, int P, co
 
 orc_batch *orc_create(const orc_config *cfg, const orc_asset_src *srcs) {
   if (cfg->n_assets < 1 || cfg->n_assets > MAXA || cfg->n_envs < 1) return NULL;
+  if (cfg->nstep < 1 || cfg->nstep > ORC_MAX_NSTEP) return NULL;
   orc_batch *b = (orc_batch *)calloc(1, sizeof(orc_batch));
   b->cfg = *cfg;
   b->N = cfg->n_envs;
@@ -618,6 +624,12 @@ orc_batch *orc_create(const orc_config *cfg, const orc_asset_src *srcs) {
   memcpy(b->src, srcs, sizeof(orc_asset_src) * (size_t)b->A);
   b->envs = (orc_env *)calloc((size_t)b->N, sizeof(orc_env));
   b->ext = (double *)calloc((size_t)b->N * b->A, sizeof(double));
+  {
+    int D = (cfg->reward_mode == ORC_REWARD_AGENT_PER_ASSET) ? b->A : 1;
+    b->nring = (double *)calloc((size_t)b->N * cfg->nstep * D, sizeof(double));
+    b->nlen = (int32_t *)calloc((size_t)b->N, sizeof(int32_t));
+    for (int i = 0; i < cfg->nstep; ++i) b->disc[i] = pow(cfg->discount, (double)i); /* :328 */
+  }
   int W = cfg->window;
   if (W > 0) {
     orc_ring *r = &b->ring;
@@ -641,6 +653,8 @@ void orc_destroy(orc_batch *b) {
   free(b->ring.ring); free(b->ring.ring_ts); free(b->ring.head); free(b->ring.len);
   free(b->envs);
   free(b->ext);
+  free(b->nring);
+  free(b->nlen);
   free(b);
 }
 
@@ -665,6 +679,46 @@ static void agent_reward(const orc_env *s, int A, const double *prevVal, double 
     if (v != v) v = NAN;
     r[i] = log(v);
   }
+}
+
+/* NStepBuffer semantics as ReplayBuffer.add drives them (replay_buffer.py:68-80):
+ * append; if full (len >= n) pop one; if done pop until empty.  Each pop
+ * aggregates the whole buffer (len L) with discounts[:L]
+ * (nstep_buffer.py:337-356) -- DSR/DDR: clip(sum_k gamma^k f(r_k) / L) then
+ * update A,B from the oldest reward (:62-77, :128-142); PPC: sum_k gamma^k
+ * (r_k + temp*cos_k) (:182-204); none: sum_k r_k gamma^k (:23-27) -- and
+ * drops the oldest entry.  Returns the number of pops; out is (pops, D). */
+static int nstep_add(orc_batch *b, int e, int D, const double *rin, const double *port, int done,
+                     double *out) {
+  const orc_config *c = &b->cfg;
+  orc_env *s = &b->envs[e];
+  int n = c->nstep;
+  double *ring = b->nring + (size_t)e * n * D;
+  int L = b->nlen[e];
+  double cs = 0.;
+  if (c->shaper == ORC_SHAPER_PPC) cs = cosine_sim(port, c->desired_portfolio, b->A + 1);
+  for (int d = 0; d < D; ++d)
+    ring[(size_t)L * D + d] = (c->shaper == ORC_SHAPER_PPC) ? rin[d] + c->cosine_temp * cs : rin[d];
+  L += 1;
+  int pops = 0;
+  while (L >= n || (done && L > 0)) {
+    double *o = out + (size_t)pops * D;
+    if (c->shaper == ORC_SHAPER_DSR) orc_dsr(ring, L, D, b->disc, c->adaptation_rate, s->sA, s->sB, o);
+    else if (c->shaper == ORC_SHAPER_DDR) orc_ddr(ring, L, D, b->disc, c->adaptation_rate, s->sA, s->sB, o);
+    else {
+      for (int d = 0; d < D; ++d) {
+        double acc = 0.0;
+        for (int k = 0; k < L; ++k) acc += b->disc[k] * ring[(size_t)k * D + d];
+        o[d] = acc;
+      }
+    }
+    memmove(ring, ring + D, sizeof(double) * (size_t)(L - 1) * D);
+    L -= 1;
+    pops += 1;
+    if (!done && L < n) break;
+  }
+  b->nlen[e] = L;
+  return pops;
 }
 
 static void step_one(orc_batch *b, int e, int kind, const double *units, int32_t single_idx,
@@ -719,14 +773,19 @@ static void step_one(orc_batch *b, int e, int kind, const double *units, int32_t
   if (c->reward_mode == ORC_REWARD_ENV_LOG) rin[0] = reward;
   else if (c->reward_mode == ORC_REWARD_AGENT_SUM) rin[0] = ar_sum;
   else for (int i = 0; i < A; ++i) rin[i] = ar[i];
-  double shaped[MAXA];
-  const double one = 1.0;
-  if (c->shaper == ORC_SHAPER_DSR) orc_dsr(rin, 1, D, &one, c->adaptation_rate, s->sA, s->sB, shaped);
-  else if (c->shaper == ORC_SHAPER_DDR) orc_ddr(rin, 1, D, &one, c->adaptation_rate, s->sA, s->sB, shaped);
-  else if (c->shaper == ORC_SHAPER_PPC) {  /* cosine_port_shaper :182-204 */
-    double cs = cosine_sim(port, c->desired_portfolio, A + 1);
-    for (int d = 0; d < D; ++d) shaped[d] = 1.0 * (rin[d] + c->cosine_temp * cs);
-  } else for (int d = 0; d < D; ++d) shaped[d] = rin[d];
+  double shaped[ORC_MAX_NSTEP * MAXA];
+  int n_shaped = 1;
+  if (c->nstep == 1) {
+    const double one = 1.0;
+    if (c->shaper == ORC_SHAPER_DSR) orc_dsr(rin, 1, D, &one, c->adaptation_rate, s->sA, s->sB, shaped);
+    else if (c->shaper == ORC_SHAPER_DDR) orc_ddr(rin, 1, D, &one, c->adaptation_rate, s->sA, s->sB, shaped);
+    else if (c->shaper == ORC_SHAPER_PPC) {  /* cosine_port_shaper :182-204 */
+      double cs = cosine_sim(port, c->desired_portfolio, A + 1);
+      for (int d = 0; d < D; ++d) shaped[d] = 1.0 * (rin[d] + c->cosine_temp * cs);
+    } else for (int d = 0; d < D; ++d) shaped[d] = rin[d];
+  } else {
+    n_shaped = nstep_add(b, e, D, rin, port, done, shaped);
+  }
 
   /* outputs */
   size_t eA = (size_t)e * A;
@@ -736,9 +795,10 @@ static void step_one(orc_batch *b, int e, int kind, const double *units, int32_t
     else for (int i = 0; i < A; ++i) o->agent_reward[eA + i] = ar[i];
   }
   if (o->shaped) {
-    if (D == 1) o->shaped[e] = shaped[0];
-    else for (int i = 0; i < A; ++i) o->shaped[eA + i] = shaped[i];
+    size_t nD = (size_t)c->nstep * D;
+    for (size_t j = 0; j < nD; ++j) o->shaped[(size_t)e * nD + j] = j < (size_t)n_shaped * D ? shaped[j] : 0.;
   }
+  if (o->n_shaped) o->n_shaped[e] = (uint8_t)n_shaped;
   if (o->done) o->done[e] = (uint8_t)done;
   if (o->obs_price) for (int i = 0; i < A; ++i) o->obs_price[eA + i] = s->P[i];
   if (o->obs_port) for (int i = 0; i <= A; ++i) o->obs_port[(size_t)e * (A + 1) + i] = port[i];
@@ -800,7 +860,7 @@ static orc_out out_at_step(const orc_batch *b, const orc_out *out, int k) {
   orc_out o = *out;
   o.reward = offs_d(out->reward, nN);
   o.agent_reward = offs_d(out->agent_reward, nN * D);
-  o.shaped = offs_d(out->shaped, nN * D);
+  o.shaped = offs_d(out->shaped, nN * D * (size_t)b->cfg.nstep);
   o.done = offs_u8(out->done, nN);
   o.obs_price = offs_d(out->obs_price, nA);
   o.obs_port = offs_d(out->obs_port, (size_t)k * N * (A + 1));
@@ -810,6 +870,7 @@ static orc_out out_at_step(const orc_batch *b, const orc_out *out, int k) {
   o.tcost = offs_d(out->tcost, nA);
   o.risk = offs_u8(out->risk, nA);
   o.margin_call = offs_u8(out->margin_call, nN);
+  o.n_shaped = offs_u8(out->n_shaped, nN);
   return o;
 }
 

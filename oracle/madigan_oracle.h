@@ -29,6 +29,7 @@ extern "C" {
 #endif
 
 #define ORC_MAX_ASSETS 64
+#define ORC_MAX_NSTEP 64
 
 /* RiskInfo enum order: madigan/environments/cpp/DataTypes.h:70-75 */
 enum { ORC_GREEN = 0, ORC_INSUFF_MARGIN = 1, ORC_MARGIN_CALL = 2, ORC_BLOWN_OUT = 3 };
@@ -82,13 +83,17 @@ typedef struct {
   int32_t auto_reset;
   int32_t action_atoms;
   double unit_size;
+  int32_t nstep;               /* n-step return length (nstep_return), <= ORC_MAX_NSTEP */
+  int32_t pad2_;
+  double discount;             /* gamma of the n-step aggregation */
 } orc_config;
 
 /* Outputs of one step for all envs.  Any pointer may be NULL. */
 typedef struct {
   double *reward;        /* (N)     env log reward */
   double *agent_reward;  /* (N) or (N,A) per reward_mode */
-  double *shaped;        /* (N) or (N,A) shaper output */
+  double *shaped;        /* (N[,n],D) shaper outputs emitted this step, in pop order
+                            (n-step: (N,n,D); n == 1: (N,D)) */
   uint8_t *done;         /* (N) */
   double *obs_price;     /* (N,A)   State.price */
   double *obs_port;      /* (N,A+1) State.portfolio = ledgerNormedFull */
@@ -98,6 +103,7 @@ typedef struct {
   double *tcost;         /* (N,A) */
   uint8_t *risk;         /* (N,A) */
   uint8_t *margin_call;  /* (N) */
+  uint8_t *n_shaped;     /* (N) shaped rewards emitted this step (n-step) */
 } orc_out;
 
 /* StackerDiscrete deques of N envs: ring (N,W,F+P), ring_ts (N,W), head/len (N) */

@@ -48,13 +48,14 @@ class Config(C.Structure):
         ("cosine_temp", C.c_double), ("desired_portfolio", C.c_double * (MAXA + 1)),
         ("window", C.c_int32), ("norm_type", C.c_int32), ("auto_reset", C.c_int32),
         ("action_atoms", C.c_int32), ("unit_size", C.c_double),
+        ("nstep", C.c_int32), ("pad2_", C.c_int32), ("discount", C.c_double),
     ]
 
 
 class Out(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in (
         "reward", "agent_reward", "shaped", "done", "obs_price", "obs_port", "timestamp",
-        "tprice", "tunits", "tcost", "risk", "margin_call")]
+        "tprice", "tunits", "tcost", "risk", "margin_call", "n_shaped")]
 
 
 _LIB = {}
@@ -157,6 +158,8 @@ class OracleBatch:
         c.auto_reset = int(cfg.get("auto_reset", 0))
         c.action_atoms = int(cfg.get("action_atoms", 3))
         c.unit_size = float(cfg.get("unit_size", 0.05))
+        c.nstep = int(cfg.get("nstep_return", 1))              # config.py:126
+        c.discount = float(cfg.get("discount", 0.99))          # config.py:154
         self.cfg = c
         self.W = c.window
         self.D = self.A if c.reward_mode == 2 else 1
@@ -173,10 +176,13 @@ class OracleBatch:
     # -- outputs ---------------------------------------------------------
     def _alloc_out(self, K=None):
         N, A, D = self.N, self.A, self.D
+        n = self.cfg.nstep
         pre = () if K is None else (K,)
+        sh = ((N,) if D == 1 else (N, A)) if n == 1 else ((N, n) if D == 1 else (N, n, A))
         o = dict(
             reward=np.zeros(pre + (N,)), agent_reward=np.zeros(pre + ((N,) if D == 1 else (N, A))),
-            shaped=np.zeros(pre + ((N,) if D == 1 else (N, A))), done=np.zeros(pre + (N,), np.uint8),
+            shaped=np.zeros(pre + sh), n_shaped=np.zeros(pre + (N,), np.uint8),
+            done=np.zeros(pre + (N,), np.uint8),
             obs_price=np.zeros(pre + (N, A)), obs_port=np.zeros(pre + (N, A + 1)),
             timestamp=np.zeros(pre + (N,), np.uint64), tprice=np.zeros(pre + (N, A)),
             tunits=np.zeros(pre + (N, A)), tcost=np.zeros(pre + (N, A)),

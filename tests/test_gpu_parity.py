@@ -254,3 +254,34 @@ def test_layouts_bit_identical(gpu, A):
                 assert_bits(v, ref[k], f"M={m} {k}")
             else:
                 assert np.array_equal(v, ref[k]), f"M={m} {k}"
+
+
+@pytest.mark.parametrize("shaper,mode,n", [("DSR", "env_log", 5), ("DDR", "agent_per_asset", 4),
+                                          ("PPC", "env_log", 3), ("none", "agent_sum", 2),
+                                          ("DDR", "env_log", 20)])
+def test_nstep_rollout(gpu, shaper, mode, n):
+    """n-step aggregation (n > 1) with done flushes from forced
+    margin calls, over two launches (the buffer carries across launches)."""
+    N, A, K = 128, 3, 48
+    kw = dict(required_margin=0.02, maintenance_margin=0.25, transaction_cost_rel=0.02,
+              unit_size=0.9, auto_reset=1, init_cash=1e5, reward_shaper=shaper, reward_mode=mode,
+              adaptation_rate=0.01, cosine_temp=0.05, desired_portfolio=[0.4, 0.3, 0.2, 0.1],
+              nstep_return=n, discount=0.97)
+    g, orc = make_pair(trendou_sources(A, [0.2, 2, 6, 0.05, 0.2, 5.0, 0.15, 0.3, 0.2, 0.99]), N, **kw)
+    acts = g.generate_actions(2 * K, seed=21)
+    D = A if mode == "agent_per_asset" else 1
+    for half in range(2):
+        a = acts[half * K:(half + 1) * K]
+        out = g.rollout(a)
+        ref = orc.rollout(a.cpu().numpy())
+        host = {k: v.cpu().numpy() for k, v in out.items()}
+        assert ref["done"].sum() > 0
+        out_check({**host, "shaped": ref["shaped"]}, ref, f"nstep{half}", D)
+        assert np.array_equal(host["n_shaped"], ref["n_shaped"]), "n_shaped"
+        np.testing.assert_allclose(host["shaped"], ref["shaped"], rtol=1e-10, atol=1e-14,
+                                   err_msg="shaped")
+    ga, gb = g.shaper_a.cpu().numpy(), g.shaper_b.cpu().numpy()
+    if ga.ndim == 2:  # the oracle's scalar accessor reports the first column
+        ga, gb = ga[:, 0], gb[:, 0]
+    close(ga, orc.scalar("shaperA"), "A")
+    close(gb, orc.scalar("shaperB"), "B")

@@ -114,7 +114,8 @@ def kernel_name(env, A: int) -> str:
     m = int(env.lib.mgn_get_layout(env.h))
     apad = 1 << max(0, (A - 1).bit_length())
     rq1 = "true" if env.cfg.required_margin == 1.0 else "false"
-    return f"mgn::k_step<{m},{apad // m},{rq1}>"
+    nst = "true" if env.nstep > 1 else "false"
+    return f"mgn::k_step<{m}, {apad // m}, {rq1}, {nst}>"  # as rocprofv3 names it
 
 
 def main():

@@ -20,6 +20,9 @@
  *                     dqn.py:160-179); Env::step(units) } fused in one launch
  *   mgn_set_prices    DataSourceTick plug-in fed from the host
  *                     (DataSource.h:48-64, PyDataSource.h:9-24, Env.h:174-179)
+ *   mgn_attach_replay HDFSourceSingle as the env's DataSource (DataSource.h:89-149,
+ *                     DataSource.cpp:194-408): the device-resident replay tape
+ *                     staged by libmadigan_hdf.so (include/madigan_hdf.h)
  *   mgn_window*       StackerDiscrete.stream_state / current_data
  *                     (madigan/utils/preprocessor.py:143-199)
  *   mgn_get_views     zero-copy property views (env.cpp:897-913)
@@ -38,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MGN_ABI_VERSION 2
+#define MGN_ABI_VERSION 3
 #define MGN_MAX_ASSETS 64
 #define MGN_MAX_NSTEP 64
 
@@ -56,7 +59,8 @@ enum {
 enum { MGN_GREEN = 0, MGN_INSUFF_MARGIN = 1, MGN_MARGIN_CALL = 2, MGN_BLOWN_OUT = 3 };
 
 /* per-asset generator kind (DataSource.cpp:56-108 factory names) */
-enum { MGN_SRC_EXTERNAL = 0, MGN_SRC_SINE = 1, MGN_SRC_OU = 2, MGN_SRC_TRENDOU = 3 };
+enum { MGN_SRC_EXTERNAL = 0, MGN_SRC_SINE = 1, MGN_SRC_OU = 2, MGN_SRC_TRENDOU = 3,
+       MGN_SRC_REPLAY = 4 /* every asset of the env, from the attached replay tape */ };
 
 enum { MGN_SHAPER_NONE = 0, MGN_SHAPER_DSR = 1, MGN_SHAPER_DDR = 2, MGN_SHAPER_PPC = 3 };
 enum { MGN_REWARD_ENV_LOG = 0, MGN_REWARD_AGENT_SUM = 1, MGN_REWARD_AGENT_PER_ASSET = 2 };
@@ -69,7 +73,8 @@ enum { MGN_STEP_NONE = 0, MGN_STEP_UNITS = 1, MGN_STEP_SINGLE = 2 };
  *  SINE    p = {freq, mu, amp, phase, dX, noise}            DataSource.cpp:455-473
  *  OU      p = {mean, theta, phi}                           DataSource.cpp:1118-1137
  *  TRENDOU p = {trendProb, minPeriod, maxPeriod, dYMin, dYMax, start,
- *               theta, phi, noiseTrend, emaAlpha}           DataSource.cpp:1364-1408 */
+ *               theta, phi, noiseTrend, emaAlpha}           DataSource.cpp:1364-1408
+ *  REPLAY  p = {}  (all assets or none; see mgn_attach_replay) */
 typedef struct {
   int32_t kind;
   int32_t pad_;
@@ -100,6 +105,9 @@ typedef struct {
                                   NStepBuffer semantics, nstep_buffer.py:315-356 */
   int32_t pad2_;
   double discount;             /* gamma of the n-step aggregation */
+  int32_t n_feats;             /* F = State.price width: n_assets for the generators
+                                  (0 = n_assets); the feature columns of a replay source */
+  int32_t pad3_;
 } mgn_config;
 
 /* Per-step outputs.  For mgn_step they are the handle's buffers (see views);
@@ -110,7 +118,7 @@ typedef struct {
   double *shaped;        /* (N[,n][,A])    shaped rewards popped this step, in
                             pop order (n-step: (N,n) or (N,n,A); n == 1: (N) or (N,A)) */
   uint8_t *done;         /* (N)                                           */
-  double *obs_price;     /* (N,A)          State.price                    */
+  double *obs_price;     /* (N,F)          State.price (features; F = A for generators) */
   double *obs_port;      /* (N,A+1)        State.portfolio                */
   uint64_t *timestamp;   /* (N)            State.timestamp                */
   double *tprice;        /* (N,A)          BrokerResponse.transactionPrice */
@@ -119,6 +127,7 @@ typedef struct {
   uint8_t *risk;         /* (N,A)          RiskInfo                       */
   uint8_t *margin_call;  /* (N)                                           */
   uint8_t *n_shaped;     /* (N)            number of shaped rewards popped (n-step) */
+  uint8_t *data_end;     /* (N)            EnvInfo.dataEnd (Env.h:226; DataSource.h:126) */
 } mgn_traj;
 
 /* Device pointers into the handle's arena (row-major, env-major). */
@@ -136,17 +145,32 @@ typedef struct {
   double *ext_prices;                                /* (N,A) external source input */
   double *units;                                     /* (N,A) staging for mgn_step input */
   int32_t *asset_idx;                                /* (N)   staging for STEP_SINGLE */
-  double *ring;                                      /* (N,W,2A+1) window ring */
+  double *ring;                                      /* (N,W,F+A+1) window ring */
   uint64_t *ring_ts;                                 /* (N,W) */
   int32_t *ring_head, *ring_len;                     /* (N) */
-  double *win_price, *win_port;                      /* (N,W,A), (N,W,A+1) gathered window */
+  double *win_price, *win_port;                      /* (N,W,F), (N,W,A+1) gathered window */
   uint64_t *win_ts;                                  /* (N,W) */
   uint8_t *reset_mask;                               /* (N) staging for mgn_reset */
   double *nstep_ring;                                /* (N,n,D) NStepBuffer rewards */
   int32_t *nstep_len, *nstep_head;                   /* (N) fill count, oldest index */
+  int64_t *replay_cursor;                            /* (N) next tape row of a replay env */
   mgn_traj out;                                      /* mgn_step outputs */
-  int32_t n_envs, n_assets, window, reward_dim, nstep, pad_;
+  int32_t n_envs, n_assets, window, reward_dim, nstep, n_feats;
 } mgn_views;
+
+/* Replay tape (caller-owned device memory, borrowed until mgn_destroy): one
+ * period of the rows HDFSourceSingle::getData visits, in visiting order
+ * (mgn_hdf_stage fills it).  Env e (global index g = env_offset + e) starts
+ * at tape row (g * stride) mod rows; stride 0 replays the reference's single
+ * path in every env. */
+typedef struct {
+  const double *price;       /* (rows, A)  currentPrices */
+  const double *feats;       /* (rows, F)  currentData = State.price */
+  const uint64_t *ts;        /* (rows)     timestamps = State.timestamp */
+  const uint8_t *data_end;   /* (rows)     dataEnd() after that row */
+  int64_t rows;
+  int64_t stride;
+} mgn_replay_tape;
 
 /* Stand-alone StackerDiscrete ring (preprocessor.py:143-199), caller-owned
  * device memory: ring (N, W, n_price + n_port), ring_ts (N, W), head/len (N). */
@@ -181,6 +205,10 @@ int mgn_rollout(mgn_env *env, const int8_t *actions_dev, int32_t k_steps, const 
 int mgn_rollout_units(mgn_env *env, const double *units_dev, int32_t k_steps, const mgn_traj *out);
 /* prices (N,A) consumed by the next getData of MGN_SRC_EXTERNAL assets */
 int mgn_set_prices(mgn_env *env, const double *prices_dev);
+/* attach the replay tape of a MGN_SRC_REPLAY handle and run the Env
+ * constructor's first getData (Env.h:150-165) from it; stepping a replay
+ * handle before this fails with MGN_ERR_CONFIG */
+int mgn_attach_replay(mgn_env *env, const mgn_replay_tape *tape);
 /* StackerDiscrete.stream_state with explicit rows (any may be NULL = current State) */
 int mgn_window_push(mgn_env *env, const double *price_dev, const double *port_dev,
                     const uint64_t *ts_dev);

@@ -7,17 +7,20 @@ libmadigan_hip.so); this package is the host side mirroring the reference's
 Python surface (madigan/environments, madigan/utils/preprocessor.py).
 """
 from . import _lib
-from .config import ConfigError, SourceSpec, spec_from_config
+from .config import ConfigError, SourceSpec, replay_spec, spec_from_config
 from .env import (Asset, BatchedEnv, BrokerResponse, DataSourceTick, Env, EnvInfo, RiskInfo, State,
                   get_env_info, make_batched_env, make_env)
+from .hdf import HDFSourceSingle, write_hdf
 from .preprocessor import PreProcessor, StackerDiscrete, make_preprocessor
 
 __all__ = ["Asset", "BatchedEnv", "BrokerResponse", "ConfigError", "DataSourceTick", "Env",
-           "EnvInfo", "PreProcessor", "RiskInfo", "SourceSpec", "StackerDiscrete", "State",
-           "get_env_info", "make_batched_env", "make_env", "make_preprocessor",
-           "spec_from_config"]
+           "EnvInfo", "HDFSourceSingle", "PreProcessor", "RiskInfo", "SourceSpec",
+           "StackerDiscrete", "State", "get_env_info", "make_batched_env", "make_env",
+           "make_preprocessor", "replay_spec", "spec_from_config", "write_hdf"]
 
 
 def load_extension():
-    """Load libmadigan_hip.so (raises if it was not built)."""
+    """Load libmadigan_hip.so and libmadigan_hdf.so (raises if not built)."""
+    from .hdf import load_hdf
+    load_hdf()
     return _lib.load()

@@ -12,14 +12,14 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmadigan_hip.so")
 MAX_ASSETS = 64
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_NSTEP = 64
 
 # status codes -> the reference's exception types (DataTypes.h:36-46, pybind11)
 OK, ERR_CONFIG, ERR_INDEX, ERR_LENGTH, ERR_DEVICE, ERR_ARG = range(6)
 
 GREEN, INSUFF_MARGIN, MARGIN_CALL, BLOWN_OUT = range(4)
-SRC_EXTERNAL, SRC_SINE, SRC_OU, SRC_TRENDOU = range(4)
+SRC_EXTERNAL, SRC_SINE, SRC_OU, SRC_TRENDOU, SRC_REPLAY = range(5)
 SHAPER_NONE, SHAPER_DSR, SHAPER_DDR, SHAPER_PPC = range(4)
 REWARD_ENV_LOG, REWARD_AGENT_SUM, REWARD_AGENT_PER_ASSET = range(3)
 NORM_NONE, NORM_LOG, NORM_LOOKBACK, NORM_STANDARD_NORMAL, NORM_LOOKBACK_LOG = range(5)
@@ -45,11 +45,12 @@ class Config(C.Structure):
         ("window", C.c_int32), ("norm_type", C.c_int32), ("auto_reset", C.c_int32),
         ("action_atoms", C.c_int32), ("unit_size", C.c_double),
         ("nstep", C.c_int32), ("pad2_", C.c_int32), ("discount", C.c_double),
+        ("n_feats", C.c_int32), ("pad3_", C.c_int32),
     ]
 
 
 TRAJ_FIELDS = ("reward", "agent_reward", "shaped", "done", "obs_price", "obs_port", "timestamp",
-               "tprice", "tunits", "tcost", "risk", "margin_call", "n_shaped")
+               "tprice", "tunits", "tcost", "risk", "margin_call", "n_shaped", "data_end")
 
 
 class Traj(C.Structure):
@@ -60,13 +61,18 @@ VIEW_PTR_FIELDS = ("ledger", "mean_entry", "borrowed", "prices", "sine_x", "ou_m
                    "trend_len", "trend_flags", "cash", "timestamp", "shaper_a", "shaper_b",
                    "ep_stats", "episode_stats", "ext_prices", "units", "asset_idx", "ring",
                    "ring_ts", "ring_head", "ring_len", "win_price", "win_port", "win_ts",
-                   "reset_mask", "nstep_ring", "nstep_len", "nstep_head")
+                   "reset_mask", "nstep_ring", "nstep_len", "nstep_head", "replay_cursor")
 
 
 class Views(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in VIEW_PTR_FIELDS] + [
         ("out", Traj), ("n_envs", C.c_int32), ("n_assets", C.c_int32), ("window", C.c_int32),
-        ("reward_dim", C.c_int32), ("nstep", C.c_int32), ("pad_", C.c_int32)]
+        ("reward_dim", C.c_int32), ("nstep", C.c_int32), ("n_feats", C.c_int32)]
+
+
+class ReplayTape(C.Structure):
+    _fields_ = [("price", C.c_void_p), ("feats", C.c_void_p), ("ts", C.c_void_p),
+                ("data_end", C.c_void_p), ("rows", C.c_int64), ("stride", C.c_int64)]
 
 
 class Ring(C.Structure):
@@ -90,6 +96,7 @@ SYMBOLS = {
     "mgn_rollout": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(Traj)]),
     "mgn_rollout_units": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(Traj)]),
     "mgn_set_prices": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mgn_attach_replay": (C.c_int, [C.c_void_p, C.POINTER(ReplayTape)]),
     "mgn_window_push": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mgn_window_clear": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mgn_window": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),

@@ -35,8 +35,38 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm toolchain required)")
 
 
+HDF_OUT = os.path.join(HERE, "libmadigan_hdf.so")
+HDF_SRC = os.path.join(CSRC, "mgn_hdf.cpp")
+HDF5_PREFIX = os.environ.get("MADIGAN_HDF5_PREFIX", "/opt/conda")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+
 def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def build_hdf(force: bool = False, verbose: bool = False) -> str:
+    """libmadigan_hdf.so: the HDF replay reader / stager (host C++ over libhdf5
+    and the HIP runtime; no device code)."""
+    deps_ = [HDF_SRC, os.path.join(ROOT, "include", "madigan_hdf.h"),
+             os.path.join(ROOT, "include", "madigan_amd.h")]
+    if not force and os.path.exists(HDF_OUT) and all(
+            os.path.getmtime(d) <= os.path.getmtime(HDF_OUT) for d in deps_):
+        return HDF_OUT
+    inc, lib = os.path.join(HDF5_PREFIX, "include"), os.path.join(HDF5_PREFIX, "lib")
+    if not os.path.exists(os.path.join(inc, "hdf5.h")):
+        raise RuntimeError(f"hdf5.h not found under {inc} (set MADIGAN_HDF5_PREFIX)")
+    cmd = [shutil.which("g++") or "g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall",
+           "-D__HIP_PLATFORM_AMD__", f"-I{inc}", f"-I{ROCM}/include", "-o", HDF_OUT + ".tmp",
+           HDF_SRC, f"-L{lib}", "-lhdf5", f"-Wl,-rpath,{lib}", f"-L{ROCM}/lib", "-lamdhip64",
+           f"-Wl,-rpath,{ROCM}/lib"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"g++ failed on {HDF_SRC}:\n{r.stderr}")
+    os.replace(HDF_OUT + ".tmp", HDF_OUT)
+    return HDF_OUT
 
 
 def deps():
@@ -52,6 +82,7 @@ def needs_build() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
+    build_hdf(force=force, verbose=verbose)
     if not force and not needs_build():
         return OUT
     os.makedirs(OBJ, exist_ok=True)

@@ -11,6 +11,9 @@ Mirrors the reference's config handling for the data sources on the hot path:
               renamed code+"_1"                         DataSource.cpp:411-437
   default constructors Synth()/OU()/TrendOU()          DataSource.cpp:475-482, :1142,
                                                        :1418-1423
+  HDFSourceSingle keys (filepath group_key price_key feature_key timestamp_key
+              cache_size [start_time end_time])        Config.cpp:551-576,
+                                                       DataSource.cpp:227-262
 Errors follow the reference: missing keys -> RuntimeError (ConfigError),
 mismatched vector lengths -> ValueError (std::length_error), unknown source
 type -> RuntimeError (NotImplemented).
@@ -18,13 +21,14 @@ type -> RuntimeError (NotImplemented).
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Any, List, Tuple
+from typing import Any, List, Optional, Tuple
 
 from . import _lib as L
 
-SUPPORTED = ("Synth", "OU", "TrendOU", "Composite")
+SUPPORTED = ("Synth", "OU", "TrendOU", "Composite", "HDFSourceSingle")
 NOT_YET = ("SawTooth", "Triangle", "SineAdder", "SineDynamic", "SineDynamicTrend", "Gaussian",
-           "OUPair", "SimpleTrend", "TrendyOU", "HDFSourceSingle")
+           "OUPair", "SimpleTrend", "TrendyOU")
+HDF_KEYS = ("filepath", "group_key", "feature_key", "timestamp_key", "price_key", "cache_size")
 
 
 class ConfigError(RuntimeError):
@@ -36,12 +40,20 @@ class SourceSpec:
     kinds: List[int] = field(default_factory=list)
     params: List[List[float]] = field(default_factory=list)
     assets: List[str] = field(default_factory=list)
+    n_feats: int = 0                 # State.price width; 0 = n_assets (generators)
+    hdf: Optional[dict] = None       # HDFSourceSingle data_source_config (replay)
 
     @property
     def n_assets(self) -> int:
         return len(self.kinds)
 
+    @property
+    def replay(self) -> bool:
+        return bool(self.kinds) and self.kinds[0] == L.SRC_REPLAY
+
     def extend(self, other: "SourceSpec") -> None:
+        if other.replay or self.replay:
+            raise RuntimeError("HDFSourceSingle cannot be a Composite child (Config.cpp:107-126)")
         for k, p, a in zip(other.kinds, other.params, other.assets):
             self.kinds.append(k)
             self.params.append(p)
@@ -104,6 +116,30 @@ def trendou_spec(trendProb, minPeriod, maxPeriod, dYMin, dYMax, start, theta, ph
     return s
 
 
+def replay_spec(n_assets: int, n_feats: int = 0, assets=None, hdf: Optional[dict] = None) -> SourceSpec:
+    """Every asset from a replay tape (HDFSourceSingle, or a tape given directly)."""
+    codes = list(assets) if assets is not None else [f"asset_{i}" for i in range(n_assets)]
+    return SourceSpec(kinds=[L.SRC_REPLAY] * n_assets, params=[[] for _ in range(n_assets)],
+                      assets=codes, n_feats=int(n_feats) or n_assets, hdf=hdf)
+
+
+def hdf_spec(params: dict) -> SourceSpec:
+    """HDFSourceSingle(Config) (DataSource.cpp:227-262): required keys, then
+    init() on the file (checkKeys, assets, dims, time bounds)."""
+    missing = [k for k in HDF_KEYS if k not in params]
+    if missing:
+        raise ConfigError("Missing keys in call to HDFSourceSingle: \n" + ", ".join(missing) + ", \n")
+    from .hdf import HDFFile
+    start, end = 0, 0
+    if "start_time" in params and "end_time" in params:
+        start, end = int(params["start_time"]), int(params["end_time"])
+    f = HDFFile(params["filepath"], params["group_key"], params["price_key"],
+                params["feature_key"], params["timestamp_key"], start, end)
+    cfg = dict(params)
+    cfg["start_time"], cfg["end_time"] = int(f.info.start_time), int(f.info.end_time)
+    return replay_spec(f.n_assets, f.n_feats, f.asset_codes, hdf=cfg)
+
+
 def default_spec(source_type: str) -> SourceSpec:
     """Default constructors (Env(type, initCash) without config)."""
     if source_type == "Synth":
@@ -151,6 +187,8 @@ def spec_from_config(config: Any) -> SourceSpec:
     if source_type == "OU":
         _require(params, ("mean", "theta", "phi"))
         return ou_spec(params["mean"], params["theta"], params["phi"])
+    if source_type == "HDFSourceSingle":
+        return hdf_spec(params)
     if source_type == "TrendOU":
         _require(params, ("trend_prob", "min_period", "max_period", "dYMin", "dYMax", "start",
                           "theta", "phi", "noise_trend", "ema_alpha"))
@@ -226,6 +264,7 @@ def build_config(spec: SourceSpec, *, n_envs: int, init_cash: float = 1_000_000.
         raise ConfigError(f"nstep_return must be in [1, {L.MAX_NSTEP}], got {nstep_return}")
     c.nstep = int(nstep_return)  # config.py:126 (Agent/Model spec)
     c.discount = float(discount)  # config.py:154
+    c.n_feats = int(spec.n_feats) if spec.replay else 0
     srcs = (L.AssetSource * A)()
     for i, (k, p) in enumerate(zip(spec.kinds, spec.params)):
         srcs[i].kind = k

@@ -19,13 +19,11 @@ namespace {
 
 thread_local std::string g_error;
 
+// bump allocator over the arena: every buffer 256-B aligned
 struct Layout {
-  size_t off[40];
-  int n = 0;
   size_t total = 0;
   size_t add(size_t bytes) {
     const size_t o = total;
-    off[n++] = o;
     total += (bytes + 255) & ~size_t(255);
     return o;
   }
@@ -41,7 +39,10 @@ int next_pow2(int a) {
 
 struct mgn_env {
   mgn_config cfg;
-  int N, A, W, D, apad;
+  int N, A, W, D, F, apad;
+  bool replay = false;        // MGN_SRC_REPLAY handle
+  bool attached = false;      // replay tape attached (mgn_attach_replay)
+  mgn_replay_tape tape{};
   hipStream_t stream;
   void* arena;
   bool own_arena;
@@ -60,8 +61,8 @@ namespace {
 struct Offsets {
   size_t L, mep, Bm, P, sx, oum, dy, tlen, tfl, cash, ts, sA, sB, ep, epstats, ext, units, aidx,
       ring, ring_ts, rhead, rlen, wprice, wport, wts, mask, reward, areward, shaped, done, obsp,
-      obsport, obsts, tprice, tunits, tcost, risk, mcall, nshaped, nring, nlen, nhead, disc, src,
-      target;
+      obsport, obsts, tprice, tunits, tcost, risk, mcall, nshaped, dend, nring, nlen, nhead, disc,
+      src, target, rcur;
   size_t total;
 };
 
@@ -70,6 +71,7 @@ Offsets plan(const mgn_config* c) {
   const size_t W = (size_t)(c->window > 0 ? c->window : 0);
   const size_t D = (c->reward_mode == MGN_REWARD_AGENT_PER_ASSET) ? A : 1;
   const size_t n = (size_t)(c->nstep > 0 ? c->nstep : 1);
+  const size_t F = (size_t)(c->n_feats > 0 ? c->n_feats : c->n_assets);
   Layout l;
   Offsets o;
   o.L = l.add(N * A * 8);
@@ -90,11 +92,11 @@ Offsets plan(const mgn_config* c) {
   o.ext = l.add(N * A * 8);
   o.units = l.add(N * A * 8);
   o.aidx = l.add(N * 4);
-  o.ring = l.add(N * W * (2 * A + 1) * 8);
+  o.ring = l.add(N * W * (F + A + 1) * 8);
   o.ring_ts = l.add(N * W * 8);
   o.rhead = l.add(N * 4);
   o.rlen = l.add(N * 4);
-  o.wprice = l.add(N * W * A * 8);
+  o.wprice = l.add(N * W * F * 8);
   o.wport = l.add(N * W * (A + 1) * 8);
   o.wts = l.add(N * W * 8);
   o.mask = l.add(N);
@@ -102,7 +104,7 @@ Offsets plan(const mgn_config* c) {
   o.areward = l.add(N * D * 8);
   o.shaped = l.add(N * n * D * 8);
   o.done = l.add(N);
-  o.obsp = l.add(N * A * 8);
+  o.obsp = l.add(N * F * 8);
   o.obsport = l.add(N * (A + 1) * 8);
   o.obsts = l.add(N * 8);
   o.tprice = l.add(N * A * 8);
@@ -111,12 +113,14 @@ Offsets plan(const mgn_config* c) {
   o.risk = l.add(N * A);
   o.mcall = l.add(N);
   o.nshaped = l.add(N);
+  o.dend = l.add(N);
   o.nring = l.add(n > 1 ? N * n * D * 8 : 0);
   o.nlen = l.add(N * 4);
   o.nhead = l.add(N * 4);
   o.disc = l.add(n * 8);
   o.src = l.add(A * sizeof(mgn_asset_source));
   o.target = l.add((A + 1) * 8);
+  o.rcur = l.add(N * 8);
   o.total = l.total;
   return o;
 }
@@ -150,9 +154,20 @@ int validate(const mgn_config* c, const mgn_asset_source* s, std::string& msg) {
     msg = "nstep_return must be in [1, 64]";
     return MGN_ERR_CONFIG;
   }
+  int n_replay = 0;
+  for (int i = 0; i < c->n_assets; ++i) n_replay += s[i].kind == MGN_SRC_REPLAY;
+  if (n_replay != 0 && n_replay != c->n_assets) {
+    msg = "a replay source supplies every asset of the env (HDFSourceSingle is not a Composite child)";
+    return MGN_ERR_CONFIG;
+  }
+  if (c->n_feats < 0 || c->n_feats > MGN_MAX_ASSETS) { msg = "n_feats must be in [0, 64]"; return MGN_ERR_LENGTH; }
+  if (n_replay == 0 && c->n_feats != 0 && c->n_feats != c->n_assets) {
+    msg = "generator sources have n_feats == n_assets";
+    return MGN_ERR_LENGTH;
+  }
   for (int i = 0; i < c->n_assets; ++i) {
     const int k = s[i].kind;
-    if (k < MGN_SRC_EXTERNAL || k > MGN_SRC_TRENDOU) {
+    if (k < MGN_SRC_EXTERNAL || k > MGN_SRC_REPLAY) {
       msg = "unknown data source kind for asset " + std::to_string(i);
       return MGN_ERR_CONFIG;
     }
@@ -167,7 +182,10 @@ int validate(const mgn_config* c, const mgn_asset_source* s, std::string& msg) {
 mgn::KParams kparams(const mgn_env* e) {
   mgn::KParams p;
   const mgn_config& c = e->cfg;
-  p.N = e->N; p.A = e->A; p.W = e->W; p.D = e->D;
+  p.N = e->N; p.A = e->A; p.W = e->W; p.D = e->D; p.F = e->F;
+  p.replay = e->replay ? 1 : 0;
+  p.rp_price = e->tape.price; p.rp_feat = e->tape.feats; p.rp_ts = e->tape.ts;
+  p.rp_end = e->tape.data_end; p.rp_rows = e->tape.rows; p.rp_stride = e->tape.stride;
   p.env_offset = c.env_offset; p.seed = c.seed;
   p.init_cash = c.init_cash; p.reqM = c.required_margin; p.mainM = c.maintenance_margin;
   p.slip_rel = c.slippage_rel; p.slip_abs = c.slippage_abs; p.tc_rel = c.tc_rel; p.tc_abs = c.tc_abs;
@@ -185,6 +203,7 @@ mgn::KParams kparams(const mgn_env* e) {
   p.src = e->src_dev; p.target = e->target_dev;
   p.nstep = c.nstep; p.nring = v.nstep_ring; p.nlen = v.nstep_len; p.nhead = v.nstep_head;
   p.disc = e->disc_dev;
+  p.rcur = e->v.replay_cursor;
   return p;
 }
 
@@ -231,7 +250,7 @@ void launch_val(const mgn_env* e, double* out) {
 
 mgn::RingDesc ring_desc(const mgn_env* e) {
   mgn::RingDesc r;
-  r.N = e->N; r.F = e->A; r.Pn = e->A + 1; r.W = e->W; r.norm = e->cfg.norm_type;
+  r.N = e->N; r.F = e->F; r.Pn = e->A + 1; r.W = e->W; r.norm = e->cfg.norm_type;
   r.ring = e->v.ring; r.ring_ts = e->v.ring_ts; r.head = e->v.ring_head; r.len = e->v.ring_len;
   return r;
 }
@@ -261,6 +280,9 @@ int mgn_create(const mgn_config* cfg, const mgn_asset_source* sources, void* str
   e->A = cfg->n_assets;
   e->W = cfg->window > 0 ? cfg->window : 0;
   e->D = (cfg->reward_mode == MGN_REWARD_AGENT_PER_ASSET) ? e->A : 1;
+  e->F = cfg->n_feats > 0 ? cfg->n_feats : e->A;
+  e->cfg.n_feats = e->F;
+  e->replay = sources[0].kind == MGN_SRC_REPLAY;
   e->apad = next_pow2(e->A);
   e->m = choose_m(e->N, e->apad);
   e->stream = (hipStream_t)stream;
@@ -301,10 +323,12 @@ int mgn_create(const mgn_config* cfg, const mgn_asset_source* sources, void* str
   v.out.tunits = (double*)(b + o.tunits); v.out.tcost = (double*)(b + o.tcost);
   v.out.risk = (uint8_t*)(b + o.risk); v.out.margin_call = (uint8_t*)(b + o.mcall);
   v.out.n_shaped = (uint8_t*)(b + o.nshaped);
+  v.out.data_end = (uint8_t*)(b + o.dend);
+  v.replay_cursor = (int64_t*)(b + o.rcur);
   v.nstep_ring = cfg->nstep > 1 ? (double*)(b + o.nring) : nullptr;
   v.nstep_len = (int32_t*)(b + o.nlen); v.nstep_head = (int32_t*)(b + o.nhead);
   v.n_envs = e->N; v.n_assets = e->A; v.window = e->W; v.reward_dim = e->D;
-  v.nstep = cfg->nstep; v.pad_ = 0;
+  v.nstep = cfg->nstep; v.n_feats = e->F;
   e->src_dev = (mgn_asset_source*)(b + o.src);
   e->target_dev = (double*)(b + o.target);
   e->disc_dev = (double*)(b + o.disc);
@@ -322,7 +346,8 @@ int mgn_create(const mgn_config* cfg, const mgn_asset_source* sources, void* str
   if (rc == MGN_OK)
     rc = check_hip(e, hipMemcpyAsync(e->disc_dev, disc, 8 * cfg->nstep, hipMemcpyHostToDevice,
                                      e->stream), "hipMemcpyAsync(discounts)");
-  if (rc == MGN_OK) {
+  // the constructor's first getData; a replay handle runs it at mgn_attach_replay
+  if (rc == MGN_OK && !e->replay) {
     launch_init(e, 0, nullptr);
     rc = check_hip(e, hipGetLastError(), "k_init_reset");
   }
@@ -357,8 +382,28 @@ int mgn_get_views(const mgn_env* e, mgn_views* views) {
   return MGN_OK;
 }
 
+static int need_tape(mgn_env* e) {
+  if (e->replay && !e->attached)
+    return fail(e, MGN_ERR_CONFIG, "replay source: attach the replay tape (mgn_attach_replay) first");
+  return MGN_OK;
+}
+
+int mgn_attach_replay(mgn_env* e, const mgn_replay_tape* t) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  if (!e->replay) return fail(e, MGN_ERR_CONFIG, "handle was not created with MGN_SRC_REPLAY sources");
+  if (!t || !t->price || !t->feats || !t->ts || !t->data_end)
+    return fail(e, MGN_ERR_ARG, "null replay tape pointer");
+  if (t->rows < 1) return fail(e, MGN_ERR_LENGTH, "replay tape needs >= 1 row");
+  if (t->stride < 0) return fail(e, MGN_ERR_CONFIG, "replay stride must be >= 0");
+  e->tape = *t;
+  e->attached = true;
+  launch_init(e, 0, nullptr);
+  return check_hip(e, hipGetLastError(), "mgn_attach_replay");
+}
+
 int mgn_reset(mgn_env* e, const uint8_t* mask_dev) {
   if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  if (need_tape(e) != MGN_OK) return MGN_ERR_CONFIG;
   launch_init(e, 1, mask_dev);
   return check_hip(e, hipGetLastError(), "mgn_reset");
 }
@@ -372,6 +417,7 @@ int mgn_step(mgn_env* e, int32_t kind, const double* units_dev, const int32_t* a
   else return fail(e, MGN_ERR_CONFIG, "unknown step kind");
   if (in_kind != mgn::IN_NONE && !units_dev) return fail(e, MGN_ERR_ARG, "units pointer is null");
   if (in_kind == mgn::IN_SINGLE && !aidx_dev) return fail(e, MGN_ERR_ARG, "asset index pointer is null");
+  if (need_tape(e) != MGN_OK) return MGN_ERR_CONFIG;
   launch_step(e, e->v.out, in_kind, units_dev, aidx_dev, nullptr, 1);
   return check_hip(e, hipGetLastError(), "mgn_step");
 }
@@ -380,6 +426,7 @@ int mgn_rollout(mgn_env* e, const int8_t* actions_dev, int32_t k_steps, const mg
   if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
   if (!actions_dev || !out) return fail(e, MGN_ERR_ARG, "null actions/out");
   if (k_steps < 1) return fail(e, MGN_ERR_LENGTH, "k_steps must be >= 1");
+  if (need_tape(e) != MGN_OK) return MGN_ERR_CONFIG;
   launch_step(e, *out, mgn::IN_DISCRETE, nullptr, nullptr, actions_dev, (int)k_steps);
   return check_hip(e, hipGetLastError(), "mgn_rollout");
 }
@@ -388,6 +435,7 @@ int mgn_rollout_units(mgn_env* e, const double* units_dev, int32_t k_steps, cons
   if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
   if (!units_dev || !out) return fail(e, MGN_ERR_ARG, "null units/out");
   if (k_steps < 1) return fail(e, MGN_ERR_LENGTH, "k_steps must be >= 1");
+  if (need_tape(e) != MGN_OK) return MGN_ERR_CONFIG;
   launch_step(e, *out, mgn::IN_UNITS, units_dev, nullptr, nullptr, (int)k_steps);
   return check_hip(e, hipGetLastError(), "mgn_rollout_units");
 }
@@ -421,7 +469,7 @@ int mgn_window(mgn_env* e, double* price_dev, double* port_dev, uint64_t* ts_dev
   if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
   if (e->W == 0) return fail(e, MGN_ERR_CONFIG, "handle has no window (window_length = 0)");
   const mgn::RingDesc r = ring_desc(e);
-  const int64_t threads = (int64_t)e->N * (2 * e->A + 1);
+  const int64_t threads = (int64_t)e->N * (e->F + e->A + 1);
   hipLaunchKernelGGL(mgn::k_ring_gather, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
                      e->stream, r, price_dev ? price_dev : e->v.win_price,
                      port_dev ? port_dev : e->v.win_port, ts_dev ? ts_dev : e->v.win_ts);

@@ -27,6 +27,8 @@ constexpr int BLOCK = 256;
 
 struct KParams {
   int N, A, W, D;
+  int F;       // State.price width (features): A for the generators
+  int replay;  // every asset from the replay tape (MGN_SRC_REPLAY)
   int64_t env_offset;
   uint64_t seed;
   double init_cash, reqM, mainM, slip_rel, slip_abs, tc_rel, tc_abs;
@@ -54,6 +56,14 @@ struct KParams {
   double *nring;
   int32_t *nlen, *nhead;
   const double *disc;
+  // replay tape (mgn_attach_replay): (rows, A) prices, (rows, F) features,
+  // timestamps, dataEnd flags; per-env cursor = next tape row
+  const double *rp_price;
+  const double *rp_feat;
+  const uint64_t *rp_ts;
+  const uint8_t *rp_end;
+  int64_t rp_rows, rp_stride;
+  int64_t *rcur;
 };
 
 // ---------------------------------------------------------------------------
@@ -179,12 +189,26 @@ struct Lane {
   int kind[M];
   int asset[M];
   bool valid[M];
+  int64_t rcur;  // replay: next tape row (same in every lane of the segment)
+  int64_t row;   // replay: tape row of the current State
 };
 
 // DataSource::getData for the lane's slots (DataSource.cpp:535-543, 1173-1180,
 // 1457-1493; Composite concatenation :439-451) ; tick = timestamp before ++.
 template <int M>
 __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, uint64_t tick) {
+  if (p.replay) {
+    // HDFSourceSingle::getData (DataSource.cpp:391-398) on the tape: the
+    // row iterCache / loadData would serve, then advance (wrap = the
+    // reference's rewind to boundsIdx_.first, :368-371, :397-399)
+    const int64_t row = s.rcur;
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+      if (s.valid[m]) s.P[m] = p.rp_price[(size_t)row * p.A + s.asset[m]];
+    s.row = row;
+    s.rcur = (row + 1 == p.rp_rows) ? 0 : row + 1;
+    return;
+  }
   const uint64_t genv = (uint64_t)(p.env_offset + env);
 #pragma unroll
   for (int m = 0; m < M; ++m) {
@@ -240,7 +264,29 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
   }
 }
 
-// source reset (DataSource.h:466, :232; DataSource.cpp:1495-1502)
+// timestamp_ after a getData: the tape's timestamp for replay (HDFSourceSingle
+// :396), else timestamp_ += 1
+template <int M>
+__device__ __forceinline__ uint64_t next_ts(const Lane<M>& s, const KParams& p, uint64_t ts) {
+  return p.replay ? p.rp_ts[s.row] : ts + 1;
+}
+
+// State.price of the current tick for the lane's columns (features): the
+// replay tape's feature row, else the generator prices (F = A)
+template <int M, int S>
+__device__ __forceinline__ void put_feats(const Lane<M>& s, const KParams& p, int ls,
+                                          double* __restrict__ dst) {
+  if (p.replay) {
+    for (int f = ls; f < p.F; f += S) dst[f] = p.rp_feat[(size_t)s.row * p.F + f];
+  } else {
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+      if (s.valid[m]) dst[s.asset[m]] = s.P[m];
+  }
+}
+
+// source reset (DataSource.h:466, :232; DataSource.cpp:1495-1502; the replay
+// source carries on, DataSource.cpp:200-206)
 template <int M>
 __device__ __forceinline__ void src_reset(Lane<M>& s, const KParams& p) {
 #pragma unroll
@@ -263,16 +309,16 @@ __device__ __forceinline__ void ring_push(const Lane<M>& s, const KParams& p, in
   const double eq = (cash + q.lp) - q.b;
   head = (head + 1) % p.W;
   if (len < p.W) len += 1;
-  const int R = 2 * p.A + 1;
+  const int R = p.F + p.A + 1;
   double* row = p.ring + ((size_t)env * p.W + head) * R;
+  put_feats<M, S>(s, p, ls, row);
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     if (!s.valid[m]) continue;
-    row[s.asset[m]] = s.P[m];
-    row[p.A + 1 + s.asset[m]] = (s.L[m] * s.P[m]) / eq;
+    row[p.F + 1 + s.asset[m]] = (s.L[m] * s.P[m]) / eq;
   }
   if (ls == 0) {
-    row[p.A] = (cash - q.b) / eq;
+    row[p.F] = (cash - q.b) / eq;
     p.ring_ts[(size_t)env * p.W + head] = ts;
   }
 }
@@ -290,14 +336,14 @@ __device__ __forceinline__ void env_reset(Lane<M>& s, const KParams& p, int env,
   }
   cash = p.init_cash;
   gen_tick<M>(s, p, env, ts);
-  ts += 1;
+  ts = next_ts<M>(s, p, ts);
   if (p.W > 0) {
     len = 0;
     head = p.W - 1;
     ring_push<M, S>(s, p, env, ls, cash, ts, head, len);
     while (len < p.W) {
       gen_tick<M>(s, p, env, ts);
-      ts += 1;
+      ts = next_ts<M>(s, p, ts);
       ring_push<M, S>(s, p, env, ls, cash, ts, head, len);
     }
   }
@@ -329,6 +375,8 @@ __device__ __forceinline__ void load_lane(Lane<M>& s, const KParams& p, int env,
       s.kind[m] = -1;
     }
   }
+  s.rcur = p.replay ? p.rcur[env] : 0;
+  s.row = 0;
 }
 
 template <int M>
@@ -954,7 +1002,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
     if (ticking) {
       // ---- dataSource->getData()
       if (!(p.ablate & 2)) gen_tick<M>(s, p, env, ts);
-      ts += 1;
+      ts = next_ts<M>(s, p, ts);
     }
     if (stepping) {
       // ---- reward / done (Env.h:211-223).  Only the L*P sum sees the new
@@ -1055,7 +1103,6 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
       for (int m = 0; m < M; ++m) {
         if (!s.valid[m] || (p.ablate & 4)) continue;
         const size_t i = oNA + (size_t)env * A + s.asset[m];
-        if (out.obs_price) out.obs_price[i] = s.P[m];
         if (out.tprice) out.tprice[i] = tp[m];
         if (out.tunits) out.tunits[i] = tu[m];
         if (out.tcost) out.tcost[i] = tc[m];
@@ -1066,7 +1113,10 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
           if (out.shaped && !nst) out.shaped[i] = shaped_v[m];
         }
       }
+      if (out.obs_price && !(p.ablate & 4))
+        put_feats<M, S>(s, p, ls, out.obs_price + (oN + env) * (size_t)p.F);
       if (ls == 0 && !(p.ablate & 4)) {
+        if (out.data_end) out.data_end[oN + env] = p.replay ? p.rp_end[s.row] : 0;
         if (out.reward) out.reward[oN + env] = reward;
         if (out.done) out.done[oN + env] = done ? 1 : 0;
         if (out.timestamp) out.timestamp[oN + env] = ts;
@@ -1127,6 +1177,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
   if (ls == 0) {
     p.cash[env] = cash;
     p.ts[env] = ts;
+    if (p.replay) p.rcur[env] = s.rcur;
     p.ep[(size_t)env * 2] = ep_ret;
     p.ep[(size_t)env * 2 + 1] = ep_len;
     if (p.W > 0) {
@@ -1188,8 +1239,13 @@ __global__ __launch_bounds__(BLOCK) void k_init_reset(KParams p, int mode,
     }
     ts = 0;
     cash = p.init_cash;
+    // replay: env g starts at tape row (g * stride) mod rows
+    s.rcur = p.replay ? (int64_t)(((uint64_t)(p.env_offset + env) * (uint64_t)p.rp_stride) %
+                                  (uint64_t)p.rp_rows)
+                      : 0;
+    s.row = 0;
     gen_tick<M>(s, p, env, ts);  // initAccountants' getData (Env.h:160)
-    ts += 1;
+    ts = next_ts<M>(s, p, ts);
     if (ls == 0) {
       p.ep[(size_t)env * 2] = 0.;
       p.ep[(size_t)env * 2 + 1] = 0.;
@@ -1217,6 +1273,7 @@ __global__ __launch_bounds__(BLOCK) void k_init_reset(KParams p, int mode,
   if (ls == 0) {
     p.cash[env] = cash;
     p.ts[env] = ts;
+    if (p.replay) p.rcur[env] = s.rcur;
   }
 }
 

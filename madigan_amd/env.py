@@ -31,7 +31,7 @@ VALUATION_FIELDS = ("cash", "equity", "pnl", "balance", "availableMargin", "used
 
 StepOutput = namedtuple("StepOutput", ["reward", "done", "obs_price", "obs_port", "timestamp",
                                        "tprice", "tunits", "tcost", "risk", "margin_call",
-                                       "shaped", "agent_reward", "n_shaped"])
+                                       "shaped", "agent_reward", "n_shaped", "data_end"])
 
 
 def _torch():
@@ -126,7 +126,14 @@ class BatchedEnv:
                  adaptation_rate: float = 0.001, cosine_temp: float = 0.0,
                  desired_portfolio=None, window: int = 0, norm_type=None,
                  auto_reset: bool = False, action_atoms: int = 3, unit_size: float = 0.05,
-                 nstep_return: int = 1, discount: float = 0.99):
+                 nstep_return: int = 1, discount: float = 0.99, replay_tape: Optional[dict] = None,
+                 replay_stride: int = 0):
+        """A replay spec (``config.replay_spec`` / HDFSourceSingle) reads its
+        prices, features and timestamps from a device replay tape: staged from
+        the spec's HDF file (``spec.hdf``, cache_size chunks, pinned
+        double-buffered H2D) or given as ``replay_tape`` = {price (P,A),
+        feats (P,F), ts (P,), data_end (P,)} device tensors.  Env g starts at
+        tape row (g * replay_stride) mod P."""
         torch = _torch()
         self.lib = L.load()
         if not torch.cuda.is_available():
@@ -146,6 +153,7 @@ class BatchedEnv:
             env_offset=env_offset, nstep_return=nstep_return, discount=discount)
         self.N = int(n_envs)
         self.A = spec.n_assets
+        self.F = int(spec.n_feats) if spec.replay else self.A
         self.W = int(window)
         nbytes = self.lib.mgn_arena_bytes(C.byref(self.cfg))
         if nbytes == 0:
@@ -164,6 +172,41 @@ class BatchedEnv:
         self.nstep = v.nstep
         self._build_views()
         self._val = torch.empty((self.N, 10), dtype=torch.float64, device=self.device)
+        self._tape = None
+        if spec.replay:
+            self._attach_replay(replay_tape, int(replay_stride))
+        elif replay_tape is not None:
+            raise RuntimeError("replay_tape given for a generator source spec")
+
+    def _attach_replay(self, tape: Optional[dict], stride: int):
+        torch = _torch()
+        if tape is None:
+            if not self.spec.hdf:
+                raise RuntimeError("replay source needs an HDF config or a replay_tape")
+            from .hdf import HDFFile
+            h = self.spec.hdf
+            f = HDFFile(h["filepath"], h["group_key"], h["price_key"], h["feature_key"],
+                        h["timestamp_key"], int(h.get("start_time", 0)), int(h.get("end_time", 0)))
+            with torch.cuda.device(self.device):
+                tape = f.stage_tape(int(h["cache_size"]), self.device, self.stream)
+            stride = int(h.get("replay_stride", stride))
+        want = dict(price=(torch.float64, 2, self.A), feats=(torch.float64, 2, self.F),
+                    ts=(torch.int64, 1, None), data_end=(torch.uint8, 1, None))
+        rows = None
+        for k, (dt, nd, cols) in want.items():
+            t = tape.get(k)
+            if t is None or t.dtype != dt or t.dim() != nd or t.device != self.device \
+                    or not t.is_contiguous() or (cols is not None and t.shape[1] != cols):
+                raise ValueError(f"replay_tape[{k!r}] must be a contiguous {dt} tensor of "
+                                 f"{nd} dims on {self.device}" + (f" with {cols} columns" if cols else ""))
+            if rows is not None and t.shape[0] != rows:
+                raise ValueError("replay_tape arrays differ in rows")
+            rows = t.shape[0]
+        self._tape = tape
+        rt = L.ReplayTape(price=tape["price"].data_ptr(), feats=tape["feats"].data_ptr(),
+                          ts=tape["ts"].data_ptr(), data_end=tape["data_end"].data_ptr(),
+                          rows=int(rows), stride=int(stride))
+        L.check(self.lib.mgn_attach_replay(self.h, C.byref(rt)), self.h)
 
     # ---- tensor views over the arena --------------------------------------
     def _t(self, ptr, dtype, shape):
@@ -178,7 +221,7 @@ class BatchedEnv:
     def _build_views(self):
         torch = _torch()
         f64, i32, u8, i64 = torch.float64, torch.int32, torch.uint8, torch.int64
-        N, A, W, D, v = self.N, self.A, self.W, self.D, self._v
+        N, A, W, D, F, v = self.N, self.A, self.W, self.D, self.F, self._v
         NA = (N, A)
         Dsh = (N,) if D == 1 else (N, A)
         self.ledger = self._t(v.ledger, f64, NA)
@@ -201,23 +244,25 @@ class BatchedEnv:
         self.asset_idx_buf = self._t(v.asset_idx, i32, (N,))
         self.reset_mask_buf = self._t(v.reset_mask, u8, (N,))
         if W:
-            self.ring = self._t(v.ring, f64, (N, W, 2 * A + 1))
-            self.win_price = self._t(v.win_price, f64, (N, W, A))
+            self.ring = self._t(v.ring, f64, (N, W, F + A + 1))
+            self.win_price = self._t(v.win_price, f64, (N, W, F))
             self.win_port = self._t(v.win_port, f64, (N, W, A + 1))
             self.win_ts = self._t(v.win_ts, i64, (N, W))
             self.ring_len = self._t(v.ring_len, i32, (N,))
         o = v.out
         self.out = StepOutput(
             reward=self._t(o.reward, f64, (N,)), done=self._t(o.done, u8, (N,)),
-            obs_price=self._t(o.obs_price, f64, NA), obs_port=self._t(o.obs_port, f64, (N, A + 1)),
+            obs_price=self._t(o.obs_price, f64, (N, F)), obs_port=self._t(o.obs_port, f64, (N, A + 1)),
             timestamp=self._t(o.timestamp, i64, (N,)), tprice=self._t(o.tprice, f64, NA),
             tunits=self._t(o.tunits, f64, NA), tcost=self._t(o.tcost, f64, NA),
             risk=self._t(o.risk, u8, NA), margin_call=self._t(o.margin_call, u8, (N,)),
             shaped=self._t(o.shaped, f64, self._shaped_shape()),
-            agent_reward=self._t(o.agent_reward, f64, Dsh), n_shaped=self._t(o.n_shaped, u8, (N,)))
+            agent_reward=self._t(o.agent_reward, f64, Dsh), n_shaped=self._t(o.n_shaped, u8, (N,)),
+            data_end=self._t(o.data_end, u8, (N,)))
+        self.replay_cursor = self._t(v.replay_cursor, i64, (N,))
         # the whole step-output block is contiguous in the arena: one D2H copy
         lo = o.reward - self.arena.data_ptr()
-        hi = o.n_shaped - self.arena.data_ptr() + N
+        hi = o.data_end - self.arena.data_ptr() + N
         self._out_span = (lo, hi)
 
     def __del__(self):
@@ -291,16 +336,16 @@ class BatchedEnv:
 
     def _traj_shapes(self, K: int) -> dict:
         torch = _torch()
-        N, A, D, n = self.N, self.A, self.D, self.nstep
+        N, A, D, n, F = self.N, self.A, self.D, self.nstep, self.F
         col = (N,) if D == 1 else (N, A)
         sh = col if n == 1 else ((N, n) if D == 1 else (N, n, A))
         return dict(reward=((K, N), torch.float64), agent_reward=((K,) + col, torch.float64),
                     shaped=((K,) + sh, torch.float64), done=((K, N), torch.uint8),
-                    obs_price=((K, N, A), torch.float64), obs_port=((K, N, A + 1), torch.float64),
+                    obs_price=((K, N, F), torch.float64), obs_port=((K, N, A + 1), torch.float64),
                     timestamp=((K, N), torch.int64), tprice=((K, N, A), torch.float64),
                     tunits=((K, N, A), torch.float64), tcost=((K, N, A), torch.float64),
                     risk=((K, N, A), torch.uint8), margin_call=((K, N), torch.uint8),
-                    n_shaped=((K, N), torch.uint8))
+                    n_shaped=((K, N), torch.uint8), data_end=((K, N), torch.uint8))
 
     def alloc_traj(self, k_steps: int, fields=None):
         """(K, ...) device buffers for rollout outputs (None fields are skipped).
@@ -407,7 +452,7 @@ class BatchedEnv:
         lo, hi = self._out_span
         blob = self.arena[lo:hi].cpu().numpy()
         base = self.arena.data_ptr() + lo
-        N, A, D = self.N, self.A, self.D
+        N, A, D, F = self.N, self.A, self.D, self.F
         o = self._v.out
         def arr(ptr, dtype, shape):  # noqa: E306
             off = ptr - base
@@ -417,11 +462,12 @@ class BatchedEnv:
         return dict(reward=arr(o.reward, np.float64, (N,)), agent_reward=arr(o.agent_reward, np.float64, Dsh),
                     shaped=arr(o.shaped, np.float64, self._shaped_shape()),
                     n_shaped=arr(o.n_shaped, np.uint8, (N,)), done=arr(o.done, np.uint8, (N,)),
-                    obs_price=arr(o.obs_price, np.float64, (N, A)),
+                    obs_price=arr(o.obs_price, np.float64, (N, F)),
                     obs_port=arr(o.obs_port, np.float64, (N, A + 1)),
                     timestamp=arr(o.timestamp, np.uint64, (N,)), tprice=arr(o.tprice, np.float64, (N, A)),
                     tunits=arr(o.tunits, np.float64, (N, A)), tcost=arr(o.tcost, np.float64, (N, A)),
-                    risk=arr(o.risk, np.uint8, (N, A)), margin_call=arr(o.margin_call, np.uint8, (N,)))
+                    risk=arr(o.risk, np.uint8, (N, A)), margin_call=arr(o.margin_call, np.uint8, (N,)),
+                    data_end=arr(o.data_end, np.uint8, (N,)))
 
 
 # ---------------------------------------------------------------------------
@@ -474,15 +520,16 @@ class _DeviceSourceView:
         self._env = env
 
     def currentData(self):
-        return self._env.currentPrices.copy()
+        return self._env.currentData.copy()
 
-    currentPrices = currentData
+    def currentPrices(self):
+        return self._env.currentPrices.copy()
 
     def currentTime(self):
         return self._env.timestamp
 
     def dataEnd(self):
-        return False
+        return self._env.dataEnd()
 
     @property
     def nAssets(self):
@@ -583,7 +630,7 @@ class Env:
             self._source.reset()
             self._feed_external()
         self._b.reset()
-        return State(self.currentPrices.copy(), self.ledgerNormedFull, self.timestamp)
+        return State(self.currentData.copy(), self.ledgerNormedFull, self.timestamp)
 
     def step(self, *args):
         if len(args) == 0:
@@ -630,6 +677,18 @@ class Env:
     @property
     def currentPrices(self):
         return self._b.prices[0].cpu().numpy()
+
+    def _replay_row(self):
+        b = self._b
+        rows = b._tape["ts"].shape[0]
+        return (int(b.replay_cursor[0].item()) - 1) % rows
+
+    @property
+    def currentData(self):
+        """Env::currentData (Env.h:52): the source's features (= prices for the generators)."""
+        if self._spec.replay:
+            return self._b._tape["feats"][self._replay_row()].cpu().numpy()
+        return self.currentPrices
 
     @property
     def ledger(self):
@@ -733,7 +792,7 @@ class Env:
 
     @property
     def nFeats(self):
-        return self._spec.n_assets
+        return self._b.F
 
     @property
     def assets(self):
@@ -741,7 +800,7 @@ class Env:
 
     @property
     def isDateTime(self):
-        return False
+        return self._spec.replay  # HDFSourceSingle::isDateTime (DataSource.h:124)
 
     @property
     def dataSource(self):
@@ -760,7 +819,12 @@ class Env:
         return PortfolioView(self)
 
     def dataEnd(self):
-        return bool(self._source.dataEnd()) if self._source is not None else False
+        """Env::dataEnd (Env.h:58) -> DataSource::dataEnd (DataSource.h:61, :126)."""
+        if self._source is not None:
+            return bool(self._source.dataEnd())
+        if self._spec.replay:
+            return bool(self._b._tape["data_end"][self._replay_row()].item())
+        return False
 
     def checkRisk(self):
         return RiskInfo(int(self._vals()["checkRisk"]))
@@ -782,10 +846,7 @@ def _cfg_get(config: Any, key: str, default=None):
 
 def make_env(config, test: bool = False, **kw) -> Env:
     """make_env (madigan/environments/__init__.py:9-22)."""
-    import copy
-    config = copy.deepcopy(dict(config))
-    if test and "data_source_config_test" in config:
-        config["data_source_config"] = config["data_source_config_test"]
+    config = adjust_config(config, test)
     if config.get("env_type", "Synth") in ("Synth",):
         if config.get("data_source_config") is not None:
             env = Env(config["data_source_type"], config["init_cash"], config, **kw)
@@ -797,6 +858,23 @@ def make_env(config, test: bool = False, **kw) -> Env:
         env.setSlippage(config["slippage_rel"], config["slippage_abs"])
         return env
     raise NotImplementedError(f"Env type {config.get('env_type')} not implemented")
+
+
+def adjust_config(config, test: bool = False) -> dict:
+    """adjust_config (madigan/environments/__init__.py:25-37): the test data
+    config, and HDFSourceSingle start/end times as pd.to_datetime(x).value."""
+    import copy
+    config = copy.deepcopy(dict(config))
+    if test and "data_source_config_test" in config:
+        config["data_source_config"] = config["data_source_config_test"]
+    if config.get("data_source_type") == "HDFSourceSingle" and config.get("data_source_config"):
+        import pandas as pd
+        dsc = dict(config["data_source_config"])
+        for key in ("start_time", "end_time"):
+            if key in dsc:
+                dsc[key] = int(pd.to_datetime(dsc[key]).value)
+        config["data_source_config"] = dsc
+    return config
 
 
 def make_batched_env(config, n_envs: int, **kw) -> BatchedEnv:

@@ -239,6 +239,10 @@ typedef struct {
   uint8_t trending[MAXA];
   int8_t dir[MAXA];
   uint64_t ts;
+  /* HDFSourceSingle (DataSource.h:136-148): currentData_, currentIdx_,
+   * currentCacheIdx_, currentCacheSize_, first file row of the cache */
+  double feat[MAXA];
+  int64_t h_idx, h_cidx, h_ccs, h_cstart;
   /* shaper state (nstep_buffer.py:38-60): index 0 for scalar */
   double sA[MAXA], sB[MAXA];
   /* episode statistics */
@@ -251,7 +255,13 @@ struct orc_batch {
   int N, A;
   orc_env *envs;
   double *ext;  /* (N,A) external prices */
-  orc_ring ring; /* StackerDiscrete deques (preprocessor.py:150-152), F = A, P = A+1 */
+  orc_ring ring; /* StackerDiscrete deques (preprocessor.py:150-152), F, P = A+1 */
+  int F;         /* State.price width: A, or the replay source's feature count */
+  int replay;
+  /* replay file arrays and bounds (HDFSourceSingle) */
+  double *rp_price, *rp_feat;
+  uint64_t *rp_ts;
+  int64_t rp_T, rp_first, rp_second, rp_cs;
   /* NStepBuffer per env (nstep_buffer.py:315-356), oldest first: (N, n, D) values
    * (raw reward; PPC: reward + temp*cos), fill count (N), discounts gamma^i */
   double *nring;
@@ -391,8 +401,49 @@ static void b_handle_transaction(const orc_config *c, orc_env *s, int A, int i, 
 
 /* ---- DataSource::getData ------------------------------------------------ */
 
+/* HDFSourceSingle::loadData (DataSource.cpp:368-379) */
+static void h_load(const orc_batch *b, orc_env *s) {
+  if (s->h_idx >= b->rp_second - 1) s->h_idx = b->rp_first;
+  int64_t rest = b->rp_second - s->h_idx;
+  s->h_ccs = b->rp_cs < rest ? b->rp_cs : rest;
+  s->h_cstart = s->h_idx;
+}
+
+/* HDFSourceSingle::getData with iterCache (DataSource.cpp:381-408) */
+static void h_get_data(const orc_batch *b, orc_env *s) {
+  const int64_t full = b->rp_second - b->rp_first;
+  if (s->h_cidx == s->h_ccs || s->h_idx == b->rp_second) {
+    if (s->h_ccs >= full) {
+      s->h_idx = b->rp_first;
+      s->h_cidx = 0;
+    } else {
+      h_load(b, s);
+      s->h_cidx = 0;
+    }
+  }
+  const int64_t row = s->h_cstart + s->h_cidx;
+  for (int i = 0; i < b->A; ++i) s->P[i] = b->rp_price[row * b->A + i];
+  for (int f = 0; f < b->F; ++f) s->feat[f] = b->rp_feat[row * b->F + f];
+  s->ts = b->rp_ts[row];
+  s->h_idx++;
+  s->h_cidx++;
+}
+
+static int h_data_end(const orc_batch *b, const orc_env *s) { /* DataSource.h:126 */
+  return b->replay && s->h_idx == b->rp_second;
+}
+
+/* State.price of the current tick: currentData (features) */
+static const double *state_price(const orc_batch *b, const orc_env *s) {
+  return b->replay ? s->feat : s->P;
+}
+
 static void src_get_data(orc_batch *b, int e) {
   orc_env *s = &b->envs[e];
+  if (b->replay) {
+    h_get_data(b, s);
+    return;
+  }
   uint64_t genv = (uint64_t)(b->cfg.env_offset + e);
   uint64_t seed = b->cfg.seed;
   uint64_t tick = s->ts;
@@ -522,7 +573,7 @@ static void window_stream(orc_batch *b, int e) {
   orc_env *s = &b->envs[e];
   double port[MAXA + 1];
   p_ledger_normed_full(s, b->A, port);
-  ring_push_one(&b->ring, e, s->P, port, s->ts);
+  ring_push_one(&b->ring, e, state_price(b, s), port, s->ts);
 }
 
 static void window_clear(orc_batch *b, int e) {
@@ -623,6 +674,8 @@ orc_batch *orc_create(const orc_config *cfg, const orc_asset_src *srcs) {
   b->A = cfg->n_assets;
   memcpy(b->src, srcs, sizeof(orc_asset_src) * (size_t)b->A);
   b->envs = (orc_env *)calloc((size_t)b->N, sizeof(orc_env));
+  b->replay = srcs[0].kind == ORC_SRC_REPLAY;
+  b->F = (b->replay && cfg->n_feats > 0) ? cfg->n_feats : b->A;
   b->ext = (double *)calloc((size_t)b->N * b->A, sizeof(double));
   {
     int D = (cfg->reward_mode == ORC_REWARD_AGENT_PER_ASSET) ? b->A : 1;
@@ -633,9 +686,9 @@ orc_batch *orc_create(const orc_config *cfg, const orc_asset_src *srcs) {
   int W = cfg->window;
   if (W > 0) {
     orc_ring *r = &b->ring;
-    r->n_envs = b->N; r->n_price = b->A; r->n_port = b->A + 1; r->window = W;
+    r->n_envs = b->N; r->n_price = b->F; r->n_port = b->A + 1; r->window = W;
     r->norm_type = cfg->norm_type;
-    r->ring = (double *)calloc((size_t)b->N * W * (2 * b->A + 1), sizeof(double));
+    r->ring = (double *)calloc((size_t)b->N * W * (b->F + b->A + 1), sizeof(double));
     r->ring_ts = (uint64_t *)calloc((size_t)b->N * W, sizeof(uint64_t));
     r->head = (int32_t *)calloc((size_t)b->N, sizeof(int32_t));
     r->len = (int32_t *)calloc((size_t)b->N, sizeof(int32_t));
@@ -643,9 +696,50 @@ orc_batch *orc_create(const orc_config *cfg, const orc_asset_src *srcs) {
   for (int e = 0; e < b->N; ++e) {
     window_clear(b, e);
     src_init(b, e);               /* Env::initMembers -> makeDataSource (Env.h:139-148) */
-    env_init_accountants(b, e);   /* -> initAccountants (one getData) */
+    if (!b->replay) env_init_accountants(b, e);   /* -> initAccountants (one getData) */
   }
   return b;
+}
+
+int64_t orc_set_replay(orc_batch *b, const double *price, const double *feats, const uint64_t *ts,
+                       int64_t T, int64_t first, int64_t second, int64_t cache_size,
+                       int64_t stride) {
+  if (!b->replay || T < 1 || first < 0 || second > T || second - first < 1) return -1;
+  free(b->rp_price); free(b->rp_feat); free(b->rp_ts);
+  b->rp_price = (double *)malloc(sizeof(double) * (size_t)T * b->A);
+  b->rp_feat = (double *)malloc(sizeof(double) * (size_t)T * b->F);
+  b->rp_ts = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)T);
+  memcpy(b->rp_price, price, sizeof(double) * (size_t)T * b->A);
+  memcpy(b->rp_feat, feats, sizeof(double) * (size_t)T * b->F);
+  memcpy(b->rp_ts, ts, sizeof(uint64_t) * (size_t)T);
+  b->rp_T = T; b->rp_first = first; b->rp_second = second;
+  int64_t full = second - first;
+  b->rp_cs = cache_size < full ? (cache_size < 1 ? 1 : cache_size) : full; /* :299 */
+  /* the period: getData calls until the source is back in its init() state */
+  orc_env probe;
+  memset(&probe, 0, sizeof probe);
+  probe.h_idx = first; probe.h_cidx = 0;
+  h_load(b, &probe);
+  int64_t period = 0, prev = -1;
+  for (;;) {
+    orc_env t = probe;
+    h_get_data(b, &t);
+    int64_t row = t.h_cstart + t.h_cidx - 1;
+    if (row <= prev) break;
+    prev = row;
+    probe = t;
+    period++;
+  }
+  for (int e = 0; e < b->N; ++e) {
+    orc_env *s = &b->envs[e];
+    s->h_idx = first; s->h_cidx = 0;      /* HDFSourceSingle::init -> loadData */
+    h_load(b, s);
+    uint64_t g = (uint64_t)(b->cfg.env_offset + e);
+    int64_t skip = (int64_t)((g * (uint64_t)stride) % (uint64_t)period);
+    for (int64_t j = 0; j < skip; ++j) h_get_data(b, s);
+    env_init_accountants(b, e);
+  }
+  return period;
 }
 
 void orc_destroy(orc_batch *b) {
@@ -653,6 +747,7 @@ void orc_destroy(orc_batch *b) {
   free(b->ring.ring); free(b->ring.ring_ts); free(b->ring.head); free(b->ring.len);
   free(b->envs);
   free(b->ext);
+  free(b->rp_price); free(b->rp_feat); free(b->rp_ts);
   free(b->nring);
   free(b->nlen);
   free(b);
@@ -800,7 +895,11 @@ static void step_one(orc_batch *b, int e, int kind, const double *units, int32_t
   }
   if (o->n_shaped) o->n_shaped[e] = (uint8_t)n_shaped;
   if (o->done) o->done[e] = (uint8_t)done;
-  if (o->obs_price) for (int i = 0; i < A; ++i) o->obs_price[eA + i] = s->P[i];
+  if (o->obs_price) {
+    const double *sp = state_price(b, s);
+    for (int f = 0; f < b->F; ++f) o->obs_price[(size_t)e * b->F + f] = sp[f];
+  }
+  if (o->data_end) o->data_end[e] = (uint8_t)h_data_end(b, s);
   if (o->obs_port) for (int i = 0; i <= A; ++i) o->obs_port[(size_t)e * (A + 1) + i] = port[i];
   if (o->timestamp) o->timestamp[e] = s->ts;
   for (int i = 0; i < A; ++i) {
@@ -862,7 +961,8 @@ static orc_out out_at_step(const orc_batch *b, const orc_out *out, int k) {
   o.agent_reward = offs_d(out->agent_reward, nN * D);
   o.shaped = offs_d(out->shaped, nN * D * (size_t)b->cfg.nstep);
   o.done = offs_u8(out->done, nN);
-  o.obs_price = offs_d(out->obs_price, nA);
+  o.obs_price = offs_d(out->obs_price, (size_t)k * N * b->F);
+  o.data_end = offs_u8(out->data_end, nN);
   o.obs_port = offs_d(out->obs_port, (size_t)k * N * (A + 1));
   o.timestamp = out->timestamp ? out->timestamp + nN : NULL;
   o.tprice = offs_d(out->tprice, nA);

@@ -35,7 +35,8 @@ extern "C" {
 enum { ORC_GREEN = 0, ORC_INSUFF_MARGIN = 1, ORC_MARGIN_CALL = 2, ORC_BLOWN_OUT = 3 };
 
 /* per-asset generator kinds */
-enum { ORC_SRC_EXTERNAL = 0, ORC_SRC_SINE = 1, ORC_SRC_OU = 2, ORC_SRC_TRENDOU = 3 };
+enum { ORC_SRC_EXTERNAL = 0, ORC_SRC_SINE = 1, ORC_SRC_OU = 2, ORC_SRC_TRENDOU = 3,
+       ORC_SRC_REPLAY = 4 /* HDFSourceSingle over in-memory arrays (all assets) */ };
 
 /* reward shapers (nstep_buffer.py:378-408) */
 enum { ORC_SHAPER_NONE = 0, ORC_SHAPER_DSR = 1, ORC_SHAPER_DDR = 2, ORC_SHAPER_PPC = 3 };
@@ -86,6 +87,8 @@ typedef struct {
   int32_t nstep;               /* n-step return length (nstep_return), <= ORC_MAX_NSTEP */
   int32_t pad2_;
   double discount;             /* gamma of the n-step aggregation */
+  int32_t n_feats;             /* State.price width (replay features); 0 = n_assets */
+  int32_t pad3_;
 } orc_config;
 
 /* Outputs of one step for all envs.  Any pointer may be NULL. */
@@ -95,7 +98,7 @@ typedef struct {
   double *shaped;        /* (N[,n],D) shaper outputs emitted this step, in pop order
                             (n-step: (N,n,D); n == 1: (N,D)) */
   uint8_t *done;         /* (N) */
-  double *obs_price;     /* (N,A)   State.price */
+  double *obs_price;     /* (N,F)   State.price (F = A for the generators) */
   double *obs_port;      /* (N,A+1) State.portfolio = ledgerNormedFull */
   uint64_t *timestamp;   /* (N) */
   double *tprice;        /* (N,A) BrokerResponse.transactionPrice */
@@ -104,6 +107,7 @@ typedef struct {
   uint8_t *risk;         /* (N,A) */
   uint8_t *margin_call;  /* (N) */
   uint8_t *n_shaped;     /* (N) shaped rewards emitted this step (n-step) */
+  uint8_t *data_end;     /* (N) EnvInfo.dataEnd */
 } orc_out;
 
 /* StackerDiscrete deques of N envs: ring (N,W,F+P), ring_ts (N,W), head/len (N) */
@@ -136,6 +140,14 @@ void orc_rollout_mt(orc_batch *b, const int8_t *actions, int k_steps, const orc_
 void orc_action_to_units(orc_batch *b, const int8_t *actions, double *units);
 /* external prices for the next getData (N,A), ORC_SRC_EXTERNAL assets */
 void orc_set_prices(orc_batch *b, const double *prices);
+/* HDFSourceSingle for every env of an ORC_SRC_REPLAY batch, over the file's
+ * arrays held in memory: price (T,A), feats (T,F), ts (T), time bounds
+ * [first, second) as findBounds left them, cacheSize.  Env g's source is first
+ * advanced (g * stride) mod period getData calls, then the Env constructor's
+ * getData runs (Env.h:150-165).  Returns the period (rows per cycle). */
+int64_t orc_set_replay(orc_batch *b, const double *price, const double *feats, const uint64_t *ts,
+                       int64_t T, int64_t first, int64_t second, int64_t cache_size,
+                       int64_t stride);
 
 /* state access: field ids */
 enum { ORC_F_LEDGER = 0, ORC_F_MEP = 1, ORC_F_BORROWED = 2, ORC_F_PRICE = 3,

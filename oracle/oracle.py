@@ -20,7 +20,7 @@ BUILD = os.path.join(HERE, "_build")
 MAXA = 64
 
 GREEN, INSUFF_MARGIN, MARGIN_CALL, BLOWN_OUT = 0, 1, 2, 3
-SRC_EXTERNAL, SRC_SINE, SRC_OU, SRC_TRENDOU = 0, 1, 2, 3
+SRC_EXTERNAL, SRC_SINE, SRC_OU, SRC_TRENDOU, SRC_REPLAY = 0, 1, 2, 3, 4
 SHAPERS = {"none": 0, None: 0, "None": 0, "DSR": 1, "DDR": 2, "PPC": 3, "cosine": 3,
            "cosine_similarity": 3, "cosine_port_shaper": 3}
 REWARD_MODES = {"env_log": 0, "agent_sum": 1, "agent_per_asset": 2}
@@ -49,13 +49,14 @@ class Config(C.Structure):
         ("window", C.c_int32), ("norm_type", C.c_int32), ("auto_reset", C.c_int32),
         ("action_atoms", C.c_int32), ("unit_size", C.c_double),
         ("nstep", C.c_int32), ("pad2_", C.c_int32), ("discount", C.c_double),
+        ("n_feats", C.c_int32), ("pad3_", C.c_int32),
     ]
 
 
 class Out(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in (
         "reward", "agent_reward", "shaped", "done", "obs_price", "obs_port", "timestamp",
-        "tprice", "tunits", "tcost", "risk", "margin_call", "n_shaped")]
+        "tprice", "tunits", "tcost", "risk", "margin_call", "n_shaped", "data_end")]
 
 
 _LIB = {}
@@ -83,6 +84,8 @@ def lib(fast: bool = False):
         L.orc_rollout_mt.argtypes = [P, P, C.c_int, C.POINTER(Out), C.c_int]
         L.orc_action_to_units.argtypes = [P, P, P]
         L.orc_set_prices.argtypes = [P, P]
+        L.orc_set_replay.argtypes = [P, P, P, P] + [C.c_int64] * 5
+        L.orc_set_replay.restype = C.c_int64
         L.orc_get_field.argtypes = [P, C.c_int, P]
         L.orc_set_field.argtypes = [P, C.c_int, P]
         L.orc_get_scalar.argtypes = [P, C.c_int, P]
@@ -160,7 +163,9 @@ class OracleBatch:
         c.unit_size = float(cfg.get("unit_size", 0.05))
         c.nstep = int(cfg.get("nstep_return", 1))              # config.py:126
         c.discount = float(cfg.get("discount", 0.99))          # config.py:154
+        c.n_feats = int(cfg.get("n_feats", 0))
         self.cfg = c
+        self.F = c.n_feats if (sources and sources[0][0] == SRC_REPLAY and c.n_feats) else self.A
         self.W = c.window
         self.D = self.A if c.reward_mode == 2 else 1
         self._srcs = make_srcs(sources)
@@ -175,7 +180,7 @@ class OracleBatch:
 
     # -- outputs ---------------------------------------------------------
     def _alloc_out(self, K=None):
-        N, A, D = self.N, self.A, self.D
+        N, A, D, F = self.N, self.A, self.D, self.F
         n = self.cfg.nstep
         pre = () if K is None else (K,)
         sh = ((N,) if D == 1 else (N, A)) if n == 1 else ((N, n) if D == 1 else (N, n, A))
@@ -183,10 +188,11 @@ class OracleBatch:
             reward=np.zeros(pre + (N,)), agent_reward=np.zeros(pre + ((N,) if D == 1 else (N, A))),
             shaped=np.zeros(pre + sh), n_shaped=np.zeros(pre + (N,), np.uint8),
             done=np.zeros(pre + (N,), np.uint8),
-            obs_price=np.zeros(pre + (N, A)), obs_port=np.zeros(pre + (N, A + 1)),
+            obs_price=np.zeros(pre + (N, F)), obs_port=np.zeros(pre + (N, A + 1)),
             timestamp=np.zeros(pre + (N,), np.uint64), tprice=np.zeros(pre + (N, A)),
             tunits=np.zeros(pre + (N, A)), tcost=np.zeros(pre + (N, A)),
-            risk=np.zeros(pre + (N, A), np.uint8), margin_call=np.zeros(pre + (N,), np.uint8))
+            risk=np.zeros(pre + (N, A), np.uint8), margin_call=np.zeros(pre + (N,), np.uint8),
+            data_end=np.zeros(pre + (N,), np.uint8))
         s = Out(**{k: _ptr(v) for k, v in o.items()})
         return o, s
 
@@ -222,6 +228,18 @@ class OracleBatch:
         m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
         self.L.orc_reset(self.h, _ptr(m))
 
+    def set_replay(self, price, feats, ts, first, second, cache_size, stride=0):
+        """HDFSourceSingle over the file's arrays; returns the period."""
+        p = np.ascontiguousarray(price, dtype=np.float64).reshape(len(ts), self.A)
+        f = np.ascontiguousarray(feats, dtype=np.float64).reshape(len(ts), self.F)
+        t = np.ascontiguousarray(ts, dtype=np.uint64)
+        self._replay = (p, f, t)
+        r = self.L.orc_set_replay(self.h, _ptr(p), _ptr(f), _ptr(t), len(t), int(first),
+                                  int(second), int(cache_size), int(stride))
+        if r < 0:
+            raise ValueError("orc_set_replay rejected the arrays")
+        return int(r)
+
     def set_prices(self, prices):
         p = np.ascontiguousarray(prices, dtype=np.float64).reshape(self.N, self.A)
         self.L.orc_set_prices(self.h, _ptr(p))
@@ -247,7 +265,7 @@ class OracleBatch:
 
     def window(self):
         W, N, A = self.W, self.N, self.A
-        price = np.zeros((N, W, A))
+        price = np.zeros((N, W, self.F))
         port = np.zeros((N, W, A + 1))
         ts = np.zeros((N, W), np.uint64)
         self.L.orc_window(self.h, _ptr(price), _ptr(port), _ptr(ts))
@@ -349,3 +367,48 @@ class Ring:
         ts = np.zeros((self.N, self.W), np.uint64)
         self.L.orc_ring_gather(C.byref(self.s), _ptr(price), _ptr(port), _ptr(ts))
         return price, port, ts
+
+
+# ---------------------------------------------------------------------------
+# HDFSourceSingle time bounds (madigan/environments/cpp/DataSource.cpp:145-189,
+# :305-366), restated over a timestamp array held in memory.
+
+def _bsearch(ts, val):
+    """binarySearchSortedHDFArray (DataSource.cpp:164-189): size_t l = 0,
+    r = T, at most int(log2(T)) + 2 probes; exact match or the last probe."""
+    import math
+    T = len(ts)
+    max_tries = int(math.log2(T)) + 2
+    l, r, m = 0, T, 0
+    mask = (1 << 64) - 1
+    while l <= r and max_tries > 0:
+        max_tries -= 1
+        m = l + (r - l) // 2
+        if m >= T:
+            raise IndexError(f"probe {m} outside the dataset")
+        buf = int(ts[m])
+        if buf == val:
+            return m
+        if buf < val:
+            l = m + 1
+        else:
+            r = (m - 1) & mask
+    return m
+
+
+def hdf_bounds(ts, start_time=0, end_time=0):
+    """getTimeBounds + findBounds: (first, second, start_time, end_time)."""
+    ts = np.asarray(ts, dtype=np.uint64)
+    b0, b1 = int(ts[0]), int(ts[-1])
+    if start_time == 0 and end_time == 0:
+        start_time, end_time = b0, b1
+    elif not (start_time >= b0 and end_time <= b1):
+        raise IndexError("Given start and endTimes not within bounds found in timestamp data")
+    si, ei = _bsearch(ts, start_time), _bsearch(ts, end_time)
+    if ((ei - si) & ((1 << 64) - 1)) < 2:
+        raise ValueError(f"dset size only {ei - si} !")
+    buf = int(ts[si])
+    first = si if (buf == start_time or si == 0) else (si + 1 if buf < start_time else si)
+    buf = int(ts[ei])
+    second = ei if (buf == end_time or ei == len(ts) - 1) else (ei - 1 if buf > end_time else ei)
+    return first, second, start_time, end_time

@@ -33,6 +33,20 @@ def test_library_exports_every_declared_symbol():
     assert set(names) == exported, f"undeclared exports: {exported - set(names)}"
 
 
+def test_hdf_library_exports_every_declared_symbol():
+    from madigan_amd import hdf as H
+    txt = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "madigan_hdf.h")).read(),
+                 flags=re.S)
+    names = sorted(set(re.findall(r"\b(mgn_hdf_[a-z_0-9]+)\s*\(", txt)))
+    assert len(names) >= 9
+    lib = H.load_hdf()
+    for n in names:
+        assert hasattr(lib, n) and n in H.HDF_SYMBOLS, n
+    out = subprocess.run(["nm", "-D", "--defined-only", H.HDF_LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    assert set(re.findall(r" T (mgn_\w+)", out)) == set(names)
+
+
 def test_abi_version():
     assert L.load().mgn_abi_version() == L.ABI_VERSION
 
@@ -43,13 +57,16 @@ LAYOUT_C = r"""
 #include "madigan_amd.h"
 #define F(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
 int main(void) {
-  printf("mgn_config %zu\nmgn_traj %zu\nmgn_views %zu\nmgn_asset_source %zu\nmgn_ring %zu\n",
+  printf("mgn_config %zu\nmgn_traj %zu\nmgn_views %zu\nmgn_asset_source %zu\nmgn_ring %zu\n"
+         "mgn_replay_tape %zu\n",
          sizeof(mgn_config), sizeof(mgn_traj), sizeof(mgn_views), sizeof(mgn_asset_source),
-         sizeof(mgn_ring));
+         sizeof(mgn_ring), sizeof(mgn_replay_tape));
   F(mgn_config, seed) F(mgn_config, shaper) F(mgn_config, adaptation_rate)
   F(mgn_config, desired_portfolio) F(mgn_config, window) F(mgn_config, unit_size)
   F(mgn_views, out) F(mgn_views, n_envs) F(mgn_views, reward_dim) F(mgn_views, reset_mask)
-  F(mgn_ring, ring) F(mgn_ring, len) F(mgn_asset_source, p)
+  F(mgn_ring, ring) F(mgn_ring, len) F(mgn_asset_source, p) F(mgn_config, n_feats)
+  F(mgn_traj, data_end) F(mgn_views, replay_cursor) F(mgn_views, n_feats)
+  F(mgn_replay_tape, rows) F(mgn_replay_tape, stride)
   return 0;
 }
 """
@@ -64,7 +81,7 @@ def test_struct_layouts_match_ctypes(tmp_path):
     got = dict(line.split() for line in subprocess.run([str(exe)], capture_output=True, text=True,
                                                         check=True).stdout.splitlines())
     py = {"mgn_config": L.Config, "mgn_traj": L.Traj, "mgn_views": L.Views,
-          "mgn_asset_source": L.AssetSource, "mgn_ring": L.Ring}
+          "mgn_asset_source": L.AssetSource, "mgn_ring": L.Ring, "mgn_replay_tape": L.ReplayTape}
     for k, v in got.items():
         if "." in k:
             t, f = k.split(".")

@@ -1,6 +1,7 @@
 """Benchmark: batched madigan market-simulation step on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--fuse F] [--n-envs 8192]
+                    [--workload C3|C2|C4|C5]
 
 Workload (BASELINE.json configs[2], SURVEY 8d "C3"): 8192 envs x 8 assets per
 GPU, TrendOU generators (config.yaml:116-138), Broker with 1e-4 relative
@@ -15,6 +16,18 @@ state held in registers.
 For N>1 (torchrun, one process per GPU) envs are sharded by global index
 (env_offset) with no per-step collective; one RCCL all-gather of the
 per-env episode statistics closes the timed region.  Prints one JSON line.
+
+The other BASELINE.json configs (SURVEY 8d) are selectable with --workload;
+they carry a W = 64 sliding window, so a step there is one Env step (K = 1
+launch, ring row written in-kernel) plus StackerDiscrete.current_data of every
+env (the window gather kernel), as the agent needs the observation before it
+acts:
+  C2  4096 envs x 4 OU (mu 10, theta .08, phi .04), 2% cost, DSR, norm none
+  C4  8192 envs/GPU x 8 Composite (Synth 2 + OU 3 + TrendOU 3), 2% cost,
+      PPC (target [1,0..0], alpha .01) over the env log reward, norm log
+  C5  8192 envs/GPU x 16 HDF replay (synthetic OU paths written to an HDF5
+      file in the HDFSourceSingle layout generalised to (T, 16), staged to HBM
+      once, per-env start stride), 2% cost, DDR, norm none
 """
 from __future__ import annotations
 
@@ -110,6 +123,89 @@ def cpu_baseline(n_envs: int, A: int, budget_s: float = 12.0):
                        f"oracle/madigan_oracle.c built -O3 -march=x86-64-v3 -ffast-math")
 
 
+def composite_spec():
+    """C4: Synth(2, DataSource.cpp:477-480 first two) + OU(3) + TrendOU(3)."""
+    from madigan_amd.config import SourceSpec, ou_spec, synth_spec, trendou_spec
+    s = SourceSpec()
+    s.extend(synth_spec([1., 0.3], [2., 2.1], [1., 1.2], [0., 1.], 0.01, 0.0))
+    s.extend(ou_spec([10.0] * 3, [0.15] * 3, [0.04] * 3))
+    s.extend(trendou_spec(*[[p] * 3 for p in TRENDOU_P]))
+    return s
+
+
+def c5_replay_file(A: int, T: int, path: str) -> None:
+    """Synthetic OU paths (mu 10, theta .08, phi .04, as C2) in the replay
+    layout: price (T, A), features = prices, timestamps 1-minute bars."""
+    from scipy.signal import lfilter
+    from madigan_amd import write_hdf
+    rng = np.random.default_rng(0x6D6164 + 5)
+    mu, th, phi = 10.0, 0.08, 0.04
+    z = rng.standard_normal((T, A))
+    # x_t = (1 - theta) x_{t-1} + theta mu + mu phi z_t, x_0 = mu
+    x = lfilter([1.0], [1.0, -(1.0 - th)], th * mu + mu * phi * z, axis=0,
+                zi=np.full((1, A), (1.0 - th) * mu))[0]
+    ts = (np.arange(T, dtype=np.uint64) + np.uint64(27_000_000)) * np.uint64(60_000_000_000)
+    write_hdf(path, "synth/ou", [f"OU_{i}" for i in range(A)], x, x, ts,
+              price_key="price", feature_key="features", timestamp_key="timestamps")
+
+
+def workload_env(name, N, A, rank, dev):
+    """(BatchedEnv, description, window) for a --workload."""
+    from madigan_amd import BatchedEnv
+    from madigan_amd.config import ou_spec, spec_from_config, trendou_spec
+    seed = 0x6D6164 + int(name[1])
+    off = rank * N
+    if name == "C3":
+        spec = trendou_spec(*[[p] * A for p in TRENDOU_P])
+        return (BatchedEnv(spec, N, device=dev, seed=seed, env_offset=off, **c3_kwargs()),
+                "C3: TrendOU x8 assets per env, slippage 1e-4 + 2% cost broker, DDR eta=.001 n=1, "
+                "discrete actions via action_to_transaction, auto-reset", 0)
+    base = dict(required_margin=1.0, maintenance_margin=0.25, transaction_cost_rel=0.02,
+                unit_size=0.05, auto_reset=True, init_cash=1_000_000.0, window=64,
+                adaptation_rate=0.001)
+    if name == "C2":
+        spec = ou_spec([10.0] * A, [0.08] * A, [0.04] * A)
+        return (BatchedEnv(spec, N, device=dev, seed=seed, env_offset=off, reward_shaper="DSR",
+                           **base),
+                f"C2: OU x{A} (mu 10, theta .08, phi .04), 2% cost, DSR eta=.001, W=64 window "
+                "(norm none) gathered every step, auto-reset", 64)
+    if name == "C4":
+        spec = composite_spec()
+        return (BatchedEnv(spec, N, device=dev, seed=seed, env_offset=off, reward_shaper="PPC",
+                           cosine_temp=0.01, desired_portfolio=[1.0] + [0.0] * spec.n_assets,
+                           norm_type="log", **base),
+                "C4: Composite Synth(2)+OU(3)+TrendOU(3), 2% cost, PPC alpha=.01 target [1,0..0] "
+                "over the env log reward, W=64 window (norm log) gathered every step, auto-reset", 64)
+    if name == "C5":
+        import tempfile
+        T = 200_000
+        path = os.path.join(tempfile.gettempdir(), f"madigan_c5_{A}x{T}_r{rank}.h5")
+        if not os.path.exists(path):
+            c5_replay_file(A, T, path)
+        cfg = {"data_source_type": "HDFSourceSingle",
+               "data_source_config": {"filepath": path, "group_key": "synth/ou",
+                                      "price_key": "price", "feature_key": "features",
+                                      "timestamp_key": "timestamps", "cache_size": 10_000}}
+        t0 = time.perf_counter()
+        env = BatchedEnv(spec_from_config(cfg), N, device=dev, seed=seed, env_offset=off,
+                         reward_shaper="DDR", replay_stride=997, **base)
+        import torch
+        torch.cuda.synchronize()
+        env._stage_s = time.perf_counter() - t0
+        return (env, f"C5: HDF replay x{A} (synthetic OU paths, {T} rows, HDFSourceSingle layout "
+                     f"(T,{A}), cache_size 10000, staged to HBM once by pinned double-buffered H2D, "
+                     "env start stride 997 rows), 2% cost, DDR eta=.001, W=64 window (norm none) "
+                     "gathered every step, auto-reset", 64)
+    raise SystemExit(f"unknown workload {name}")
+
+
+def gather_bytes(env) -> float:
+    """Algorithmic bytes of one window gather launch: per env read the ring
+    W*(F+A+1)*8 + its timestamps W*8, write the same (price, portfolio, ts)."""
+    C = env.F + env.A + 1
+    return env.N * 2.0 * env.W * (C + 1) * 8
+
+
 def kernel_name(env, A: int) -> str:
     m = int(env.lib.mgn_get_layout(env.h))
     apad = 1 << max(0, (A - 1).bit_length())
@@ -132,12 +228,11 @@ def main():
                     help="also time 1/16/64/256 steps per launch (separate launches; keep it off "
                          "when profiling, so the kernel's rocprof average is the headline's)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--workload", default="C3", choices=["C2", "C3", "C4", "C5"])
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
-    from madigan_amd import BatchedEnv
-    from madigan_amd.config import trendou_spec
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -148,9 +243,10 @@ def main():
     dev = torch.device(f"cuda:{local_rank}")
     torch.cuda.set_device(dev)
 
+    if args.workload != "C3":
+        return windowed(args, world, rank, dev)
     N, A, F = args.n_envs, args.assets, args.fuse
-    spec = trendou_spec(*[[p] * A for p in TRENDOU_P])
-    env = BatchedEnv(spec, N, device=dev, seed=0x6D6164 + 3, env_offset=rank * N, **c3_kwargs())
+    env, _, _ = workload_env("C3", N, A, rank, dev)
     if args.layout:
         env.lib.mgn_set_layout(env.h, args.layout)
     total = args.warmup + args.steps
@@ -254,6 +350,93 @@ def main():
             res["fusion_sweep"] = sweep
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(N, A, args.cpu_budget)
+        print(json.dumps(res))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def windowed(args, world, rank, dev):
+    """C2 / C4 / C5: per step one K = 1 step launch + the window gather."""
+    import torch
+    import torch.distributed as dist
+    wl = args.workload
+    N = {"C2": 4096}.get(wl, args.n_envs)
+    A = {"C2": 4, "C4": 8, "C5": 16}[wl]
+    env, desc, W = workload_env(wl, N, A, rank, dev)
+    total = args.warmup + args.steps
+    actions = env.generate_actions(total, seed=0x6D6164)
+    traj = env.alloc_traj(1, fields=["reward", "shaped", "done", "obs_price", "obs_port",
+                                     "timestamp", "tprice", "tunits", "tcost", "risk",
+                                     "margin_call", "data_end"])
+    stream = torch.cuda.current_stream(dev)
+
+    def run(k0, k1, ev=None):
+        for k in range(k0, k1):
+            if ev is not None:
+                ev[0].append(torch.cuda.Event(enable_timing=True))
+                ev[0][-1].record(stream)
+            env.rollout(actions[k:k + 1], out=traj)
+            if ev is not None:
+                ev[1].append(torch.cuda.Event(enable_timing=True))
+                ev[1][-1].record(stream)
+            env.window()
+            if ev is not None:
+                ev[2].append(torch.cuda.Event(enable_timing=True))
+                ev[2][-1].record(stream)
+
+    run(0, args.warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = ([], [], [])
+    t0 = time.perf_counter()
+    run(args.warmup, total, ev)
+    stats = env.episode_stats
+    if world > 1:
+        gathered = torch.empty((world * N, 4), dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(gathered, stats)
+    else:
+        gathered = stats
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    step_us = float(np.mean([a.elapsed_time(b) for a, b in zip(ev[0], ev[1])])) * 1e3
+    gather_us = float(np.mean([b.elapsed_time(c) for b, c in zip(ev[1], ev[2])])) * 1e3
+    gb = gather_bytes(env)
+    achieved = gb / (gather_us * 1e-6) / 1e9
+    value = world * N * args.steps / elapsed
+    if rank == 0:
+        C = env.F + env.A + 1
+        res = {
+            "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": desc, "n_envs_per_gpu": N, "n_assets": A, "n_feats": env.F,
+                       "window": W, "steps_per_launch": 1,
+                       "parallelism": f"env-sharded x{world} (no per-step collective)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
+                         "traffic": load_pmc_traffic(f"{wl}_gather_{N}x{A}_W{W}"),
+                         "kernel": "mgn::k_ring_gather_elem" if env.cfg.norm_type != 3
+                         else "mgn::k_ring_gather",
+                         "bytes_per_env_step": 2.0 * W * (C + 1) * 8,
+                         "avg_launch_us": gather_us},
+            "step_kernel_avg_us": step_us,
+            "episodes_completed": int(gathered[:, 3].sum().item()),
+        }
+        if wl == "C5":
+            tape_bytes = sum(t.numel() * t.element_size() for t in env._tape.values())
+            res["replay_staging"] = {"tape_rows": int(env._tape["ts"].shape[0]),
+                                     "tape_bytes": tape_bytes, "stage_s": env._stage_s,
+                                     "pcie_inclusive_GBs": tape_bytes / env._stage_s / 1e9}
         print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()

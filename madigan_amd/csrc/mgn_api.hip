@@ -184,6 +184,7 @@ mgn::KParams kparams(const mgn_env* e) {
   const mgn_config& c = e->cfg;
   p.N = e->N; p.A = e->A; p.W = e->W; p.D = e->D; p.F = e->F;
   p.replay = e->replay ? 1 : 0;
+  p.ring_log = (e->W > 0 && c.norm_type == MGN_NORM_LOG) ? 1 : 0;
   p.rp_price = e->tape.price; p.rp_feat = e->tape.feats; p.rp_ts = e->tape.ts;
   p.rp_end = e->tape.data_end; p.rp_rows = e->tape.rows; p.rp_stride = e->tape.stride;
   p.env_offset = c.env_offset; p.seed = c.seed;
@@ -251,8 +252,31 @@ void launch_val(const mgn_env* e, double* out) {
 mgn::RingDesc ring_desc(const mgn_env* e) {
   mgn::RingDesc r;
   r.N = e->N; r.F = e->F; r.Pn = e->A + 1; r.W = e->W; r.norm = e->cfg.norm_type;
+  r.prelog = e->cfg.norm_type == MGN_NORM_LOG;  // the step kernel logs at push
   r.ring = e->v.ring; r.ring_ts = e->v.ring_ts; r.head = e->v.ring_head; r.len = e->v.ring_len;
   return r;
+}
+
+// StackerDiscrete.current_data: element-parallel for the element-wise
+// normalisers; column-parallel (two passes over the window per column) for
+// standard_normal
+void launch_gather(const mgn::RingDesc& r, double* price, double* port, uint64_t* ts,
+                   hipStream_t stream) {
+  const int C = r.F + r.Pn;
+  if (r.norm == MGN_NORM_STANDARD_NORMAL) {
+    const int64_t threads = (int64_t)r.N * C;
+    hipLaunchKernelGGL(mgn::k_ring_gather, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                       stream, r, price, port, ts);
+  } else if ((int64_t)r.N * r.W * C < ((int64_t)1 << 31) && r.W % 2 == 0) {
+    const uint32_t pairs = (uint32_t)((int64_t)r.N * r.W * C / 2);
+    const uint32_t per_block = 256 * mgn::GATHER_U;
+    hipLaunchKernelGGL(mgn::k_ring_gather_elem, dim3((pairs + per_block - 1) / per_block), dim3(256),
+                       0, stream, r, price, port, ts, pairs, 1.0 / (double)(r.W * C), 1.0 / (double)C);
+  } else {  // odd window or > 2^31 ring elements: the column-parallel kernel
+    const int64_t threads = (int64_t)r.N * C;
+    hipLaunchKernelGGL(mgn::k_ring_gather, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                       stream, r, price, port, ts);
+  }
 }
 
 }  // namespace
@@ -468,11 +492,8 @@ int mgn_window_clear(mgn_env* e, const uint8_t* mask_dev) {
 int mgn_window(mgn_env* e, double* price_dev, double* port_dev, uint64_t* ts_dev) {
   if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
   if (e->W == 0) return fail(e, MGN_ERR_CONFIG, "handle has no window (window_length = 0)");
-  const mgn::RingDesc r = ring_desc(e);
-  const int64_t threads = (int64_t)e->N * (e->F + e->A + 1);
-  hipLaunchKernelGGL(mgn::k_ring_gather, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
-                     e->stream, r, price_dev ? price_dev : e->v.win_price,
-                     port_dev ? port_dev : e->v.win_port, ts_dev ? ts_dev : e->v.win_ts);
+  launch_gather(ring_desc(e), price_dev ? price_dev : e->v.win_price,
+                port_dev ? port_dev : e->v.win_port, ts_dev ? ts_dev : e->v.win_ts, e->stream);
   return check_hip(e, hipGetLastError(), "mgn_window");
 }
 
@@ -506,6 +527,7 @@ int mgn_set_broker(mgn_env* e, double required_margin, double maintenance_margin
 static mgn::RingDesc ring_from(const mgn_ring* r) {
   mgn::RingDesc d;
   d.N = r->n_envs; d.F = r->n_price; d.Pn = r->n_port; d.W = r->window; d.norm = r->norm_type;
+  d.prelog = 0;
   d.ring = r->ring; d.ring_ts = r->ring_ts; d.head = r->head; d.len = r->len;
   return d;
 }
@@ -538,9 +560,7 @@ int mgn_ring_clear(const mgn_ring* r, const uint8_t* mask_dev, void* stream) {
 int mgn_ring_gather(const mgn_ring* r, double* price_dev, double* port_dev, uint64_t* ts_dev, void* stream) {
   int rc = ring_ok(r);
   if (rc != MGN_OK) return rc;
-  const int64_t threads = (int64_t)r->n_envs * (r->n_price + r->n_port);
-  hipLaunchKernelGGL(mgn::k_ring_gather, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, ring_from(r), price_dev, port_dev, ts_dev);
+  launch_gather(ring_from(r), price_dev, port_dev, ts_dev, (hipStream_t)stream);
   return check_hip(nullptr, hipGetLastError(), "mgn_ring_gather");
 }
 

@@ -11,6 +11,7 @@ namespace mgn {
 // (N, W, C) with C = F + P columns (price features then portfolio entries).
 struct RingDesc {
   int N, F, Pn, W, norm;
+  int prelog;  // norm "log" already applied to the price columns at push
   double* ring;
   uint64_t* ring_ts;
   int32_t* head;
@@ -25,7 +26,10 @@ __global__ void k_ring_push(RingDesc r, const double* __restrict__ price,
   const int C = r.F + r.Pn;
   const int h = (r.head[env] + 1) % r.W;
   double* row = r.ring + ((size_t)env * r.W + h) * C;
-  for (int c = 0; c < r.F; ++c) row[c] = price ? price[(size_t)env * r.F + c] : 0.;
+  for (int c = 0; c < r.F; ++c) {
+    const double v = price ? price[(size_t)env * r.F + c] : 0.;
+    row[c] = r.prelog ? log_norm(v) : v;
+  }
   for (int c = 0; c < r.Pn; ++c) row[r.F + c] = port ? port[(size_t)env * r.Pn + c] : 0.;
   r.ring_ts[(size_t)env * r.W + h] = ts ? ts[env] : 0;
   r.head[env] = h;
@@ -95,11 +99,89 @@ __global__ __launch_bounds__(BLOCK) void k_ring_gather(RingDesc r, double* __res
     double v = 0.;
     if (w < len) {
       v = base[(size_t)row_of(w) * C + c];
-      if (nt == MGN_NORM_LOG) v = log((v < 1e-5) ? 1e-5 : v);
+      if (nt == MGN_NORM_LOG && !r.prelog) v = log((v < 1e-5) ? 1e-5 : v);
       else if (nt == MGN_NORM_LOOKBACK) v = v / last;
       else if (nt == MGN_NORM_LOOKBACK_LOG) v = log(v / last);
     }
     o[(size_t)w * r.F] = v;
+  }
+}
+
+// current_data for the element-wise normalisers (none / log / lookback /
+// lookback_log), in the ring's physical order: the ring of all envs is one
+// contiguous array (N, W, C), so lane t of the grid reads 16 B pairs
+// 2t, 2t+1 (W even: a pair never straddles two envs), fully coalesced, and
+// scatters each element to its logical window row w = (row - head + len - 1)
+// mod W of the price (c < F) or portfolio (c >= F) output; rows w >= len are
+// written as zeros.  Index math is 32-bit with reciprocal division (exact
+// after one correction step).  HBM-bound: per env read W*(C+1)*8 B (ring +
+// timestamps), write W*(C+1)*8 B.
+__device__ __forceinline__ void divmod_u32(uint32_t n, uint32_t d, double inv, uint32_t& q,
+                                           uint32_t& r) {
+  q = (uint32_t)((double)n * inv);
+  int32_t rr = (int32_t)(n - q * d);
+  if (rr < 0) { q -= 1; rr += (int32_t)d; }
+  else if (rr >= (int32_t)d) { q += 1; rr -= (int32_t)d; }
+  r = (uint32_t)rr;
+}
+
+constexpr int GATHER_U = 4;  // 16-B pairs per lane per pass
+
+__global__ __launch_bounds__(BLOCK) void k_ring_gather_elem(RingDesc r, double* __restrict__ price_out,
+                                                            double* __restrict__ port_out,
+                                                            uint64_t* __restrict__ ts_out,
+                                                            uint32_t n_pairs, double inv_wc,
+                                                            double inv_c) {
+  const int C = r.F + r.Pn;
+  const uint32_t WC = (uint32_t)(r.W * C);
+  const int W = r.W;
+  const d2* src = reinterpret_cast<const d2*>(r.ring);
+  const uint32_t p0 = blockIdx.x * (BLOCK * GATHER_U) + threadIdx.x;
+  d2 v[GATHER_U];
+#pragma unroll
+  for (int u = 0; u < GATHER_U; ++u) {
+    const uint32_t pi = p0 + u * BLOCK;
+    if (pi < n_pairs) v[u] = src[pi];
+  }
+#pragma unroll
+  for (int u = 0; u < GATHER_U; ++u) {
+    const uint32_t pi = p0 + u * BLOCK;
+    if (pi >= n_pairs) continue;
+    uint32_t env, rem, pr, c;
+    divmod_u32(2 * pi, WC, inv_wc, env, rem);
+    divmod_u32(rem, (uint32_t)C, inv_c, pr, c);
+    const int len = r.len[env];
+    const int hd = r.head[env];
+    const double* base = r.ring + (size_t)env * WC;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      double x = h ? v[u].y : v[u].x;
+      const int w = ((int)pr - hd + len - 1 + 2 * W) % W;
+      const bool valid = w < len;
+      if (!valid) x = 0.;
+      if ((int)c >= r.F) {
+        if (port_out) port_out[((size_t)env * W + w) * r.Pn + ((int)c - r.F)] = x;
+      } else {
+        if (c == 0 && ts_out) ts_out[(size_t)env * W + w] = valid ? r.ring_ts[(size_t)env * W + pr] : 0;
+        if (price_out) {
+          if (valid) {
+            const int nt = r.norm;
+            if (nt == MGN_NORM_LOG && !r.prelog) {
+              x = log((x < 1e-5) ? 1e-5 : x);
+            } else if (nt == MGN_NORM_LOOKBACK || nt == MGN_NORM_LOOKBACK_LOG) {
+              x = x / base[(size_t)hd * C + c];
+              if (nt == MGN_NORM_LOOKBACK_LOG) x = log(x);
+            }
+          }
+          price_out[((size_t)env * W + w) * r.F + c] = x;
+        }
+      }
+      // the pair's second element: next column, or column 0 of the next row
+      if (++c == (uint32_t)C) {
+        c = 0;
+        ++pr;
+      }
+    }
   }
 }
 

@@ -28,6 +28,7 @@ constexpr int BLOCK = 256;
 struct KParams {
   int N, A, W, D;
   int F;       // State.price width (features): A for the generators
+  int ring_log;  // window norm "log": the ring stores log(max(x, 1e-5)) (applied once at push)
   int replay;  // every asset from the replay tape (MGN_SRC_REPLAY)
   int64_t env_offset;
   uint64_t seed;
@@ -273,15 +274,21 @@ __device__ __forceinline__ uint64_t next_ts(const Lane<M>& s, const KParams& p, 
 
 // State.price of the current tick for the lane's columns (features): the
 // replay tape's feature row, else the generator prices (F = A)
+__device__ __forceinline__ double log_norm(double x) { return log((x < 1e-5) ? 1e-5 : x); }
+
+// lg: apply StackerDiscrete's log normaliser (preprocessor.py:79-81)
 template <int M, int S>
 __device__ __forceinline__ void put_feats(const Lane<M>& s, const KParams& p, int ls,
-                                          double* __restrict__ dst) {
+                                          double* __restrict__ dst, bool lg = false) {
   if (p.replay) {
-    for (int f = ls; f < p.F; f += S) dst[f] = p.rp_feat[(size_t)s.row * p.F + f];
+    for (int f = ls; f < p.F; f += S) {
+      const double v = p.rp_feat[(size_t)s.row * p.F + f];
+      dst[f] = lg ? log_norm(v) : v;
+    }
   } else {
 #pragma unroll
     for (int m = 0; m < M; ++m)
-      if (s.valid[m]) dst[s.asset[m]] = s.P[m];
+      if (s.valid[m]) dst[s.asset[m]] = lg ? log_norm(s.P[m]) : s.P[m];
   }
 }
 
@@ -311,7 +318,7 @@ __device__ __forceinline__ void ring_push(const Lane<M>& s, const KParams& p, in
   if (len < p.W) len += 1;
   const int R = p.F + p.A + 1;
   double* row = p.ring + ((size_t)env * p.W + head) * R;
-  put_feats<M, S>(s, p, ls, row);
+  put_feats<M, S>(s, p, ls, row, p.ring_log != 0);
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     if (!s.valid[m]) continue;

@@ -60,7 +60,9 @@ enum { MGN_GREEN = 0, MGN_INSUFF_MARGIN = 1, MGN_MARGIN_CALL = 2, MGN_BLOWN_OUT 
 
 /* per-asset generator kind (DataSource.cpp:56-108 factory names) */
 enum { MGN_SRC_EXTERNAL = 0, MGN_SRC_SINE = 1, MGN_SRC_OU = 2, MGN_SRC_TRENDOU = 3,
-       MGN_SRC_REPLAY = 4 /* every asset of the env, from the attached replay tape */ };
+       MGN_SRC_REPLAY = 4 /* every asset of the env, from the attached replay tape */,
+       MGN_SRC_SIMPLETREND = 5, MGN_SRC_TRENDYOU = 6, MGN_SRC_GAUSSIAN = 7,
+       MGN_SRC_SAWTOOTH = 8, MGN_SRC_TRIANGLE = 9, MGN_SRC_OUPAIR = 10 };
 
 enum { MGN_SHAPER_NONE = 0, MGN_SHAPER_DSR = 1, MGN_SHAPER_DDR = 2, MGN_SHAPER_PPC = 3 };
 enum { MGN_REWARD_ENV_LOG = 0, MGN_REWARD_AGENT_SUM = 1, MGN_REWARD_AGENT_PER_ASSET = 2 };
@@ -74,7 +76,14 @@ enum { MGN_STEP_NONE = 0, MGN_STEP_UNITS = 1, MGN_STEP_SINGLE = 2 };
  *  OU      p = {mean, theta, phi}                           DataSource.cpp:1118-1137
  *  TRENDOU p = {trendProb, minPeriod, maxPeriod, dYMin, dYMax, start,
  *               theta, phi, noiseTrend, emaAlpha}           DataSource.cpp:1364-1408
- *  REPLAY  p = {}  (all assets or none; see mgn_attach_replay) */
+ *  REPLAY  p = {}  (all assets or none; see mgn_attach_replay)
+ *  SIMPLETREND p = {trendProb, minPeriod, maxPeriod, noise, start, dYMin, dYMax}
+ *                                                           DataSource.cpp:1252-1356
+ *  TRENDYOU    p = as TRENDOU                               DataSource.cpp:1506-1653
+ *  GAUSSIAN    p = {mean, var (the normal's stddev)}        DataSource.cpp:1057-1114
+ *  SAWTOOTH / TRIANGLE p = as SINE                          DataSource.cpp:557-577
+ *  OUPAIR      p = {theta, phi, noise, role}: role 0 / 1 = the pair's first /
+ *              second asset, adjacent in asset order        DataSource.cpp:1183-1250 */
 typedef struct {
   int32_t kind;
   int32_t pad_;

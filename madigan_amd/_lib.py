@@ -19,7 +19,8 @@ MAX_NSTEP = 64
 OK, ERR_CONFIG, ERR_INDEX, ERR_LENGTH, ERR_DEVICE, ERR_ARG = range(6)
 
 GREEN, INSUFF_MARGIN, MARGIN_CALL, BLOWN_OUT = range(4)
-SRC_EXTERNAL, SRC_SINE, SRC_OU, SRC_TRENDOU, SRC_REPLAY = range(5)
+(SRC_EXTERNAL, SRC_SINE, SRC_OU, SRC_TRENDOU, SRC_REPLAY, SRC_SIMPLETREND, SRC_TRENDYOU, SRC_GAUSSIAN,
+ SRC_SAWTOOTH, SRC_TRIANGLE, SRC_OUPAIR) = range(11)
 SHAPER_NONE, SHAPER_DSR, SHAPER_DDR, SHAPER_PPC = range(4)
 REWARD_ENV_LOG, REWARD_AGENT_SUM, REWARD_AGENT_PER_ASSET = range(3)
 NORM_NONE, NORM_LOG, NORM_LOOKBACK, NORM_STANDARD_NORMAL, NORM_LOOKBACK_LOG = range(5)

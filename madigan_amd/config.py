@@ -11,6 +11,13 @@ Mirrors the reference's config handling for the data sources on the hot path:
               renamed code+"_1"                         DataSource.cpp:411-437
   default constructors Synth()/OU()/TrendOU()          DataSource.cpp:475-482, :1142,
                                                        :1418-1423
+  SimpleTrend keys (trend_prob min_period max_period noise dYMin dYMax start)
+                                                       Config.cpp:422-476
+  TrendyOU    keys as TrendOU                          Config.cpp:127-139, :479-549
+  OUPair      keys (theta phi noise)                   Config.cpp:387-419
+  SawTooth / Triangle keys as Synth                    Config.cpp:15-28
+  Gaussian    from config always raises: its key check asks for "" (Config.cpp:324),
+              reproduced; the default constructor works
   HDFSourceSingle keys (filepath group_key price_key feature_key timestamp_key
               cache_size [start_time end_time])        Config.cpp:551-576,
                                                        DataSource.cpp:227-262
@@ -25,9 +32,9 @@ from typing import Any, List, Optional, Tuple
 
 from . import _lib as L
 
-SUPPORTED = ("Synth", "OU", "TrendOU", "Composite", "HDFSourceSingle")
-NOT_YET = ("SawTooth", "Triangle", "SineAdder", "SineDynamic", "SineDynamicTrend", "Gaussian",
-           "OUPair", "SimpleTrend", "TrendyOU")
+SUPPORTED = ("Synth", "OU", "TrendOU", "Composite", "HDFSourceSingle", "SimpleTrend", "TrendyOU",
+             "Gaussian", "SawTooth", "Triangle", "OUPair")
+NOT_YET = ("SineAdder", "SineDynamic", "SineDynamicTrend")
 HDF_KEYS = ("filepath", "group_key", "feature_key", "timestamp_key", "price_key", "cache_size")
 
 
@@ -81,11 +88,13 @@ def _same_len(name: str, *vecs) -> int:
     return n
 
 
-def synth_spec(freq, mu, amp, phase, dX, noise=0.0) -> SourceSpec:
-    n = _same_len("Synth", freq, mu, amp, phase)
+def synth_spec(freq, mu, amp, phase, dX, noise=0.0, kind: int = L.SRC_SINE,
+               name: str = "Synth") -> SourceSpec:
+    """Synth (and its SawTooth / Triangle subclasses, DataSource.h:413-423)."""
+    n = _same_len(name, freq, mu, amp, phase)
     s = SourceSpec()
     for i in range(n):
-        s.kinds.append(L.SRC_SINE)
+        s.kinds.append(kind)
         s.params.append([float(freq[i]), float(mu[i]), float(amp[i]), float(phase[i]), float(dX),
                          float(noise)])
         s.assets.append(f"sine_{i}")
@@ -114,6 +123,42 @@ def trendou_spec(trendProb, minPeriod, maxPeriod, dYMin, dYMax, start, theta, ph
                          float(phi[i]), float(noiseTrend[i]), float(emaAlpha[i])])
         s.assets.append(f"TrendOU_{i}")
     return s
+
+
+def simpletrend_spec(trendProb, minPeriod, maxPeriod, noise, start, dYMin, dYMax) -> SourceSpec:
+    """SimpleTrend::initParams (DataSource.cpp:1252-1283)."""
+    n = _same_len("SimpleTrend", trendProb, minPeriod, maxPeriod, noise, start, dYMin, dYMax)
+    s = SourceSpec()
+    for i in range(n):
+        s.kinds.append(L.SRC_SIMPLETREND)
+        s.params.append([float(trendProb[i]), float(int(minPeriod[i])), float(int(maxPeriod[i])),
+                         float(noise[i]), float(start[i]), float(dYMin[i]), float(dYMax[i])])
+        s.assets.append(f"SimpleTrend_{i}")
+    return s
+
+
+def trendyou_spec(trendProb, minPeriod, maxPeriod, dYMin, dYMax, start, theta, phi, noiseTrend,
+                  emaAlpha) -> SourceSpec:
+    """TrendyOU::initParams (DataSource.cpp:1506-1552): TrendOU's parameters."""
+    s = trendou_spec(trendProb, minPeriod, maxPeriod, dYMin, dYMax, start, theta, phi, noiseTrend,
+                     emaAlpha)
+    s.kinds = [L.SRC_TRENDYOU] * s.n_assets
+    s.assets = [f"TrendyOU_{i}" for i in range(s.n_assets)]
+    return s
+
+
+def gaussian_spec(mean, var) -> SourceSpec:
+    """Gaussian::initParams (DataSource.cpp:1057-1075): normal(mean, var)."""
+    n = _same_len("Gaussian", mean, var)
+    return SourceSpec(kinds=[L.SRC_GAUSSIAN] * n, params=[[float(m), float(v)] for m, v in zip(mean, var)],
+                      assets=[f"Gaussian_{i}" for i in range(n)])
+
+
+def oupair_spec(theta, phi, noise) -> SourceSpec:
+    """OUPair::initParams (DataSource.cpp:1183-1196): two assets, one shared mean."""
+    p = [float(theta), float(phi), float(noise)]
+    return SourceSpec(kinds=[L.SRC_OUPAIR] * 2, params=[p + [0.0], p + [1.0]],
+                      assets=["OUPair_0", "OUPair_1"])
 
 
 def replay_spec(n_assets: int, n_feats: int = 0, assets=None, hdf: Optional[dict] = None) -> SourceSpec:
@@ -147,9 +192,21 @@ def default_spec(source_type: str) -> SourceSpec:
                           [0., 1., 2., 1.], 0.01, 0.)
     if source_type == "OU":
         return ou_spec([2., 4.3, 3., 0.5], [1., 0.3, 2., 0.5], [2., 2.1, 2.2, 2.3])
-    if source_type == "TrendOU":
-        return trendou_spec([0.001, 0.001], [100, 500], [200, 1500], [0.001, 0.01], [0.003, 0.03],
-                            [10., 15.], [1., 0.5], [2., 2.1], [1., 1.2], [0.1, 0.2])
+    if source_type in ("TrendOU", "TrendyOU"):
+        f = trendou_spec if source_type == "TrendOU" else trendyou_spec
+        return f([0.001, 0.001], [100, 500], [200, 1500], [0.001, 0.01], [0.003, 0.03],
+                 [10., 15.], [1., 0.5], [2., 2.1], [1., 1.2], [0.1, 0.2])
+    if source_type in ("SawTooth", "Triangle"):  # Synth() (DataSource.cpp:475-482)
+        kind = L.SRC_SAWTOOTH if source_type == "SawTooth" else L.SRC_TRIANGLE
+        return synth_spec([1., 0.3, 2., 0.5], [2., 2.1, 2.2, 2.3], [1., 1.2, 1.3, 1.],
+                          [0., 1., 2., 1.], 0.01, 0., kind=kind, name=source_type)
+    if source_type == "SimpleTrend":  # DataSource.cpp:1291-1293
+        return simpletrend_spec([0.001, 0.001], [100, 500], [200, 1500], [1., 0.1], [10., 15.],
+                                [0.001, 0.01], [0.003, 0.03])
+    if source_type == "Gaussian":     # DataSource.cpp:1079
+        return gaussian_spec([2., 5., 10., 15.], [1., 1., 2., 5.])
+    if source_type == "OUPair":       # DataSource.cpp:1201
+        return oupair_spec(.015, .01, .03)
     return _not_implemented(source_type)
 
 
@@ -189,10 +246,28 @@ def spec_from_config(config: Any) -> SourceSpec:
         return ou_spec(params["mean"], params["theta"], params["phi"])
     if source_type == "HDFSourceSingle":
         return hdf_spec(params)
-    if source_type == "TrendOU":
+    if source_type in ("SawTooth", "Triangle"):
+        _require(params, ("freq", "mu", "amp", "phase", "dX", "noise"))
+        kind = L.SRC_SAWTOOTH if source_type == "SawTooth" else L.SRC_TRIANGLE
+        return synth_spec(params["freq"], params["mu"], params["amp"], params["phase"],
+                          params["dX"], params["noise"], kind=kind, name=source_type)
+    if source_type == "SimpleTrend":
+        _require(params, ("trend_prob", "min_period", "max_period", "noise", "dYMin", "dYMax",
+                          "start"))
+        return simpletrend_spec(params["trend_prob"], params["min_period"], params["max_period"],
+                                params["noise"], params["start"], params["dYMin"], params["dYMax"])
+    if source_type == "Gaussian":
+        # makeGaussianConfigFromPyDict checks for the keys {"mean", ""} (Config.cpp:324):
+        # the empty key is never present, so the reference always raises here
+        _require(params, ("mean", ""))
+    if source_type == "OUPair":
+        _require(params, ("theta", "phi", "noise"))
+        return oupair_spec(params["theta"], params["phi"], params["noise"])
+    if source_type in ("TrendOU", "TrendyOU"):
         _require(params, ("trend_prob", "min_period", "max_period", "dYMin", "dYMax", "start",
                           "theta", "phi", "noise_trend", "ema_alpha"))
-        return trendou_spec(params["trend_prob"], params["min_period"], params["max_period"],
+        f = trendou_spec if source_type == "TrendOU" else trendyou_spec
+        return f(params["trend_prob"], params["min_period"], params["max_period"],
                             params["dYMin"], params["dYMax"], params["start"], params["theta"],
                             params["phi"], params["noise_trend"], params["ema_alpha"])
     return _not_implemented(source_type)

@@ -167,11 +167,20 @@ int validate(const mgn_config* c, const mgn_asset_source* s, std::string& msg) {
   }
   for (int i = 0; i < c->n_assets; ++i) {
     const int k = s[i].kind;
-    if (k < MGN_SRC_EXTERNAL || k > MGN_SRC_REPLAY) {
+    if (k < MGN_SRC_EXTERNAL || k > MGN_SRC_OUPAIR) {
       msg = "unknown data source kind for asset " + std::to_string(i);
       return MGN_ERR_CONFIG;
     }
-    if (k == MGN_SRC_TRENDOU && s[i].p[2] < s[i].p[1]) {
+    if (k == MGN_SRC_OUPAIR) {
+      const bool first = s[i].p[3] == 0.0;
+      const int j = first ? i + 1 : i - 1;
+      if (j < 0 || j >= c->n_assets || s[j].kind != MGN_SRC_OUPAIR || (s[j].p[3] == 0.0) == first) {
+        msg = "OUPair assets come in adjacent (role 0, role 1) pairs; asset " + std::to_string(i);
+        return MGN_ERR_CONFIG;
+      }
+    }
+    if ((k == MGN_SRC_TRENDOU || k == MGN_SRC_TRENDYOU || k == MGN_SRC_SIMPLETREND) &&
+        s[i].p[2] < s[i].p[1]) {
       msg = "TrendOU maxPeriod < minPeriod for asset " + std::to_string(i);
       return MGN_ERR_CONFIG;
     }

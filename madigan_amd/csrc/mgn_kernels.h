@@ -253,12 +253,84 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
       double x = s.P[m];
       x += (q[1] * (q[0] - x)) + q[0] * q[2] * z;
       s.P[m] = x;
-    } else if (kind == MGN_SRC_SINE) {
+    } else if (kind == MGN_SRC_SINE || kind == MGN_SRC_SAWTOOTH || kind == MGN_SRC_TRIANGLE) {
+      // Synth / SawTooth / Triangle::getData (DataSource.cpp:535-543, 557-577)
       double noise = 0.0;
       if (q[5] != 0.0) noise = draw0(p.seed, genv, (uint32_t)a, tick).z * q[5] + 0.0;
       const double PI2 = 3.141592653589793238463 * 2;
-      s.P[m] = noise + q[1] + q[2] * det_sin(PI2 * s.sx[m] * q[0]);
+      double wave;
+      if (kind == MGN_SRC_SINE) wave = q[2] * det_sin(PI2 * s.sx[m] * q[0]);
+      else if (kind == MGN_SRC_SAWTOOTH) wave = q[2] * frac_part(s.sx[m] * q[0]);
+      else wave = 4 * q[2] / PI2 * det_asin(det_sin(PI2 * s.sx[m] / q[0]));
+      s.P[m] = noise + q[1] + wave;
       s.sx[m] += q[4];
+    } else if (kind == MGN_SRC_SIMPLETREND) {
+      // SimpleTrend::getData (DataSource.cpp:1322-1347)
+      double y = s.P[m];
+      const Draw d = draw0(p.seed, genv, (uint32_t)a, tick);
+      if (s.tfl[m] & 1) {
+        const double dir = (s.tfl[m] & 2) ? -1.0 : 1.0;
+        y += y * s.dy[m] * dir;
+        s.tlen[m] -= 1;
+        if (s.tlen[m] == 0) s.tfl[m] &= ~1;
+      } else if (d.ut < q[0]) {
+        double u_len, u_dy;
+        uniform2(p.seed, genv, (uint32_t)a, 1, tick, u_len, u_dy);
+        const int32_t lo = (int32_t)q[1], hi = (int32_t)q[2];
+        int32_t len = lo + (int32_t)(u_len * (double)(hi - lo + 1));
+        s.tlen[m] = len > hi ? hi : len;
+        s.dy[m] = (q[6] - q[5]) * u_dy + q[5];
+        s.tfl[m] = (uint8_t)(1 | (d.dbit ? 2 : 0));
+      }
+      if (y <= .1) s.tfl[m] &= ~2;
+      y += y * (d.z * q[3] + 0.0);
+      s.P[m] = (0.01 < y) ? y : 0.01;
+    } else if (kind == MGN_SRC_TRENDYOU) {
+      // TrendyOU::getData (DataSource.cpp:1608-1640): sx = ouComponent, oum = trendComponent
+      const Draw d = draw0(p.seed, genv, (uint32_t)a, tick);
+      const double ou_noise = s.oum[m] * (d.z * q[7] + 0.0);
+      const double ou_rev = q[6] * (-s.sx[m]);
+      s.sx[m] += ou_rev + ou_noise;
+      const int32_t lo = (int32_t)q[1], hi = (int32_t)q[2];
+      if (s.tfl[m] & 1) {
+        double tc = s.oum[m];
+        const double dir = (s.tfl[m] & 2) ? -1.0 : 1.0;
+        tc += tc * (s.dy[m] * dir);
+        tc = (0.1 < tc) ? tc : 0.1;
+        if (tc <= .1) {  // floored: restart an up-trend of a fresh length
+          double u_len, u_dy;
+          uniform2(p.seed, genv, (uint32_t)a, 1, tick, u_len, u_dy);
+          const int32_t len = lo + (int32_t)(u_len * (double)(hi - lo + 1));
+          s.tlen[m] = len > hi ? hi : len;
+          s.tfl[m] = 1;
+        }
+        s.oum[m] = tc;
+        s.tlen[m] -= 1;
+        if (s.tlen[m] == 0) s.tfl[m] &= ~1;
+      } else if (d.ut < q[0]) {
+        double u_len, u_dy;
+        uniform2(p.seed, genv, (uint32_t)a, 1, tick, u_len, u_dy);
+        const int32_t len = lo + (int32_t)(u_len * (double)(hi - lo + 1));
+        s.tlen[m] = len > hi ? hi : len;
+        s.dy[m] = (q[4] - q[3]) * u_dy + q[3];
+        s.tfl[m] = (uint8_t)(1 | (d.dbit ? 2 : 0));
+      }
+      s.P[m] = s.sx[m] + s.oum[m];
+    } else if (kind == MGN_SRC_GAUSSIAN) {
+      // Gaussian::getData (DataSource.cpp:1108-1114): normal(mean, var)
+      s.P[m] = draw0(p.seed, genv, (uint32_t)a, tick).z * q[1] + q[0];
+    } else if (kind == MGN_SRC_OUPAIR) {
+      // OUPair::getData (DataSource.cpp:1236-1244): the pair's shared mean random
+      // walk is recomputed identically by the lanes of both assets (its variate
+      // is keyed by the pair's first asset, counter slot 2)
+      const uint32_t a0 = (uint32_t)(a - (q[3] != 0.0 ? 1 : 0));
+      double mean = s.oum[m];
+      mean += mean * (draw_s(p.seed, genv, a0, 2, tick).z * q[2] + 0.0);
+      const double z = draw0(p.seed, genv, (uint32_t)a, tick).z * q[1] + 0.0;
+      double x = s.P[m];
+      x += (q[0] * (mean - x)) + mean * z;
+      s.P[m] = x;
+      s.oum[m] = mean;
     } else {
       s.P[m] = p.ext[(size_t)env * p.A + a];
     }
@@ -298,12 +370,27 @@ template <int M>
 __device__ __forceinline__ void src_reset(Lane<M>& s, const KParams& p) {
 #pragma unroll
   for (int m = 0; m < M; ++m) {
-    if (s.valid[m] && s.kind[m] == MGN_SRC_TRENDOU) {
-      const double start = p.src[s.asset[m]].p[5];
+    if (!s.valid[m]) continue;
+    const double* q = p.src[s.asset[m]].p;
+    const int kind = s.kind[m];
+    if (kind == MGN_SRC_TRENDOU) {
       s.tfl[m] &= ~1;
-      s.P[m] = start;
+      s.P[m] = q[5];
       s.tlen[m] = 0;
-      s.oum[m] = start;
+      s.oum[m] = q[5];
+    } else if (kind == MGN_SRC_SIMPLETREND) {  // DataSource.cpp:1349-1356
+      s.P[m] = q[4];
+      s.tfl[m] = 0;  // not trending, direction +1
+      s.tlen[m] = 0;
+    } else if (kind == MGN_SRC_TRENDYOU) {     // DataSource.cpp:1642-1653
+      s.sx[m] = 0.;
+      s.oum[m] = q[5];
+      s.tfl[m] &= ~1;
+      s.P[m] = q[5];
+      s.tlen[m] = 0;
+    } else if (kind == MGN_SRC_OUPAIR) {       // DataSource.cpp:1246-1250
+      s.P[m] = 10.;
+      s.oum[m] = 10.;
     }
   }
 }
@@ -1237,11 +1324,17 @@ __global__ __launch_bounds__(BLOCK) void k_init_reset(KParams p, int mode,
       s.kind[m] = s.valid[m] ? p.src[a].kind : -1;
       if (!s.valid[m]) continue;
       const double* q = p.src[a].p;
-      if (s.kind[m] == MGN_SRC_SINE) s.sx[m] = q[3];
-      else if (s.kind[m] == MGN_SRC_OU) s.P[m] = q[0];
-      else if (s.kind[m] == MGN_SRC_TRENDOU) {
+      const int kd = s.kind[m];
+      if (kd == MGN_SRC_SINE || kd == MGN_SRC_SAWTOOTH || kd == MGN_SRC_TRIANGLE) s.sx[m] = q[3];
+      else if (kd == MGN_SRC_OU) s.P[m] = q[0];
+      else if (kd == MGN_SRC_TRENDOU || kd == MGN_SRC_TRENDYOU) {
         s.P[m] = q[5];
         s.oum[m] = q[5];
+      } else if (kd == MGN_SRC_SIMPLETREND) s.P[m] = q[4];
+      else if (kd == MGN_SRC_GAUSSIAN) s.P[m] = q[0];
+      else if (kd == MGN_SRC_OUPAIR) {
+        s.P[m] = 10.;
+        s.oum[m] = 10.;
       }
     }
     ts = 0;

@@ -173,8 +173,9 @@ struct Draw {
   uint32_t dbit;
 };
 
-__device__ __forceinline__ Draw draw0(uint64_t seed, uint64_t env, uint32_t asset, uint64_t tick) {
-  const u4 x = block(seed, env, asset, 0, tick);
+__device__ __forceinline__ Draw draw_s(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot,
+                                      uint64_t tick) {
+  const u4 x = block(seed, env, asset, slot, tick);
   const uint64_t a = (((uint64_t)x.y << 32) | x.x) >> 11;
   const double u1 = (double)(a + 1) * TWO_M53;
   const double u2 = (double)x.z * TWO_M32;
@@ -183,6 +184,56 @@ __device__ __forceinline__ Draw draw0(uint64_t seed, uint64_t env, uint32_t asse
   d.ut = (double)x.w * TWO_M32;
   d.dbit = x.x & 1u;
   return d;
+}
+
+__device__ __forceinline__ Draw draw0(uint64_t seed, uint64_t env, uint32_t asset, uint64_t tick) {
+  return draw_s(seed, env, asset, 0, tick);
+}
+
+// std::modf's fractional part: x - trunc(x) is exact; its sign follows x (modf(-3.0) = -0.0)
+__device__ __forceinline__ double frac_part(double x) { return copysign(x - trunc(x), x); }
+
+// fdlibm e_asin.c on |x| <= 1 (same statements as the oracle's orc_asin)
+__device__ __noinline__ double det_asin(double x) {
+  const double pio2_hi = bits_to_d(0x3FF921FB54442D18ull), pio2_lo = bits_to_d(0x3C91A62633145C07ull),
+               pio4_hi = bits_to_d(0x3FE921FB54442D18ull);
+  const double pS0 = bits_to_d(0x3FC5555555555555ull), pS1 = bits_to_d(0xBFD4D61203EB6F7Dull),
+               pS2 = bits_to_d(0x3FC9C1550E884455ull), pS3 = bits_to_d(0xBFA48228B5688F3Bull),
+               pS4 = bits_to_d(0x3F49EFE07501B288ull), pS5 = bits_to_d(0x3F023DE10DFDF709ull),
+               qS1 = bits_to_d(0xC0033A271C8A2D4Bull), qS2 = bits_to_d(0x40002AE59C598AC8ull),
+               qS3 = bits_to_d(0xBFE6066C1B8D0159ull), qS4 = bits_to_d(0x3FB3B8C5B12E9282ull);
+  const uint64_t bx = d_to_bits(x);
+  const int32_t hx = (int32_t)(bx >> 32);
+  const int32_t ix = hx & 0x7fffffff;
+  if (ix >= 0x3ff00000) {
+    if (((ix - 0x3ff00000) | (int32_t)(uint32_t)bx) == 0) return x * pio2_hi + x * pio2_lo;
+    return (x - x) / (x - x);
+  }
+  if (ix < 0x3fe00000) {
+    if (ix < 0x3e400000) return x;
+    const double t = x * x;
+    const double p = t * (pS0 + t * (pS1 + t * (pS2 + t * (pS3 + t * (pS4 + t * pS5)))));
+    const double q = 1.0 + t * (qS1 + t * (qS2 + t * (qS3 + t * qS4)));
+    const double w = p / q;
+    return x + x * w;
+  }
+  double w = 1.0 - fabs(x);
+  double t = w * 0.5;
+  double p = t * (pS0 + t * (pS1 + t * (pS2 + t * (pS3 + t * (pS4 + t * pS5)))));
+  double q = 1.0 + t * (qS1 + t * (qS2 + t * (qS3 + t * qS4)));
+  const double sr = sqrt(t);
+  if (ix >= 0x3FEF3333) {
+    w = p / q;
+    t = pio2_hi - (2.0 * (sr + sr * w) - pio2_lo);
+  } else {
+    w = bits_to_d(d_to_bits(sr) & 0xffffffff00000000ull);
+    const double c = (t - w * w) / (sr + w);
+    const double r = p / q;
+    p = 2.0 * sr * r - (pio2_lo - 2.0 * c);
+    q = pio4_hi - 2.0 * w;
+    t = pio4_hi - (p - q);
+  }
+  return (hx > 0) ? t : -t;
 }
 
 }  // namespace mgn

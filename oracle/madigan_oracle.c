@@ -203,6 +203,65 @@ void orc_draw0(uint64_t seed, uint64_t env, uint32_t asset, uint64_t tick, doubl
   *dbit = x[0] & 1u;
 }
 
+/* the same variates from the block of counter slot `slot` (orc_draw0 = slot 0) */
+static void draw_slot(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot, uint64_t tick,
+                      double *z, double *ut, uint32_t *dbit) {
+  uint32_t ctr[4] = {(uint32_t)tick, (uint32_t)env, asset | (slot << 16),
+                     (uint32_t)(tick >> 32) ^ (uint32_t)(env >> 32)};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t x[4];
+  orc_philox4x32_10(ctr, key, x);
+  uint64_t a = (((uint64_t)x[1] << 32) | x[0]) >> 11;
+  double u1 = (double)(a + 1) * TWO_M53;
+  double u2 = (double)x[2] * TWO_M32;
+  *z = sqrt(-2.0 * orc_log(u1)) * orc_cos2pi(u2);
+  *ut = (double)x[3] * TWO_M32;
+  *dbit = x[0] & 1u;
+}
+
+/* fdlibm e_asin.c (Sun Microsystems) on |x| <= 1, plain binary64 */
+double orc_asin(double x) {
+  const double pio2_hi = from_bits(0x3FF921FB54442D18ull), pio2_lo = from_bits(0x3C91A62633145C07ull),
+               pio4_hi = from_bits(0x3FE921FB54442D18ull);
+  const double pS0 = from_bits(0x3FC5555555555555ull), pS1 = from_bits(0xBFD4D61203EB6F7Dull),
+               pS2 = from_bits(0x3FC9C1550E884455ull), pS3 = from_bits(0xBFA48228B5688F3Bull),
+               pS4 = from_bits(0x3F49EFE07501B288ull), pS5 = from_bits(0x3F023DE10DFDF709ull),
+               qS1 = from_bits(0xC0033A271C8A2D4Bull), qS2 = from_bits(0x40002AE59C598AC8ull),
+               qS3 = from_bits(0xBFE6066C1B8D0159ull), qS4 = from_bits(0x3FB3B8C5B12E9282ull);
+  uint64_t bx = to_bits(x);
+  int32_t hx = (int32_t)(bx >> 32);
+  int32_t ix = hx & 0x7fffffff;
+  if (ix >= 0x3ff00000) {
+    if (((ix - 0x3ff00000) | (int32_t)(uint32_t)bx) == 0) return x * pio2_hi + x * pio2_lo;
+    return (x - x) / (x - x);
+  }
+  if (ix < 0x3fe00000) {                  /* |x| < 0.5 */
+    if (ix < 0x3e400000) return x;        /* |x| < 2^-27 */
+    double t = x * x;
+    double p = t * (pS0 + t * (pS1 + t * (pS2 + t * (pS3 + t * (pS4 + t * pS5)))));
+    double q = 1.0 + t * (qS1 + t * (qS2 + t * (qS3 + t * qS4)));
+    double w = p / q;
+    return x + x * w;
+  }
+  double w = 1.0 - fabs(x);
+  double t = w * 0.5;
+  double p = t * (pS0 + t * (pS1 + t * (pS2 + t * (pS3 + t * (pS4 + t * pS5)))));
+  double q = 1.0 + t * (qS1 + t * (qS2 + t * (qS3 + t * qS4)));
+  double sr = sqrt(t);
+  if (ix >= 0x3FEF3333) {                 /* |x| > 0.975 */
+    w = p / q;
+    t = pio2_hi - (2.0 * (sr + sr * w) - pio2_lo);
+  } else {
+    w = from_bits(to_bits(sr) & 0xffffffff00000000ull);
+    double c = (t - w * w) / (sr + w);
+    double r = p / q;
+    p = 2.0 * sr * r - (pio2_lo - 2.0 * c);
+    q = pio4_hi - 2.0 * w;
+    t = pio4_hi - (p - q);
+  }
+  return (hx > 0) ? t : -t;
+}
+
 double orc_normal(uint64_t seed, uint64_t env, uint32_t asset, uint64_t tick) {
   double z, ut;
   uint32_t b;
@@ -500,6 +559,105 @@ static void src_get_data(orc_batch *b, int e) {
         s->P[i] = y;
         break;
       }
+      case ORC_SRC_SIMPLETREND: { /* SimpleTrend::getData, DataSource.cpp:1322-1347 */
+        double y = s->P[i];
+        double z, u_trend;
+        uint32_t dbit;
+        orc_draw0(seed, genv, (uint32_t)i, tick, &z, &u_trend, &dbit);
+        if (s->trending[i]) {
+          y += y * s->dY[i] * (double)s->dir[i];
+          if (--s->tlen[i] == 0) s->trending[i] = 0;
+        } else if (u_trend < p[0]) {
+          double u_len, u_dy;
+          orc_uniform2(seed, genv, (uint32_t)i, 1, tick, &u_len, &u_dy);
+          s->trending[i] = 1;
+          s->dir[i] = dbit ? -1 : 1;
+          int32_t lo = (int32_t)p[1], hi = (int32_t)p[2];
+          int32_t len = lo + (int32_t)(u_len * (double)(hi - lo + 1));
+          if (len > hi) len = hi;
+          s->tlen[i] = len;
+          s->dY[i] = (p[6] - p[5]) * u_dy + p[5];
+        }
+        if (y <= .1) s->dir[i] = 1;
+        y += y * (z * p[3] + 0.0);
+        s->P[i] = (0.01 < y) ? y : 0.01;   /* std::max(0.01, y) */
+        break;
+      }
+      case ORC_SRC_TRENDYOU: { /* TrendyOU::getData, DataSource.cpp:1608-1640;
+                                  x = ouComponent, ouMean = trendComponent */
+        double z, u_trend;
+        uint32_t dbit;
+        orc_draw0(seed, genv, (uint32_t)i, tick, &z, &u_trend, &dbit);
+        double ou_noise = s->ouMean[i] * (z * p[7] + 0.0);
+        double ou_rev = p[6] * (-s->x[i]);
+        s->x[i] += ou_rev + ou_noise;
+        int32_t lo = (int32_t)p[1], hi = (int32_t)p[2];
+        if (s->trending[i]) {
+          double tc = s->ouMean[i];
+          tc += tc * (s->dY[i] * (double)s->dir[i]);
+          tc = (0.1 < tc) ? tc : 0.1;       /* std::max(0.1, .) */
+          if (tc <= .1) {                    /* floored: restart the up-trend */
+            double u_len, u_dy;
+            orc_uniform2(seed, genv, (uint32_t)i, 1, tick, &u_len, &u_dy);
+            s->dir[i] = 1;
+            s->trending[i] = 1;
+            int32_t len = lo + (int32_t)(u_len * (double)(hi - lo + 1));
+            s->tlen[i] = len > hi ? hi : len;
+          }
+          s->ouMean[i] = tc;
+          if (--s->tlen[i] == 0) s->trending[i] = 0;
+        } else if (u_trend < p[0]) {
+          double u_len, u_dy;
+          orc_uniform2(seed, genv, (uint32_t)i, 1, tick, &u_len, &u_dy);
+          s->trending[i] = 1;
+          s->dir[i] = dbit ? -1 : 1;
+          int32_t len = lo + (int32_t)(u_len * (double)(hi - lo + 1));
+          s->tlen[i] = len > hi ? hi : len;
+          s->dY[i] = (p[4] - p[3]) * u_dy + p[3];
+        }
+        s->P[i] = s->x[i] + s->ouMean[i];
+        break;
+      }
+      case ORC_SRC_GAUSSIAN: /* Gaussian::getData, DataSource.cpp:1108-1114 */
+        s->P[i] = orc_normal(seed, genv, (uint32_t)i, tick) * p[1] + p[0];
+        break;
+      case ORC_SRC_SAWTOOTH: { /* SawTooth::getData, DataSource.cpp:557-566 */
+        double noise = 0.0;
+        if (p[5] != 0.0) noise = orc_normal(seed, genv, (uint32_t)i, tick) * p[5] + 0.0;
+        double ip;
+        s->P[i] = noise + p[1] + p[2] * modf(s->x[i] * p[0], &ip);
+        s->x[i] += p[4];
+        break;
+      }
+      case ORC_SRC_TRIANGLE: { /* Triangle::getData, DataSource.cpp:568-577 */
+        double noise = 0.0;
+        if (p[5] != 0.0) noise = orc_normal(seed, genv, (uint32_t)i, tick) * p[5] + 0.0;
+        const double PI2 = 3.141592653589793238463 * 2;
+        s->P[i] = noise + p[1] + 4 * p[2] / PI2 * orc_asin(orc_sin(PI2 * s->x[i] / p[0]));
+        s->x[i] += p[4];
+        break;
+      }
+      case ORC_SRC_OUPAIR: { /* OUPair::getData, DataSource.cpp:1236-1244: both assets
+                                share mean (kept in ouMean of each; the mean's variate is
+                                keyed by the pair's first asset, counter slot 2) */
+        if (p[3] == 0.0) {
+          const uint32_t a0 = (uint32_t)i;
+          double zm, um;
+          uint32_t bm;
+          draw_slot(seed, genv, a0, 2, tick, &zm, &um, &bm);
+          double mean = s->ouMean[i];
+          mean += mean * (zm * p[2] + 0.0);
+          for (int j = 0; j < 2; ++j) {
+            const double *pj = b->src[i + j].p;
+            double zj = orc_normal(seed, genv, (uint32_t)(i + j), tick) * pj[1] + 0.0;
+            double x = s->P[i + j];
+            x += (pj[0] * (mean - x)) + mean * zj;
+            s->P[i + j] = x;
+            s->ouMean[i + j] = mean;
+          }
+        }
+        break;
+      }
       default: /* external replay: prices supplied via orc_set_prices */
         s->P[i] = b->ext[(size_t)e * b->A + i];
         break;
@@ -513,11 +671,24 @@ static void src_get_data(orc_batch *b, int e) {
 static void src_reset(orc_batch *b, int e) {
   orc_env *s = &b->envs[e];
   for (int i = 0; i < b->A; ++i) {
-    if (b->src[i].kind == ORC_SRC_TRENDOU) {
-      s->trending[i] = 0;
-      s->P[i] = b->src[i].p[5];
-      s->tlen[i] = 0;
-      s->ouMean[i] = b->src[i].p[5];
+    const double *p = b->src[i].p;
+    switch (b->src[i].kind) {
+      case ORC_SRC_TRENDOU:
+        s->trending[i] = 0;
+        s->P[i] = p[5];
+        s->tlen[i] = 0;
+        s->ouMean[i] = p[5];
+        break;
+      case ORC_SRC_SIMPLETREND: /* DataSource.cpp:1349-1356 */
+        s->P[i] = p[4]; s->trending[i] = 0; s->dir[i] = 1; s->tlen[i] = 0;
+        break;
+      case ORC_SRC_TRENDYOU:    /* DataSource.cpp:1642-1653 */
+        s->x[i] = 0.; s->ouMean[i] = p[5]; s->trending[i] = 0; s->P[i] = p[5]; s->tlen[i] = 0;
+        break;
+      case ORC_SRC_OUPAIR:      /* DataSource.cpp:1246-1250 */
+        s->P[i] = 10.; s->ouMean[i] = 10.;
+        break;
+      default: break;           /* Synth family, OU, Gaussian: no-op */
     }
   }
 }
@@ -534,6 +705,14 @@ static void src_init(orc_batch *b, int e) {
       case ORC_SRC_TRENDOU:                                             /* :1380-1400, quirk 1 fixed */
         s->P[i] = p[5]; s->ouMean[i] = p[5]; s->dir[i] = 1; s->tlen[i] = 0;
         s->dY[i] = 0.; s->trending[i] = 0; break;
+      case ORC_SRC_SIMPLETREND:                                         /* :1262-1276 */
+        s->P[i] = p[4]; s->tlen[i] = 0; s->dY[i] = 0.; s->trending[i] = 0; break;
+      case ORC_SRC_TRENDYOU:                                            /* :1528-1545, quirk 1 fixed */
+        s->P[i] = p[5]; s->ouMean[i] = p[5]; s->x[i] = 0.; s->tlen[i] = 0;
+        s->dY[i] = 0.; s->trending[i] = 0; break;
+      case ORC_SRC_GAUSSIAN: s->P[i] = p[0]; break;                     /* :1067 */
+      case ORC_SRC_SAWTOOTH: case ORC_SRC_TRIANGLE: s->x[i] = p[3]; s->P[i] = 0.0; break;
+      case ORC_SRC_OUPAIR: s->P[i] = 10.; s->ouMean[i] = 10.; break;   /* :1191-1196 */
       default: s->P[i] = 0.0; break;
     }
   }

@@ -36,7 +36,9 @@ enum { ORC_GREEN = 0, ORC_INSUFF_MARGIN = 1, ORC_MARGIN_CALL = 2, ORC_BLOWN_OUT 
 
 /* per-asset generator kinds */
 enum { ORC_SRC_EXTERNAL = 0, ORC_SRC_SINE = 1, ORC_SRC_OU = 2, ORC_SRC_TRENDOU = 3,
-       ORC_SRC_REPLAY = 4 /* HDFSourceSingle over in-memory arrays (all assets) */ };
+       ORC_SRC_REPLAY = 4 /* HDFSourceSingle over in-memory arrays (all assets) */,
+       ORC_SRC_SIMPLETREND = 5, ORC_SRC_TRENDYOU = 6, ORC_SRC_GAUSSIAN = 7,
+       ORC_SRC_SAWTOOTH = 8, ORC_SRC_TRIANGLE = 9, ORC_SRC_OUPAIR = 10 };
 
 /* reward shapers (nstep_buffer.py:378-408) */
 enum { ORC_SHAPER_NONE = 0, ORC_SHAPER_DSR = 1, ORC_SHAPER_DDR = 2, ORC_SHAPER_PPC = 3 };
@@ -57,6 +59,12 @@ enum { ORC_STEP_NONE = 0, ORC_STEP_UNITS = 1, ORC_STEP_SINGLE = 2 };
  *  OU      p = {mean, theta, phi}
  *  TRENDOU p = {trendProb, minPeriod, maxPeriod, dYMin, dYMax, start,
  *               theta, phi, noiseTrend, emaAlpha}
+ *  SIMPLETREND p = {trendProb, minPeriod, maxPeriod, noise, start, dYMin, dYMax}
+ *  TRENDYOU    p = as TRENDOU
+ *  GAUSSIAN    p = {mean, var (the normal's stddev argument)}
+ *  SAWTOOTH / TRIANGLE p = as SINE
+ *  OUPAIR      p = {theta, phi, noise, role}: role 0 / 1 = first / second
+ *              asset of the pair, adjacent in asset order
  */
 typedef struct {
   int32_t kind;
@@ -195,6 +203,7 @@ void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t ou
 double orc_log(double x);
 double orc_sin(double x);
 double orc_cos2pi(double u);
+double orc_asin(double x);
 double orc_normal(uint64_t seed, uint64_t env, uint32_t asset, uint64_t tick);
 void orc_draw0(uint64_t seed, uint64_t env, uint32_t asset, uint64_t tick, double *z, double *ut,
                uint32_t *dbit);

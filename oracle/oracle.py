@@ -20,7 +20,8 @@ BUILD = os.path.join(HERE, "_build")
 MAXA = 64
 
 GREEN, INSUFF_MARGIN, MARGIN_CALL, BLOWN_OUT = 0, 1, 2, 3
-SRC_EXTERNAL, SRC_SINE, SRC_OU, SRC_TRENDOU, SRC_REPLAY = 0, 1, 2, 3, 4
+(SRC_EXTERNAL, SRC_SINE, SRC_OU, SRC_TRENDOU, SRC_REPLAY, SRC_SIMPLETREND, SRC_TRENDYOU,
+ SRC_GAUSSIAN, SRC_SAWTOOTH, SRC_TRIANGLE, SRC_OUPAIR) = range(11)
 SHAPERS = {"none": 0, None: 0, "None": 0, "DSR": 1, "DDR": 2, "PPC": 3, "cosine": 3,
            "cosine_similarity": 3, "cosine_port_shaper": 3}
 REWARD_MODES = {"env_log": 0, "agent_sum": 1, "agent_per_asset": 2}
@@ -104,7 +105,7 @@ def lib(fast: bool = False):
             fn.argtypes = [P, C.c_int, C.c_int, P, C.c_double, P, P, P]
         L.orc_ppc.argtypes = [P, P, C.c_int, C.c_int, C.c_int, P, C.c_double, P, P]
         L.orc_philox4x32_10.argtypes = [P, P, P]
-        for fn in (L.orc_log, L.orc_sin, L.orc_cos2pi):
+        for fn in (L.orc_log, L.orc_sin, L.orc_cos2pi, L.orc_asin):
             fn.argtypes = [C.c_double]
             fn.restype = C.c_double
         L.orc_normal.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64]

@@ -36,3 +36,27 @@ def spec_from_sources(sources):
     from madigan_amd.config import SourceSpec
     return SourceSpec(kinds=[k for k, _ in sources], params=[list(map(float, p)) for _, p in sources],
                       assets=[f"a{i}" for i in range(len(sources))])
+
+
+# SURVEY 8f #4 generators (reference defaults, DataSource.cpp:1201, :1291-1293, :1079, :1578-1582)
+SIMPLETREND_P = [0.01, 20, 80, 0.01, 10.0, 0.001, 0.01]   # trendProb min max noise start dYMin dYMax
+
+
+def simpletrend_sources(A, params=None):
+    return [(O.SRC_SIMPLETREND, list(params or SIMPLETREND_P))] * A
+
+
+def trendyou_sources(A, params=None):
+    return [(O.SRC_TRENDYOU, list(params or [0.02, 10, 60, 0.001, 0.03, 5.0, 0.1, 0.02, 0.0, 0.1]))] * A
+
+
+def gaussian_sources(mean, var):
+    return [(O.SRC_GAUSSIAN, [m, v]) for m, v in zip(mean, var)]
+
+
+def oupair_sources(theta=0.015, phi=0.01, noise=0.03):
+    return [(O.SRC_OUPAIR, [theta, phi, noise, 0.0]), (O.SRC_OUPAIR, [theta, phi, noise, 1.0])]
+
+
+def wave_sources(kind, freq, mu, amp, phase, dX=0.01, noise=0.0):
+    return [(kind, [f, m, a, p, dX, noise]) for f, m, a, p in zip(freq, mu, amp, phase)]

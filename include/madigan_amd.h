@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MGN_ABI_VERSION 3
+#define MGN_ABI_VERSION 4
 #define MGN_MAX_ASSETS 64
 #define MGN_MAX_NSTEP 64
 
@@ -64,10 +64,17 @@ enum { MGN_SRC_EXTERNAL = 0, MGN_SRC_SINE = 1, MGN_SRC_OU = 2, MGN_SRC_TRENDOU =
        MGN_SRC_SIMPLETREND = 5, MGN_SRC_TRENDYOU = 6, MGN_SRC_GAUSSIAN = 7,
        MGN_SRC_SAWTOOTH = 8, MGN_SRC_TRIANGLE = 9, MGN_SRC_OUPAIR = 10 };
 
-enum { MGN_SHAPER_NONE = 0, MGN_SHAPER_DSR = 1, MGN_SHAPER_DDR = 2, MGN_SHAPER_PPC = 3 };
+/* reward shapers (nstep_buffer.py:378-408): DSR :30-98, DDR :101-169, PPC = cosine_port_shaper
+ * :182-204, SHARPE = sharpe_shaper :207-239, SORTINO_A/B = sortino_shaperA/B :242-312 */
+enum { MGN_SHAPER_NONE = 0, MGN_SHAPER_DSR = 1, MGN_SHAPER_DDR = 2, MGN_SHAPER_PPC = 3,
+       MGN_SHAPER_SHARPE = 4, MGN_SHAPER_SORTINO_A = 5, MGN_SHAPER_SORTINO_B = 6 };
 enum { MGN_REWARD_ENV_LOG = 0, MGN_REWARD_AGENT_SUM = 1, MGN_REWARD_AGENT_PER_ASSET = 2 };
 enum { MGN_NORM_NONE = 0, MGN_NORM_LOG = 1, MGN_NORM_LOOKBACK = 2,
-       MGN_NORM_STANDARD_NORMAL = 3, MGN_NORM_LOOKBACK_LOG = 4 };
+       MGN_NORM_STANDARD_NORMAL = 3, MGN_NORM_LOOKBACK_LOG = 4,
+       MGN_NORM_LOG_STANDARD_NORMAL = 5 /* log_standard_norm, preprocessor.py:95-107 */ };
+/* ring push transforms: StackerDiscretePairs' price[:, 0] / price[:, 1]
+ * (preprocessor.py:303-316) is row-wise, so it is applied once at push */
+enum { MGN_RING_PLAIN = 0, MGN_RING_PAIR_RATIO = 1 };
 /* step kinds: Env::step() / step(units) / step(assetIdx, units) */
 enum { MGN_STEP_NONE = 0, MGN_STEP_UNITS = 1, MGN_STEP_SINGLE = 2 };
 
@@ -117,6 +124,7 @@ typedef struct {
   int32_t n_feats;             /* F = State.price width: n_assets for the generators
                                   (0 = n_assets); the feature columns of a replay source */
   int32_t pad3_;
+  double sortino_exp;          /* sortino_shaperA/B exponent (shaper config "sortino_exp") */
 } mgn_config;
 
 /* Per-step outputs.  For mgn_step they are the handle's buffers (see views);
@@ -182,12 +190,18 @@ typedef struct {
 } mgn_replay_tape;
 
 /* Stand-alone StackerDiscrete ring (preprocessor.py:143-199), caller-owned
- * device memory: ring (N, W, n_price + n_port), ring_ts (N, W), head/len (N). */
+ * device memory: ring (N, W, n_price + n_port), ring_ts (N, W), head/len (N).
+ * transform: MGN_RING_* applied to the pushed price row (PAIR_RATIO: the
+ * pushed row has 2 columns, the ring stores n_price = 1).  out_stride /
+ * out_offset: row stride (0 = n_price) and first column of the gathered price
+ * in the caller's buffer, so the rings of a MultiStackerDiscrete
+ * (preprocessor.py:202-288) gather side by side into one (N, W, sum) array. */
 typedef struct {
-  int32_t n_envs, n_price, n_port, window, norm_type, pad_;
+  int32_t n_envs, n_price, n_port, window, norm_type, transform;
   double *ring;
   uint64_t *ring_ts;
   int32_t *head, *len;
+  int32_t out_stride, out_offset;
 } mgn_ring;
 
 typedef struct mgn_env mgn_env;
@@ -243,6 +257,10 @@ int mgn_ring_clear(const mgn_ring *ring, const uint8_t *mask_dev, void *stream);
 /* current_data: price (N,W,n_price) normalised, port (N,W,n_port), ts (N,W) */
 int mgn_ring_gather(const mgn_ring *ring, double *price_dev, double *port_dev, uint64_t *ts_dev,
                     void *stream);
+/* StackerDiscreteReturns.current_data's np.diff (preprocessor.py:319-327; numpy's
+ * default axis -1, i.e. across the price columns): out (rows, cols - 1) =
+ * in[:, 1:] - in[:, :-1] for a (rows, cols) device array */
+int mgn_feat_diff(const double *in_dev, double *out_dev, int64_t rows, int32_t cols, void *stream);
 /* Lane layout of the step kernels: assets held per lane (1, 2, 4, 8; 0 =
  * automatic, the default).  Results are bit-identical for every layout (the
  * canonical reduction tree does not depend on it); only speed changes. */

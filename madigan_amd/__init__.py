@@ -11,12 +11,14 @@ from .config import ConfigError, SourceSpec, replay_spec, spec_from_config
 from .env import (Asset, BatchedEnv, BrokerResponse, DataSourceTick, Env, EnvInfo, RiskInfo, State,
                   get_env_info, make_batched_env, make_env)
 from .hdf import HDFSourceSingle, write_hdf
-from .preprocessor import PreProcessor, StackerDiscrete, make_preprocessor
+from .preprocessor import (MultiStackerDiscrete, PreProcessor, StackerDiscrete, StackerDiscretePairs,
+                           StackerDiscreteReturns, make_preprocessor)
 
 __all__ = ["Asset", "BatchedEnv", "BrokerResponse", "ConfigError", "DataSourceTick", "Env",
            "EnvInfo", "HDFSourceSingle", "PreProcessor", "RiskInfo", "SourceSpec",
            "StackerDiscrete", "State", "get_env_info", "make_batched_env", "make_env",
-           "make_preprocessor", "replay_spec", "spec_from_config", "write_hdf"]
+           "make_preprocessor", "MultiStackerDiscrete", "StackerDiscretePairs",
+           "StackerDiscreteReturns", "replay_spec", "spec_from_config", "write_hdf"]
 
 
 def load_extension():

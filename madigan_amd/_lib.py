@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmadigan_hip.so")
 MAX_ASSETS = 64
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_NSTEP = 64
 
 # status codes -> the reference's exception types (DataTypes.h:36-46, pybind11)
@@ -21,9 +21,12 @@ OK, ERR_CONFIG, ERR_INDEX, ERR_LENGTH, ERR_DEVICE, ERR_ARG = range(6)
 GREEN, INSUFF_MARGIN, MARGIN_CALL, BLOWN_OUT = range(4)
 (SRC_EXTERNAL, SRC_SINE, SRC_OU, SRC_TRENDOU, SRC_REPLAY, SRC_SIMPLETREND, SRC_TRENDYOU, SRC_GAUSSIAN,
  SRC_SAWTOOTH, SRC_TRIANGLE, SRC_OUPAIR) = range(11)
-SHAPER_NONE, SHAPER_DSR, SHAPER_DDR, SHAPER_PPC = range(4)
+(SHAPER_NONE, SHAPER_DSR, SHAPER_DDR, SHAPER_PPC, SHAPER_SHARPE, SHAPER_SORTINO_A,
+ SHAPER_SORTINO_B) = range(7)
 REWARD_ENV_LOG, REWARD_AGENT_SUM, REWARD_AGENT_PER_ASSET = range(3)
-NORM_NONE, NORM_LOG, NORM_LOOKBACK, NORM_STANDARD_NORMAL, NORM_LOOKBACK_LOG = range(5)
+(NORM_NONE, NORM_LOG, NORM_LOOKBACK, NORM_STANDARD_NORMAL, NORM_LOOKBACK_LOG,
+ NORM_LOG_STANDARD_NORMAL) = range(6)
+RING_PLAIN, RING_PAIR_RATIO = range(2)
 STEP_NONE, STEP_UNITS, STEP_SINGLE = range(3)
 
 
@@ -46,7 +49,7 @@ class Config(C.Structure):
         ("window", C.c_int32), ("norm_type", C.c_int32), ("auto_reset", C.c_int32),
         ("action_atoms", C.c_int32), ("unit_size", C.c_double),
         ("nstep", C.c_int32), ("pad2_", C.c_int32), ("discount", C.c_double),
-        ("n_feats", C.c_int32), ("pad3_", C.c_int32),
+        ("n_feats", C.c_int32), ("pad3_", C.c_int32), ("sortino_exp", C.c_double),
     ]
 
 
@@ -78,9 +81,9 @@ class ReplayTape(C.Structure):
 
 class Ring(C.Structure):
     _fields_ = [("n_envs", C.c_int32), ("n_price", C.c_int32), ("n_port", C.c_int32),
-                ("window", C.c_int32), ("norm_type", C.c_int32), ("pad_", C.c_int32),
+                ("window", C.c_int32), ("norm_type", C.c_int32), ("transform", C.c_int32),
                 ("ring", C.c_void_p), ("ring_ts", C.c_void_p), ("head", C.c_void_p),
-                ("len", C.c_void_p)]
+                ("len", C.c_void_p), ("out_stride", C.c_int32), ("out_offset", C.c_int32)]
 
 
 SYMBOLS = {
@@ -107,6 +110,7 @@ SYMBOLS = {
     "mgn_ring_push": (C.c_int, [C.POINTER(Ring), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mgn_ring_clear": (C.c_int, [C.POINTER(Ring), C.c_void_p, C.c_void_p]),
     "mgn_ring_gather": (C.c_int, [C.POINTER(Ring), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mgn_feat_diff": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p]),
     "mgn_set_layout": (C.c_int, [C.c_void_p, C.c_int32]),
     "mgn_get_layout": (C.c_int, [C.c_void_p]),
     "mgn_set_ablation": (C.c_int, [C.c_void_p, C.c_int32]),

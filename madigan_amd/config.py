@@ -273,14 +273,20 @@ def spec_from_config(config: Any) -> SourceSpec:
     return _not_implemented(source_type)
 
 
+# NStepBuffer.make_reward_shaper (nstep_buffer.py:378-408): cosine aliases, the
+# sortino pair, DSR / DDR, any module-level shaper function by name
+# (sum_default, sharpe_shaper), and None
 SHAPER_CODES = {None: L.SHAPER_NONE, "None": L.SHAPER_NONE, "none": L.SHAPER_NONE,
+                "sum_default": L.SHAPER_NONE,
                 "DSR": L.SHAPER_DSR, "DDR": L.SHAPER_DDR, "PPC": L.SHAPER_PPC, "cosine": L.SHAPER_PPC,
-                "cosine_similarity": L.SHAPER_PPC, "cosine_port_shaper": L.SHAPER_PPC}
+                "cosine_similarity": L.SHAPER_PPC, "cosine_port_shaper": L.SHAPER_PPC,
+                "sharpe_shaper": L.SHAPER_SHARPE, "sortino_shaperA": L.SHAPER_SORTINO_A,
+                "sortino_shaperB": L.SHAPER_SORTINO_B}
 REWARD_MODES = {"env_log": L.REWARD_ENV_LOG, "agent_sum": L.REWARD_AGENT_SUM,
                 "agent_per_asset": L.REWARD_AGENT_PER_ASSET}
 NORM_CODES = {None: L.NORM_NONE, "none": L.NORM_NONE, "log": L.NORM_LOG,
               "lookback": L.NORM_LOOKBACK, "standard_normal": L.NORM_STANDARD_NORMAL,
-              "lookback_log": L.NORM_LOOKBACK_LOG}
+              "lookback_log": L.NORM_LOOKBACK_LOG, "log_standard_normal": L.NORM_LOG_STANDARD_NORMAL}
 
 
 def shaper_code(name) -> int:
@@ -305,7 +311,7 @@ def build_config(spec: SourceSpec, *, n_envs: int, init_cash: float = 1_000_000.
                  cosine_temp: float = 0.0, desired_portfolio=None, window: int = 0,
                  norm_type=None, auto_reset: bool = False, action_atoms: int = 3,
                  unit_size: float = 0.05, seed: int = 0, env_offset: int = 0,
-                 nstep_return: int = 1, discount: float = 0.99):
+                 nstep_return: int = 1, discount: float = 0.99, sortino_exp=None):
     A = spec.n_assets
     if A < 1 or A > L.MAX_ASSETS:
         raise ValueError(f"n_assets must be in [1, {L.MAX_ASSETS}], got {A}")
@@ -340,6 +346,12 @@ def build_config(spec: SourceSpec, *, n_envs: int, init_cash: float = 1_000_000.
     c.nstep = int(nstep_return)  # config.py:126 (Agent/Model spec)
     c.discount = float(discount)  # config.py:154
     c.n_feats = int(spec.n_feats) if spec.replay else 0
+    if c.shaper in (L.SHAPER_SORTINO_A, L.SHAPER_SORTINO_B):
+        if sortino_exp is None:  # shaper_config["sortino_exp"] (nstep_buffer.py:392)
+            raise KeyError("sortino_exp")
+        if not float(sortino_exp) > 0:
+            raise ConfigError(f"sortino_exp must be > 0, got {sortino_exp}")
+    c.sortino_exp = float(sortino_exp) if sortino_exp is not None else 2.0
     srcs = (L.AssetSource * A)()
     for i, (k, p) in enumerate(zip(spec.kinds, spec.params)):
         srcs[i].kind = k

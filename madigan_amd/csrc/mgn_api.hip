@@ -144,12 +144,19 @@ int validate(const mgn_config* c, const mgn_asset_source* s, std::string& msg) {
     return MGN_ERR_LENGTH;
   }
   if (c->window < 0) { msg = "window must be >= 0"; return MGN_ERR_CONFIG; }
-  if (c->shaper < 0 || c->shaper > MGN_SHAPER_PPC) { msg = "unknown reward shaper"; return MGN_ERR_CONFIG; }
+  if (c->shaper < 0 || c->shaper > MGN_SHAPER_SORTINO_B) { msg = "unknown reward shaper"; return MGN_ERR_CONFIG; }
   if (c->reward_mode < 0 || c->reward_mode > MGN_REWARD_AGENT_PER_ASSET) {
     msg = "unknown reward_mode";
     return MGN_ERR_CONFIG;
   }
-  if (c->norm_type < 0 || c->norm_type > MGN_NORM_LOOKBACK_LOG) { msg = "unknown norm_type"; return MGN_ERR_CONFIG; }
+  if (c->norm_type < 0 || c->norm_type > MGN_NORM_LOG_STANDARD_NORMAL) {
+    msg = "unknown norm_type";
+    return MGN_ERR_CONFIG;
+  }
+  if (c->shaper >= MGN_SHAPER_SORTINO_A && !(c->sortino_exp > 0.)) {
+    msg = "sortino_exp must be > 0";
+    return MGN_ERR_CONFIG;
+  }
   if (c->nstep < 1 || c->nstep > MGN_MAX_NSTEP) {
     msg = "nstep_return must be in [1, 64]";
     return MGN_ERR_CONFIG;
@@ -202,6 +209,7 @@ mgn::KParams kparams(const mgn_env* e) {
   p.shaper = c.shaper; p.reward_mode = c.reward_mode; p.auto_reset = c.auto_reset;
   p.atoms = c.action_atoms; p.eta = c.adaptation_rate; p.cos_temp = c.cosine_temp;
   p.unit_size = c.unit_size;
+  p.sexp = c.sortino_exp;
   p.ablate = e->ablate;
   p.reqm_one = (c.required_margin == 1.0) ? 1 : 0;
   const mgn_views& v = e->v;
@@ -262,6 +270,7 @@ mgn::RingDesc ring_desc(const mgn_env* e) {
   mgn::RingDesc r;
   r.N = e->N; r.F = e->F; r.Pn = e->A + 1; r.W = e->W; r.norm = e->cfg.norm_type;
   r.prelog = e->cfg.norm_type == MGN_NORM_LOG;  // the step kernel logs at push
+  r.transform = MGN_RING_PLAIN; r.ostride = e->F; r.ooff = 0;
   r.ring = e->v.ring; r.ring_ts = e->v.ring_ts; r.head = e->v.ring_head; r.len = e->v.ring_len;
   return r;
 }
@@ -272,7 +281,8 @@ mgn::RingDesc ring_desc(const mgn_env* e) {
 void launch_gather(const mgn::RingDesc& r, double* price, double* port, uint64_t* ts,
                    hipStream_t stream) {
   const int C = r.F + r.Pn;
-  if (r.norm == MGN_NORM_STANDARD_NORMAL) {
+  if (r.norm == MGN_NORM_STANDARD_NORMAL || r.norm == MGN_NORM_LOG_STANDARD_NORMAL ||
+      r.ostride != r.F || r.ooff != 0) {
     const int64_t threads = (int64_t)r.N * C;
     hipLaunchKernelGGL(mgn::k_ring_gather, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
                        stream, r, price, port, ts);
@@ -537,6 +547,9 @@ static mgn::RingDesc ring_from(const mgn_ring* r) {
   mgn::RingDesc d;
   d.N = r->n_envs; d.F = r->n_price; d.Pn = r->n_port; d.W = r->window; d.norm = r->norm_type;
   d.prelog = 0;
+  d.transform = r->transform;
+  d.ostride = r->out_stride > 0 ? r->out_stride : r->n_price;
+  d.ooff = r->out_offset;
   d.ring = r->ring; d.ring_ts = r->ring_ts; d.head = r->head; d.len = r->len;
   return d;
 }
@@ -545,7 +558,12 @@ static int ring_ok(const mgn_ring* r) {
   if (!r || !r->ring || !r->ring_ts || !r->head || !r->len) return fail(nullptr, MGN_ERR_ARG, "null ring buffers");
   if (r->n_envs < 1 || r->window < 1 || r->n_price < 0 || r->n_port < 0)
     return fail(nullptr, MGN_ERR_LENGTH, "bad ring dimensions");
-  if (r->norm_type < 0 || r->norm_type > MGN_NORM_LOOKBACK_LOG) return fail(nullptr, MGN_ERR_CONFIG, "unknown norm_type");
+  if (r->norm_type < 0 || r->norm_type > MGN_NORM_LOG_STANDARD_NORMAL)
+    return fail(nullptr, MGN_ERR_CONFIG, "unknown norm_type");
+  if (r->transform != MGN_RING_PLAIN && !(r->transform == MGN_RING_PAIR_RATIO && r->n_price == 1))
+    return fail(nullptr, MGN_ERR_CONFIG, "ring transform PAIR_RATIO stores one price column");
+  if (r->out_offset < 0 || (r->out_stride > 0 && r->out_offset + r->n_price > r->out_stride))
+    return fail(nullptr, MGN_ERR_LENGTH, "gathered price columns exceed out_stride");
   return MGN_OK;
 }
 
@@ -571,6 +589,16 @@ int mgn_ring_gather(const mgn_ring* r, double* price_dev, double* port_dev, uint
   if (rc != MGN_OK) return rc;
   launch_gather(ring_from(r), price_dev, port_dev, ts_dev, (hipStream_t)stream);
   return check_hip(nullptr, hipGetLastError(), "mgn_ring_gather");
+}
+
+int mgn_feat_diff(const double* in_dev, double* out_dev, int64_t rows, int32_t cols, void* stream) {
+  if (!in_dev || !out_dev) return fail(nullptr, MGN_ERR_ARG, "null buffers");
+  if (rows < 0 || cols < 1) return fail(nullptr, MGN_ERR_LENGTH, "bad diff dimensions");
+  const int64_t n = rows * (int64_t)(cols - 1);
+  if (n == 0) return MGN_OK;
+  hipLaunchKernelGGL(mgn::k_feat_diff, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, in_dev, out_dev, rows, (int)cols);
+  return check_hip(nullptr, hipGetLastError(), "mgn_feat_diff");
 }
 
 int mgn_set_layout(mgn_env* e, int32_t assets_per_lane) {

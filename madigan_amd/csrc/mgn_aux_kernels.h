@@ -12,6 +12,8 @@ namespace mgn {
 struct RingDesc {
   int N, F, Pn, W, norm;
   int prelog;  // norm "log" already applied to the price columns at push
+  int transform;  // MGN_RING_PAIR_RATIO: pushed price rows have 2 columns, stored p0 / p1
+  int ostride, ooff;  // gathered price: row stride and first column in the output
   double* ring;
   uint64_t* ring_ts;
   int32_t* head;
@@ -26,9 +28,13 @@ __global__ void k_ring_push(RingDesc r, const double* __restrict__ price,
   const int C = r.F + r.Pn;
   const int h = (r.head[env] + 1) % r.W;
   double* row = r.ring + ((size_t)env * r.W + h) * C;
-  for (int c = 0; c < r.F; ++c) {
-    const double v = price ? price[(size_t)env * r.F + c] : 0.;
-    row[c] = r.prelog ? log_norm(v) : v;
+  if (r.transform == MGN_RING_PAIR_RATIO) {  // (price[:, 0] / price[:, 1]), preprocessor.py:311
+    row[0] = price ? price[(size_t)env * 2] / price[(size_t)env * 2 + 1] : 0.;
+  } else {
+    for (int c = 0; c < r.F; ++c) {
+      const double v = price ? price[(size_t)env * r.F + c] : 0.;
+      row[c] = r.prelog ? log_norm(v) : v;
+    }
   }
   for (int c = 0; c < r.Pn; ++c) row[r.F + c] = port ? port[(size_t)env * r.Pn + c] : 0.;
   r.ring_ts[(size_t)env * r.W + h] = ts ? ts[env] : 0;
@@ -45,7 +51,15 @@ __global__ void k_ring_clear(RingDesc r, const uint8_t* __restrict__ mask) {
 }
 
 // current_data: one thread per (env, column); rows oldest -> newest, norm on
-// price columns (log_norm :79-81, lookback :63-66, standard_norm :83-92).
+// price columns (log_norm :79-81, lookback :63-66, standard_norm :83-92,
+// log_standard_norm :95-107: log without the clamp, nan-skipping mean / std).
+__device__ __forceinline__ double nan_to_num(double v) {
+  if (v != v) return 0.;
+  if (v == __builtin_inf()) return 1.7976931348623157e308;
+  if (v == -__builtin_inf()) return -1.7976931348623157e308;
+  return v;
+}
+
 __global__ __launch_bounds__(BLOCK) void k_ring_gather(RingDesc r, double* __restrict__ price_out,
                                                        double* __restrict__ port_out,
                                                        uint64_t* __restrict__ ts_out) {
@@ -70,8 +84,29 @@ __global__ __launch_bounds__(BLOCK) void k_ring_gather(RingDesc r, double* __res
     for (int w = 0; w < W; ++w)
       ts_out[(size_t)env * W + w] = (w < len) ? r.ring_ts[(size_t)env * W + row_of(w)] : 0;
   if (!price_out) return;
-  double* o = price_out + (size_t)env * W * r.F + c;
+  double* o = price_out + (size_t)env * W * r.ostride + r.ooff + c;
   const int nt = r.norm;
+  if (nt == MGN_NORM_LOG_STANDARD_NORMAL) {
+    // np.nanmean / np.nanstd over the window of log(x); log of x <= 0 is nan / -inf
+    double sum = 0.;
+    int cnt = 0;
+    for (int w = 0; w < len; ++w) {
+      const double x = log(base[(size_t)row_of(w) * C + c]);
+      if (x == x) { sum += x; cnt += 1; }
+    }
+    const double mean = sum / cnt;
+    double ss = 0.;
+    for (int w = 0; w < len; ++w) {
+      const double x = log(base[(size_t)row_of(w) * C + c]);
+      if (x == x) { const double d = x - mean; ss += d * d; }
+    }
+    const double sd = sqrt(ss / cnt);
+    for (int w = 0; w < W; ++w) {
+      const double x = (w < len) ? log(base[(size_t)row_of(w) * C + c]) : 0.;
+      o[(size_t)w * r.ostride] = (w < len) ? nan_to_num((x - mean) / sd) : 0.;
+    }
+    return;
+  }
   if (nt == MGN_NORM_STANDARD_NORMAL) {
     double sum = 0.;
     for (int w = 0; w < len; ++w) sum += base[(size_t)row_of(w) * C + c];
@@ -84,13 +119,8 @@ __global__ __launch_bounds__(BLOCK) void k_ring_gather(RingDesc r, double* __res
     const double sd = sqrt(ss / len);
     for (int w = 0; w < W; ++w) {
       double v = 0.;
-      if (w < len) {
-        v = (base[(size_t)row_of(w) * C + c] - mean) / sd;
-        if (v != v) v = 0.;
-        else if (v == __builtin_inf()) v = 1.7976931348623157e308;
-        else if (v == -__builtin_inf()) v = -1.7976931348623157e308;
-      }
-      o[(size_t)w * r.F] = v;
+      if (w < len) v = nan_to_num((base[(size_t)row_of(w) * C + c] - mean) / sd);
+      o[(size_t)w * r.ostride] = v;
     }
     return;
   }
@@ -103,7 +133,7 @@ __global__ __launch_bounds__(BLOCK) void k_ring_gather(RingDesc r, double* __res
       else if (nt == MGN_NORM_LOOKBACK) v = v / last;
       else if (nt == MGN_NORM_LOOKBACK_LOG) v = log(v / last);
     }
-    o[(size_t)w * r.F] = v;
+    o[(size_t)w * r.ostride] = v;
   }
 }
 
@@ -183,6 +213,18 @@ __global__ __launch_bounds__(BLOCK) void k_ring_gather_elem(RingDesc r, double* 
       }
     }
   }
+}
+
+// StackerDiscreteReturns' np.diff along the last axis: out (rows, cols-1)
+__global__ __launch_bounds__(BLOCK) void k_feat_diff(const double* __restrict__ in,
+                                                     double* __restrict__ out, int64_t rows,
+                                                     int cols) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int co = cols - 1;
+  if (gid >= rows * co) return;
+  const int64_t rw = gid / co;
+  const int c = (int)(gid % co);
+  out[gid] = in[rw * cols + c + 1] - in[rw * cols + c];
 }
 
 // Philox discrete actions U{0..atoms-1}: counter (k, env, asset, 0xAC7)

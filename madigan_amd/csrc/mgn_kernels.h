@@ -37,6 +37,7 @@ struct KParams {
   int reqm_one;  // required_margin == 1.0
   int ablate;  // diagnostic timing builds only (mgn_set_ablation); 0 in every real run
   double eta, cos_temp, unit_size;
+  double sexp;  // sortino_shaperA/B exponent
   // state
   double *L, *mep, *Bm, *P, *sx, *oum, *dy;
   int32_t *tlen;
@@ -865,9 +866,66 @@ __device__ __forceinline__ double ddr_one(double r, double A, double B) {
 }
 __device__ __forceinline__ double clip1(double v) { return v < -1. ? -1. : (v > 1. ? 1. : v); }
 
+// naive shapers (nstep_buffer.py:207-312), benchmark 0.  x**e and x**(1/e) as
+// numpy evaluates them on float64 arrays: exponents 2 and 0.5 take numpy's
+// square / sqrt fast paths, others pow (the oracle makes the same split).
+__device__ __forceinline__ double pow_e(double x, double e) { return e == 2.0 ? x * x : pow(x, e); }
+__device__ __forceinline__ double root_e(double x, double e) {
+  return e == 2.0 ? sqrt(x) : pow(x, 1.0 / e);
+}
+__device__ __forceinline__ double max_m1(double x) { return (x < -1.) ? -1. : x; }          // clip(x, -1, None)
+__device__ __forceinline__ double min_0(double x) { return (x < 0. || x != x) ? x : 0.; }  // minimum(x, 0.)
+
+// the len(nstep_buffer) == 1 heuristics (:212-216, :244-249, :286-291)
+__device__ __noinline__ double naive1(int shaper, double r, double ex) {
+  double diff = r - 0.;
+  if (shaper == MGN_SHAPER_SHARPE) {  // no clip; r == 0 gives 0/0 = nan as in the reference
+    diff = (diff != 0.) ? diff : 0.;
+    return diff / sqrt(diff * diff);
+  }
+  if (shaper == MGN_SHAPER_SORTINO_A) {
+    const double downside = root_e(pow_e(fabs(diff), ex), ex);
+    return clip1(0.1 * ((diff != 0.) ? diff / downside : 0.));
+  }
+  diff = max_m1(diff);
+  diff = (diff < 0.) ? -root_e(-diff, ex) : diff;
+  return clip1(diff);
+}
+
+// L > 1 entries r_k = ring[(head + k) % n][d], diffs_k = (r_k - 0.) * gamma^k
+// (sharpe :217-239, sortino_shaperA :251-272, sortino_shaperB :293-312)
+__device__ __noinline__ double naive_n(int shaper, const double* ring, int n, int D, int d, int head,
+                                       int len, const double* disc, double ex) {
+  double s = 0., s2 = 0.;
+  for (int k = 0; k < len; ++k) {
+    const double x = (ring[(size_t)((head + k) % n) * D + d] - 0.) * disc[k];
+    if (shaper == MGN_SHAPER_SHARPE) {
+      s += x;
+      s2 += x * x;
+    } else if (shaper == MGN_SHAPER_SORTINO_A) {
+      s += x;
+      const double down = max_m1(min_0(x));
+      s2 += root_e(pow_e(fabs(down), ex) / (len - 1), ex);
+    } else {
+      const double v = max_m1(x);
+      s += (v < 0.) ? -root_e(-v, ex) : v;
+    }
+  }
+  if (shaper == MGN_SHAPER_SHARPE) {
+    const double num = s / len;
+    const double denom = sqrt(s2 / (len - 1));
+    return clip1(.1 * ((denom != 0.) ? num / denom : 0.));
+  }
+  if (shaper == MGN_SHAPER_SORTINO_A) {
+    const double num = s / len;
+    return (s2 != 0.) ? clip1(.1 * (num / s2)) : ((num == 0.) ? 0. : 1.);
+  }
+  return clip1(s);
+}
+
 // one shaper evaluation + parameter update, n = 1 (nstep_buffer.py:62-91, :128-162)
 __device__ __forceinline__ double shape(int shaper, double r, double& A, double& B, double eta,
-                                        double cos_term) {
+                                        double cos_term, double ex) {
   if (shaper == MGN_SHAPER_DSR) {
     const double out = clip1((0.0 + 1.0 * dsr_one(r, A, B)) / 1);
     A += eta * (r - A);
@@ -883,6 +941,7 @@ __device__ __forceinline__ double shape(int shaper, double r, double& A, double&
     return out;
   }
   if (shaper == MGN_SHAPER_PPC) return 1.0 * (r + cos_term);
+  if (shaper >= MGN_SHAPER_SHARPE) return naive1(shaper, r, ex);
   return r;
 }
 
@@ -902,8 +961,19 @@ __device__ __forceinline__ void nstep_column(const KParams& p, double* out, int 
   ring[(size_t)((head + len) % n) * D + d] = v;
   len += 1;
   const bool sr = p.shaper == MGN_SHAPER_DSR || p.shaper == MGN_SHAPER_DDR;
+  const bool naive = p.shaper >= MGN_SHAPER_SHARPE;
   int pops = 0;
   while (len >= n || (done && len > 0)) {
+    if (naive) {
+      const double res = (len == 1) ? naive1(p.shaper, ring[(size_t)head * D + d], p.sexp)
+                                    : naive_n(p.shaper, ring, n, D, d, head, len, p.disc, p.sexp);
+      if (out) out[(size_t)pops * D + d] = res;
+      head = (head + 1) % n;
+      len -= 1;
+      pops += 1;
+      if (!done && len < n) break;
+      continue;
+    }
     double acc = 0.0;
     for (int k = 0; k < len; ++k) {
       const double r = ring[(size_t)((head + k) % n) * D + d];
@@ -1162,11 +1232,11 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
       if (D == 1) rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
       if constexpr (!NST) {
         if (D == 1) {
-          shaped_s = shape(p.shaper, rin_s, shA[0], shB[0], p.eta, cos_term);
+          shaped_s = shape(p.shaper, rin_s, shA[0], shB[0], p.eta, cos_term, p.sexp);
         } else {
 #pragma unroll
           for (int m = 0; m < M; ++m)
-            shaped_v[m] = s.valid[m] ? shape(p.shaper, ar[m], shA[m], shB[m], p.eta, cos_term) : 0.;
+            shaped_v[m] = s.valid[m] ? shape(p.shaper, ar[m], shA[m], shB[m], p.eta, cos_term, p.sexp) : 0.;
         }
       } else {
         // NStepBuffer add + pops (replay_buffer.py:68-80); every lane tracks the

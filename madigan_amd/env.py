@@ -127,7 +127,7 @@ class BatchedEnv:
                  desired_portfolio=None, window: int = 0, norm_type=None,
                  auto_reset: bool = False, action_atoms: int = 3, unit_size: float = 0.05,
                  nstep_return: int = 1, discount: float = 0.99, replay_tape: Optional[dict] = None,
-                 replay_stride: int = 0):
+                 replay_stride: int = 0, sortino_exp=None):
         """A replay spec (``config.replay_spec`` / HDFSourceSingle) reads its
         prices, features and timestamps from a device replay tape: staged from
         the spec's HDF file (``spec.hdf``, cache_size chunks, pinned
@@ -150,7 +150,8 @@ class BatchedEnv:
             reward_mode=reward_mode, adaptation_rate=adaptation_rate, cosine_temp=cosine_temp,
             desired_portfolio=desired_portfolio, window=window, norm_type=norm_type,
             auto_reset=auto_reset, action_atoms=action_atoms, unit_size=unit_size, seed=seed,
-            env_offset=env_offset, nstep_return=nstep_return, discount=discount)
+            env_offset=env_offset, nstep_return=nstep_return, discount=discount,
+            sortino_exp=sortino_exp)
         self.N = int(n_envs)
         self.A = spec.n_assets
         self.F = int(spec.n_feats) if spec.replay else self.A
@@ -902,6 +903,7 @@ def make_batched_env(config, n_envs: int, **kw) -> BatchedEnv:
         transaction_cost_abs=_cfg_get(config, "transaction_cost_abs", 0.0),
         reward_shaper=shaper, adaptation_rate=_cfg_get(rconf, "adaptation_rate", 0.001),
         cosine_temp=_cfg_get(rconf, "cosine_temp", 0.0),
+        sortino_exp=_cfg_get(rconf, "sortino_exp", None),
         desired_portfolio=_cfg_get(rconf, "desired_portfolio", None) if shaper in (
             "cosine", "cosine_similarity", "cosine_port_shaper") else None,
         window=window, norm_type=norm_type, nstep_return=nstep, discount=discount,

@@ -842,6 +842,69 @@ void orc_ppc(const double *rewards, const double *ports, int L, int D, int P, co
   }
 }
 
+/* ---- naive n-step shapers (nstep_buffer.py:207-312), benchmark = 0. -------- */
+
+/* x**e and x**(1/e) as numpy evaluates them on float64 arrays: the scalar
+ * exponents 2 and 0.5 take numpy's square / sqrt fast paths (equal to the
+ * correctly rounded pow); other exponents go through pow. */
+static double pow_e(double x, double e) { return e == 2.0 ? x * x : pow(x, e); }
+static double root_e(double x, double e) { return e == 2.0 ? sqrt(x) : pow(x, 1.0 / e); }
+static double max_m1(double x) { return (x < -1.) ? -1. : x; }           /* np.clip(x, -1, None) */
+static double min_0(double x) { return (x < 0. || x != x) ? x : 0.; }   /* np.minimum(x, 0.) */
+
+void orc_naive(int shaper, const double *rewards, int L, int D, const double *discounts,
+               double ex, double *out) {
+  for (int d = 0; d < D; ++d) {
+    if (L == 1) {  /* the len(nstep_buffer) == 1 heuristics */
+      double diff = rewards[d] - 0.;
+      if (shaper == ORC_SHAPER_SHARPE) {                     /* :212-216 (no clip; r = 0 -> nan) */
+        diff = (diff != 0.) ? diff : 0.;
+        out[d] = diff / sqrt(diff * diff);
+      } else if (shaper == ORC_SHAPER_SORTINO_A) {           /* :244-249 */
+        double downside = root_e(pow_e(fabs(diff), ex), ex);
+        out[d] = clip1(0.1 * ((diff != 0.) ? diff / downside : 0.));
+      } else {                                               /* sortino_shaperB :286-291 */
+        diff = max_m1(diff);
+        diff = (diff < 0.) ? -root_e(-diff, ex) : diff;
+        out[d] = clip1(diff);
+      }
+      continue;
+    }
+    double diffs[ORC_MAX_NSTEP];
+    for (int k = 0; k < L; ++k) diffs[k] = (rewards[(size_t)k * D + d] - 0.) * discounts[k];
+    if (shaper == ORC_SHAPER_SHARPE) {                       /* :217-239 */
+      double s = 0., s2 = 0.;
+      for (int k = 0; k < L; ++k) s += diffs[k];
+      for (int k = 0; k < L; ++k) s2 += diffs[k] * diffs[k];
+      double num = s / L;
+      double denom = sqrt(s2 / (L - 1));
+      double o = (denom != 0.) ? num / denom : 0.;           /* np.divide(..., where=denom != 0) */
+      out[d] = clip1(.1 * o);
+    } else if (shaper == ORC_SHAPER_SORTINO_A) {             /* :251-272 */
+      double s = 0., den = 0.;
+      for (int k = 0; k < L; ++k) s += diffs[k];
+      double num = s / L;
+      for (int k = 0; k < L; ++k) {
+        double down = max_m1(min_0(diffs[k]));
+        den += root_e(pow_e(fabs(down), ex) / (L - 1), ex);
+      }
+      out[d] = (den != 0.) ? clip1(.1 * (num / den)) : ((num == 0.) ? 0. : 1.);
+    } else {                                                 /* sortino_shaperB :293-312 */
+      double s = 0.;
+      for (int k = 0; k < L; ++k) {
+        double v = max_m1(diffs[k]);
+        s += (v < 0.) ? -root_e(-v, ex) : v;
+      }
+      out[d] = clip1(s);
+    }
+  }
+}
+
+static int is_naive(int shaper) {
+  return shaper == ORC_SHAPER_SHARPE || shaper == ORC_SHAPER_SORTINO_A ||
+         shaper == ORC_SHAPER_SORTINO_B;
+}
+
 /* ---- public API ---------------------------------------------------------- */
 
 orc_batch *orc_create(const orc_config *cfg, const orc_asset_src *srcs) {
@@ -979,6 +1042,7 @@ static int nstep_add(orc_batch *b, int e, int D, const double *rin, const double
     double *o = out + (size_t)pops * D;
     if (c->shaper == ORC_SHAPER_DSR) orc_dsr(ring, L, D, b->disc, c->adaptation_rate, s->sA, s->sB, o);
     else if (c->shaper == ORC_SHAPER_DDR) orc_ddr(ring, L, D, b->disc, c->adaptation_rate, s->sA, s->sB, o);
+    else if (is_naive(c->shaper)) orc_naive(c->shaper, ring, L, D, b->disc, c->sortino_exp, o);
     else {
       for (int d = 0; d < D; ++d) {
         double acc = 0.0;
@@ -1053,6 +1117,7 @@ static void step_one(orc_batch *b, int e, int kind, const double *units, int32_t
     const double one = 1.0;
     if (c->shaper == ORC_SHAPER_DSR) orc_dsr(rin, 1, D, &one, c->adaptation_rate, s->sA, s->sB, shaped);
     else if (c->shaper == ORC_SHAPER_DDR) orc_ddr(rin, 1, D, &one, c->adaptation_rate, s->sA, s->sB, shaped);
+    else if (is_naive(c->shaper)) orc_naive(c->shaper, rin, 1, D, &one, c->sortino_exp, shaped);
     else if (c->shaper == ORC_SHAPER_PPC) {  /* cosine_port_shaper :182-204 */
       double cs = cosine_sim(port, c->desired_portfolio, A + 1);
       for (int d = 0; d < D; ++d) shaped[d] = 1.0 * (rin[d] + c->cosine_temp * cs);
@@ -1343,6 +1408,29 @@ void orc_ring_gather(const orc_ring *r, double *price, double *port, uint64_t *t
         for (int w = 0; w < len; ++w) {
           double v = (xp[(size_t)w * F + i] - mean) / sd;
           if (v != v) v = 0.;                       /* np.nan_to_num */
+          else if (v == INFINITY) v = 1.7976931348623157e308;
+          else if (v == -INFINITY) v = -1.7976931348623157e308;
+          xp[(size_t)w * F + i] = v;
+        }
+      }
+    } else if (nt == ORC_NORM_LOG_STANDARD_NORMAL) { /* log_standard_norm :95-107 */
+      for (int i = 0; i < F; ++i) {
+        double sum = 0.;
+        int cnt = 0;                                /* np.nanmean / np.nanstd skip nan */
+        for (int w = 0; w < len; ++w) {
+          double x = log(xp[(size_t)w * F + i]);
+          if (x == x) { sum += x; cnt += 1; }
+        }
+        double mean = sum / cnt;
+        double ss = 0.;
+        for (int w = 0; w < len; ++w) {
+          double x = log(xp[(size_t)w * F + i]);
+          if (x == x) { double d = x - mean; ss += d * d; }
+        }
+        double sd = sqrt(ss / cnt);
+        for (int w = 0; w < len; ++w) {
+          double v = (log(xp[(size_t)w * F + i]) - mean) / sd;
+          if (v != v) v = 0.;
           else if (v == INFINITY) v = 1.7976931348623157e308;
           else if (v == -INFINITY) v = -1.7976931348623157e308;
           xp[(size_t)w * F + i] = v;

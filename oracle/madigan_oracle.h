@@ -41,14 +41,16 @@ enum { ORC_SRC_EXTERNAL = 0, ORC_SRC_SINE = 1, ORC_SRC_OU = 2, ORC_SRC_TRENDOU =
        ORC_SRC_SAWTOOTH = 8, ORC_SRC_TRIANGLE = 9, ORC_SRC_OUPAIR = 10 };
 
 /* reward shapers (nstep_buffer.py:378-408) */
-enum { ORC_SHAPER_NONE = 0, ORC_SHAPER_DSR = 1, ORC_SHAPER_DDR = 2, ORC_SHAPER_PPC = 3 };
+enum { ORC_SHAPER_NONE = 0, ORC_SHAPER_DSR = 1, ORC_SHAPER_DDR = 2, ORC_SHAPER_PPC = 3,
+       ORC_SHAPER_SHARPE = 4, ORC_SHAPER_SORTINO_A = 5, ORC_SHAPER_SORTINO_B = 6 };
 
 /* which raw reward feeds the shaper */
 enum { ORC_REWARD_ENV_LOG = 0, ORC_REWARD_AGENT_SUM = 1, ORC_REWARD_AGENT_PER_ASSET = 2 };
 
 /* StackerDiscrete normalisers (preprocessor.py:53-107) */
 enum { ORC_NORM_NONE = 0, ORC_NORM_LOG = 1, ORC_NORM_LOOKBACK = 2,
-       ORC_NORM_STANDARD_NORMAL = 3, ORC_NORM_LOOKBACK_LOG = 4 };
+       ORC_NORM_STANDARD_NORMAL = 3, ORC_NORM_LOOKBACK_LOG = 4,
+       ORC_NORM_LOG_STANDARD_NORMAL = 5 };
 
 /* step variants: Env.h:189-204 (none), :206-230 (units), :232-256 (single) */
 enum { ORC_STEP_NONE = 0, ORC_STEP_UNITS = 1, ORC_STEP_SINGLE = 2 };
@@ -97,6 +99,7 @@ typedef struct {
   double discount;             /* gamma of the n-step aggregation */
   int32_t n_feats;             /* State.price width (replay features); 0 = n_assets */
   int32_t pad3_;
+  double sortino_exp;          /* sortino_shaperA/B exponent (shaper config "sortino_exp") */
 } orc_config;
 
 /* Outputs of one step for all envs.  Any pointer may be NULL. */
@@ -197,6 +200,11 @@ void orc_ddr(const double *rewards, int L, int D, const double *discounts,
 
 void orc_ppc(const double *rewards, const double *ports, int L, int D, int P, const double *target,
              double temp, const double *discounts, double *out);
+
+/* sharpe_shaper / sortino_shaperA / sortino_shaperB (nstep_buffer.py:207-312),
+ * benchmark 0.: rewards (L, D) oldest first, out (D).  Stateless. */
+void orc_naive(int shaper, const double *rewards, int L, int D, const double *discounts,
+               double exp_, double *out);
 
 /* RNG + deterministic math shared (by specification) with the device path */
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

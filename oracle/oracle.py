@@ -22,10 +22,12 @@ MAXA = 64
 GREEN, INSUFF_MARGIN, MARGIN_CALL, BLOWN_OUT = 0, 1, 2, 3
 (SRC_EXTERNAL, SRC_SINE, SRC_OU, SRC_TRENDOU, SRC_REPLAY, SRC_SIMPLETREND, SRC_TRENDYOU,
  SRC_GAUSSIAN, SRC_SAWTOOTH, SRC_TRIANGLE, SRC_OUPAIR) = range(11)
-SHAPERS = {"none": 0, None: 0, "None": 0, "DSR": 1, "DDR": 2, "PPC": 3, "cosine": 3,
-           "cosine_similarity": 3, "cosine_port_shaper": 3}
+SHAPERS = {"none": 0, None: 0, "None": 0, "sum_default": 0, "DSR": 1, "DDR": 2, "PPC": 3,
+           "cosine": 3, "cosine_similarity": 3, "cosine_port_shaper": 3, "sharpe_shaper": 4,
+           "sortino_shaperA": 5, "sortino_shaperB": 6}
 REWARD_MODES = {"env_log": 0, "agent_sum": 1, "agent_per_asset": 2}
-NORMS = {None: 0, "none": 0, "log": 1, "lookback": 2, "standard_normal": 3, "lookback_log": 4}
+NORMS = {None: 0, "none": 0, "log": 1, "lookback": 2, "standard_normal": 3, "lookback_log": 4,
+         "log_standard_normal": 5}
 STEP_NONE, STEP_UNITS, STEP_SINGLE = 0, 1, 2
 
 F_LEDGER, F_MEP, F_BORROWED, F_PRICE, F_SINE_X, F_OU_MEAN, F_DY, F_TLEN, F_TRENDING, F_DIR, \
@@ -50,7 +52,7 @@ class Config(C.Structure):
         ("window", C.c_int32), ("norm_type", C.c_int32), ("auto_reset", C.c_int32),
         ("action_atoms", C.c_int32), ("unit_size", C.c_double),
         ("nstep", C.c_int32), ("pad2_", C.c_int32), ("discount", C.c_double),
-        ("n_feats", C.c_int32), ("pad3_", C.c_int32),
+        ("n_feats", C.c_int32), ("pad3_", C.c_int32), ("sortino_exp", C.c_double),
     ]
 
 
@@ -104,6 +106,7 @@ def lib(fast: bool = False):
         for fn in (L.orc_dsr, L.orc_ddr):
             fn.argtypes = [P, C.c_int, C.c_int, P, C.c_double, P, P, P]
         L.orc_ppc.argtypes = [P, P, C.c_int, C.c_int, C.c_int, P, C.c_double, P, P]
+        L.orc_naive.argtypes = [C.c_int, P, C.c_int, C.c_int, P, C.c_double, P]
         L.orc_philox4x32_10.argtypes = [P, P, P]
         for fn in (L.orc_log, L.orc_sin, L.orc_cos2pi, L.orc_asin):
             fn.argtypes = [C.c_double]
@@ -165,6 +168,7 @@ class OracleBatch:
         c.nstep = int(cfg.get("nstep_return", 1))              # config.py:126
         c.discount = float(cfg.get("discount", 0.99))          # config.py:154
         c.n_feats = int(cfg.get("n_feats", 0))
+        c.sortino_exp = float(cfg.get("sortino_exp", 2.0))
         self.cfg = c
         self.F = c.n_feats if (sources and sources[0][0] == SRC_REPLAY and c.n_feats) else self.A
         self.W = c.window
@@ -305,6 +309,16 @@ def dsr(rewards, discounts, eta, A, B, ddr=False):
     return out
 
 
+def naive(shaper, rewards, discounts, exp=2.0):
+    """sharpe_shaper / sortino_shaperA / sortino_shaperB over an (L, D) buffer."""
+    r = np.ascontiguousarray(rewards, dtype=np.float64)
+    L_, D = r.shape
+    d = np.ascontiguousarray(discounts, dtype=np.float64)
+    out = np.zeros(D)
+    lib().orc_naive(SHAPERS[shaper], _ptr(r), L_, D, _ptr(d), float(exp), _ptr(out))
+    return out
+
+
 def ppc(rewards, ports, target, temp, discounts):
     r = np.ascontiguousarray(rewards, dtype=np.float64)
     p = np.ascontiguousarray(ports, dtype=np.float64)
@@ -368,6 +382,52 @@ class Ring:
         ts = np.zeros((self.N, self.W), np.uint64)
         self.L.orc_ring_gather(C.byref(self.s), _ptr(price), _ptr(port), _ptr(ts))
         return price, port, ts
+
+
+# ---------------------------------------------------------------------------
+# StackerDiscrete variants (preprocessor.py:202-327) on top of Ring, N = 1.
+
+def pairs_row(price2):
+    """StackerDiscretePairs: (price[:, 0] / price[:, 1]) row-wise (:311)."""
+    p = np.asarray(price2, np.float64).reshape(-1)
+    return np.array([p[0] / p[1]])
+
+
+def returns_view(ring: "Ring"):
+    """StackerDiscreteReturns.current_data (:320-327) of env 0: normalised
+    window (len rows), np.diff along the last (feature) axis, portfolio and
+    timestamps without their first row."""
+    pr, po, ts = ring.gather()
+    n = int(ring.len[0])
+    return np.diff(pr[0, :n], axis=-1), po[0, 1:n], ts[0, 1:n].astype(np.int64)
+
+
+class MultiRing:
+    """MultiStackerDiscrete (:202-288), N = 1: a Ring per dilation fed every
+    d-th State by a countdown; price windows concatenated along the features,
+    portfolio / timestamps from the first dilation."""
+
+    def __init__(self, window, dilations, n_price, n_port, norm_type):
+        self.d = list(dilations)
+        self.cnt = [0] * len(self.d)
+        self.rings = [Ring(1, n_price, n_port, window, norm_type) for _ in self.d]
+
+    def push(self, price, port, ts):
+        for i, d in enumerate(self.d):
+            if self.cnt[i] == 0:
+                self.rings[i].push(price, port, ts)
+                self.cnt[i] = d - 1
+            else:
+                self.cnt[i] -= 1
+
+    def view(self):
+        lens = [int(r.len[0]) for r in self.rings]
+        if len(set(lens)) != 1:
+            return None  # np.concatenate raises ValueError
+        outs = [r.gather() for r in self.rings]
+        n = lens[0]
+        price = np.concatenate([o[0][0, :n] for o in outs], axis=-1)
+        return price, outs[0][1][0, :n], outs[0][2][0, :n].astype(np.int64)
 
 
 # ---------------------------------------------------------------------------

@@ -57,7 +57,14 @@ def shaper_vectors(nstep_buffer, data):
     from madigan.utils.data import SARSD, State
     rng = np.random.default_rng(20261015)
     cases = []
-    for shaper in ("DSR", "DDR", "cosine"):
+    # (shaper type, sortino_exp, case-key prefix); the naive shapers (sharpe_shaper,
+    # sortino_shaperA/B, nstep_buffer.py:207-312) follow the original three so the
+    # earlier cases keep their random draws
+    shapers = [("DSR", 2, "DSR"), ("DDR", 2, "DDR"), ("cosine", 2, "cosine"),
+               ("sharpe_shaper", 2, "sharpe"), ("sortino_shaperA", 2, "sortinoA"),
+               ("sortino_shaperB", 2, "sortinoB"), ("sortino_shaperA", 3, "sortinoA3"),
+               ("sortino_shaperB", 3, "sortinoB3")]
+    for shaper, sexp, prefix in shapers:
         for n in (1, 5, 20):
             for D in (1, 4):
                 T = 64
@@ -68,7 +75,8 @@ def shaper_vectors(nstep_buffer, data):
                 dones = np.zeros(T, bool)
                 dones[[17, 40]] = True                            # done-flush
                 cfg = {"reward_shaper": shaper, "adaptation_rate": 0.01,
-                       "desired_portfolio": list(np.linspace(1, 0, D + 1)), "cosine_temp": 0.05}
+                       "desired_portfolio": list(np.linspace(1, 0, D + 1)), "cosine_temp": 0.05,
+                       "sortino_exp": sexp}
                 nb = nstep_buffer.NStepBuffer(n, 0.99, cfg)
                 outs, out_steps = [], []
                 for t in range(T):
@@ -82,7 +90,9 @@ def shaper_vectors(nstep_buffer, data):
                         while len(nb) > 0:
                             outs.append(np.atleast_1d(np.asarray(nb.pop_nstep_sarsd().reward, float)))
                             out_steps.append(t)
-                key = f"{shaper}_n{n}_D{D}"
+                key = f"{prefix}_n{n}_D{D}"
+                data[key + "_shaper"] = np.array(shaper)
+                data[key + "_exp"] = np.array(float(sexp))
                 data[key + "_rewards"] = rewards
                 data[key + "_ports"] = ports
                 data[key + "_dones"] = dones
@@ -124,6 +134,86 @@ def window_vectors(preprocessor, data):
         data["win_none_raises"] = np.array(False)
     except NotImplementedError:
         data["win_none_raises"] = np.array(True)
+    # 'expanding' builds, but its lambda calls _expanding_mean(x) with one of
+    # two required arguments (preprocessor.py:73, :475): current_data raises TypeError
+    sd = preprocessor.StackerDiscrete(W, F, norm=True, norm_type="expanding")
+    sd.stream_state(State(prices[0], ports[0], 2))
+    try:
+        sd.current_data()
+        data["win_expanding_raises"] = np.array(False)
+    except TypeError:
+        data["win_expanding_raises"] = np.array(True)
+
+
+def stacker_variant_vectors(preprocessor, data):
+    """log_standard_normal, StackerDiscreteReturns, StackerDiscretePairs and
+    MultiStackerDiscrete (preprocessor.py:95-107, :202-327) over one stream."""
+    from madigan.utils.data import State
+    rng = np.random.default_rng(11)
+    T, F, W = 40, 3, 8
+    prices = 10 + np.cumsum(rng.normal(0, 0.3, (T, F)), axis=0)
+    prices[13, 0] = -0.5                     # log(x < 0) = nan: nanmean / nanstd skip it
+    ports = rng.normal(0, 0.3, (T, F + 1))
+    data["var_prices"] = prices
+    data["var_ports"] = ports
+    data["var_W"] = np.array(W)
+
+    def store(key, outs):
+        """outs: per step (price (r, c), port (r2, P), ts (r2,)); zero-padded to
+        (T, W, cmax) / (T, W, P) / (T, W) with the row and column counts."""
+        cmax = max([o[0].shape[1] for o in outs if o[0].ndim == 2] + [1])
+        pr = np.zeros((T, W, cmax))
+        po = np.zeros((T, W, F + 1))
+        ts = np.zeros((T, W), np.int64)
+        shape = np.zeros((T, 3), np.int64)   # price rows, price cols, port/ts rows
+        for t, (p, q, s) in enumerate(outs):
+            p = p.reshape(p.shape[0], -1) if p.size else np.zeros((0, 0))
+            pr[t, :p.shape[0], :p.shape[1]] = p
+            po[t, :q.shape[0], :q.shape[1]] = q.reshape(q.shape[0], -1) if q.size else 0
+            ts[t, :s.shape[0]] = s
+            shape[t] = (p.shape[0], p.shape[1], q.shape[0])
+        data[key + "_price"], data[key + "_port"], data[key + "_ts"] = pr, po, ts
+        data[key + "_shape"] = shape
+
+    def run(pp, feed, key):
+        outs = []
+        for t in range(T):
+            pp.stream_state(State(feed[t], ports[t], t + 2))
+            cur = pp.current_data()
+            outs.append((np.asarray(cur.price, float), np.asarray(cur.portfolio, float),
+                         np.asarray(cur.timestamp, np.int64)))
+        store(key, outs)
+
+    with np.errstate(all="ignore"):
+        run(preprocessor.StackerDiscrete(W, F, norm=True, norm_type="log_standard_normal"),
+            prices, "var_lsn")
+        for nt in ("log", "lookback", "standard_normal"):
+            run(preprocessor.StackerDiscreteReturns(W, F, norm=True, norm_type=nt), prices,
+                f"var_returns_{nt}")
+        for nt in ("lookback", "log"):
+            run(preprocessor.StackerDiscretePairs(W, 2, norm=True, norm_type=nt), prices[:, :2],
+                f"var_pairs_{nt}")
+    # MultiStackerDiscrete allocates its counters with np.int (numpy < 1.24, the
+    # reference pins 1.18.1); numpy 2 dropped the alias, so restore it for the run
+    if not hasattr(np, "int"):
+        np.int = int
+    dil = [1, 3, 4]
+    data["var_multi_dilations"] = np.array(dil)
+    for nt in ("lookback", "standard_normal"):
+        ms = preprocessor.MultiStackerDiscrete(W, dil, F, norm=True, norm_type=nt)
+        outs, ok = [], []
+        for t in range(T):
+            ms.stream_state(State(prices[t], ports[t], t + 2))
+            try:
+                cur = ms.current_data()
+                outs.append((np.asarray(cur.price, float), np.asarray(cur.portfolio, float),
+                             np.asarray(cur.timestamp, np.int64)))
+                ok.append(True)
+            except ValueError:  # dilation buffers of unequal length cannot be concatenated
+                outs.append((np.zeros((0, F * len(dil))), np.zeros((0, F + 1)), np.zeros(0, np.int64)))
+                ok.append(False)
+        data[f"var_multi_{nt}_ok"] = np.array(ok)
+        store(f"var_multi_{nt}", outs)
 
 
 def main():
@@ -133,6 +223,7 @@ def main():
     data = {"eps": np.array(float(nstep_buffer.EPS))}
     shaper_vectors(nstep_buffer, data)
     window_vectors(preprocessor, data)
+    stacker_variant_vectors(preprocessor, data)
     path = os.path.join(OUT, "reference_vectors.npz")
     np.savez_compressed(path, **data)
     print(f"wrote {path}: {len(data)} arrays")

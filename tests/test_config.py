@@ -3,7 +3,7 @@ DataSource constructors (keys, defaults, Composite, error types)."""
 import pytest
 
 from madigan_amd import _lib as L
-from madigan_amd.config import ConfigError, build_config, default_spec, spec_from_config
+from madigan_amd.config import ConfigError, build_config, default_spec, ou_spec, spec_from_config
 
 SYNTH = {"data_source_type": "Synth",
          "data_source_config": {"freq": [1., 0.3], "mu": [2., 2.1], "amp": [1., 1.2],
@@ -86,3 +86,38 @@ def test_build_config_fields():
         build_config(spec_from_config(OU), n_envs=1, reward_shaper="nope")
     with pytest.raises(ValueError):
         build_config(spec_from_config(OU), n_envs=1, desired_portfolio=[1., 0.])
+
+
+def test_make_preprocessor_dispatch_like_reference():
+    """make_preprocessor (preprocessor.py:28-50): StackerDiscreteReturns maps to
+    plain StackerDiscrete; Pairs / Multi dispatch by substring test."""
+    from madigan_amd import (MultiStackerDiscrete, StackerDiscrete, StackerDiscretePairs,
+                             make_preprocessor)
+    base = {"window_length": 8, "norm": True, "norm_type": "lookback"}
+    mk = lambda t, **kw: make_preprocessor({"preprocessor_type": t,
+                                            "preprocessor_config": {**base, **kw}}, 2)
+    assert type(mk("StackerDiscreteReturns")) is StackerDiscrete
+    assert type(mk("WindowedStacker")) is StackerDiscrete
+    assert type(mk("StackerDiscretePairs")) is StackerDiscretePairs
+    m = mk("MultiStackerDiscrete", dilations=[1, 4])
+    assert type(m) is MultiStackerDiscrete and m.feature_output_shape == (8, 4)
+    assert mk("StackerDiscretePairs").feature_output_shape == (8, 1)
+    with pytest.raises(NotImplementedError):
+        mk("RollerDiscrete")
+    with pytest.raises(NotImplementedError):
+        mk("StackerDiscrete", norm_type="bogus")
+    mk("StackerDiscrete", norm_type="expanding")  # builds; current_data raises TypeError
+    mk("StackerDiscrete", norm_type="log_standard_normal")
+
+
+def test_naive_shaper_config():
+    from madigan_amd.config import build_config, shaper_code
+    from madigan_amd import _lib as L
+    assert shaper_code("sharpe_shaper") == L.SHAPER_SHARPE
+    assert shaper_code("sortino_shaperB") == L.SHAPER_SORTINO_B
+    assert shaper_code("sum_default") == L.SHAPER_NONE
+    spec = ou_spec([1.0], [0.1], [0.1])
+    with pytest.raises(KeyError):
+        build_config(spec, n_envs=2, reward_shaper="sortino_shaperA")
+    c, _ = build_config(spec, n_envs=2, reward_shaper="sortino_shaperA", sortino_exp=3)
+    assert c.sortino_exp == 3.0 and c.shaper == L.SHAPER_SORTINO_A

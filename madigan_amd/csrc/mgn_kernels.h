@@ -632,27 +632,13 @@ struct Node {
   static constexpr int hi = lo + span;
 };
 
-// value of node K once leaves 0..R are decided (fin) and the rest are not (pre)
-template <int APAD, int K, int R>
-__device__ __forceinline__ double node_val(const double (&pre)[2 * APAD],
-                                           const double (&fin)[2 * APAD]) {
-  if constexpr (Node<APAD, K>::hi - 1 <= R) {
-    return fin[K];
-  } else if constexpr (Node<APAD, K>::lo > R) {
-    return pre[K];
-  } else {
-    return node_val<APAD, 2 * K, R>(pre, fin) + node_val<APAD, 2 * K + 1, R>(pre, fin);
-  }
-}
-
-// leaf R decided: finalize every ancestor whose last leaf is R
-template <int APAD, int K, int R>
-__device__ __forceinline__ void finalize_up(double (&fin)[2 * APAD]) {
+// leaf L of the heap tree changed: recompute its ancestors bottom-up (each node
+// the sum of its two children, the canonical order)
+template <int APAD, int K>
+__device__ __forceinline__ void update_up(double (&t)[2 * APAD]) {
   if constexpr (K >= 1) {
-    if constexpr (Node<APAD, K>::hi - 1 == R) {
-      fin[K] = fin[2 * K] + fin[2 * K + 1];
-      finalize_up<APAD, K / 2, R>(fin);
-    }
+    t[K] = t[2 * K] + t[2 * K + 1];
+    update_up<APAD, K / 2>(t);
   }
 }
 
@@ -688,30 +674,26 @@ __device__ __forceinline__ RoundIn load_round(const EnvRecs<APAD>& er, int i) {
 // (Broker.cpp:128-135, Portfolio.cpp:284-323) for round I; RQ1: required
 // margin == 1 (x / 1.0 == x, division skipped with identical bits).  The next
 // round's record is loaded before this round computes (LDS latency hidden),
-// and the logic is straight-line (no short-circuit branches).
+// and the logic is straight-line (no short-circuit branches).  t[q] is the
+// canonical tree of sum q over the current leaves: leaves < I hold their
+// decided values, leaves >= I their pre-order values, so t[q][1] is the sum
+// the reference's accessor recomputes before order I.
 template <int M, int S, bool RQ1, int I>
 struct XRounds {
   static constexpr int APAD = M * S;
   static __device__ __forceinline__ void run(const EnvRecs<APAD>& er, const RoundIn& r,
                                              const KParams& p, double& cash,
-                                             const double (&s0)[4], double (&pre)[4][2 * APAD],
-                                             double (&fin)[4][2 * APAD], bool (&go_own)[M],
+                                             double (&t)[4][2 * APAD], bool (&go_own)[M],
                                              int (&rk)[M], int& any_mc, int ls) {
     if constexpr (I < APAD) {
       RoundIn nxt;
       if constexpr (I + 1 < APAD) nxt = load_round<APAD>(er, I + 1);
       const double post[4] = {r.post01.x, r.post01.y, r.post23.x, r.post23.y};
-      double R[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if constexpr (I == 0) R[q] = s0[q];
-        else R[q] = node_val<APAD, 1, I - 1>(pre[q], fin[q]);
-      }
-      const double pnl = R[0] - R[1];
-      const double balance = cash + R[2];
+      const double pnl = t[0][1] - t[1][1];
+      const double balance = cash + t[2][1];
       const double bp = balance + pnl;
       const double availM = RQ1 ? bp : bp / p.reqM;
-      const double equity = (cash + R[0]) - R[3];
+      const double equity = (cash + t[0][1]) - t[3][1];
       const double mr = p.mainM * pnl;
       const int mc = (r.fl.y != 0) & ((equity <= -mr) | (bp <= -mr));
       const int insuff = (r.fl.z != 0) & ((availM <= r.ax1.x) | (balance <= 0.));
@@ -719,17 +701,22 @@ struct XRounds {
       any_mc |= (r.fl.x != 0) & mc;
       const double c4 = ((cash + r.ax1.y) - r.yz.x) - r.yz.y;
       cash = go ? c4 : cash;
+      if constexpr (I + 1 < APAD) {  // the last round's sums are recomputed by the caller
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        fin[q][APAD + I] = go ? post[q] : pre[q][APAD + I];
-        finalize_up<APAD, (APAD + I) / 2, I>(fin[q]);
+        for (int q = 0; q < 4; ++q) {
+          t[q][APAD + I] = go ? post[q] : t[q][APAD + I];
+          update_up<APAD, (APAD + I) / 2>(t[q]);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[q][APAD + I] = go ? post[q] : t[q][APAD + I];
       }
       const int risk = mc ? MGN_MARGIN_CALL : (insuff ? MGN_INSUFF_MARGIN : MGN_GREEN);
       const bool own = ls == I / M;
       go_own[I % M] = own ? (go != 0) : go_own[I % M];
       rk[I % M] = (own & (r.fl.x != 0)) ? risk : rk[I % M];
       if constexpr (I + 1 < APAD)
-        XRounds<M, S, RQ1, I + 1>::run(er, nxt, p, cash, s0, pre, fin, go_own, rk, any_mc, ls);
+        XRounds<M, S, RQ1, I + 1>::run(er, nxt, p, cash, t, go_own, rk, any_mc, ls);
     }
   }
 };
@@ -805,24 +792,27 @@ __device__ __forceinline__ void broker_x(Lane<M>& s, const KParams& p, EnvRecs<M
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-  double pre[4][2 * APAD], fin[4][2 * APAD];
+  double t[4][2 * APAD];
 #pragma unroll
   for (int a = 0; a < APAD; ++a) {
     const d2* rv = reinterpret_cast<const d2*>(&er.r[a]);
     const d2 p01 = rv[0], p23 = rv[1];
-    pre[0][APAD + a] = p01.x;
-    pre[1][APAD + a] = p01.y;
-    pre[2][APAD + a] = p23.x;
-    pre[3][APAD + a] = p23.y;
+    t[0][APAD + a] = p01.x;
+    t[1][APAD + a] = p01.y;
+    t[2][APAD + a] = p23.x;
+    t[3][APAD + a] = p23.y;
   }
+  // internal nodes over the pre-order leaves; the root equals the carried s0
 #pragma unroll
-  for (int q = 0; q < 4; ++q) build_pre<APAD, APAD - 1>(pre[q]);
-  const double s0a[4] = {s0.lp, s0.ml, s0.sh, s0.b};
+  for (int q = 0; q < 4; ++q) build_pre<APAD, APAD - 1>(t[q]);
+  t[0][1] = s0.lp;
+  t[1][1] = s0.ml;
+  t[2][1] = s0.sh;
+  t[3][1] = s0.b;
   bool go_own[M];
 #pragma unroll
   for (int m = 0; m < M; ++m) go_own[m] = false;
-  XRounds<M, S, RQ1, 0>::run(er, load_round<APAD>(er, 0), p, cash, s0a, pre, fin, go_own, rk,
-                             any_mc, ls);
+  XRounds<M, S, RQ1, 0>::run(er, load_round<APAD>(er, 0), p, cash, t, go_own, rk, any_mc, ls);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
 
@@ -836,10 +826,12 @@ __device__ __forceinline__ void broker_x(Lane<M>& s, const KParams& p, EnvRecs<M
     tu[m] = go ? uc[m] : tu[m];
     tc[m] = go ? tco[m] : tc[m];
   }
-  after.lp = fin[0][1];
-  after.ml = fin[1][1];
-  after.sh = fin[2][1];
-  after.b = fin[3][1];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) update_up<APAD, (2 * APAD - 1) / 2>(t[q]);
+  after.lp = t[0][1];
+  after.ml = t[1][1];
+  after.sh = t[2][1];
+  after.b = t[3][1];
 }
 
 // input selector
@@ -1032,6 +1024,26 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
   // exchange-form Broker rounds (LDS: M * 28 KB per block)
   constexpr bool XCH = (M * S <= 16) && (M <= 2) && (S >= 2);
   __shared__ EnvRecs<XCH ? M * S : 1> recs[XCH ? EPB : 1];
+  // loop-invariant tables read every step (generator parameters, PPC target,
+  // n-step discounts) are staged in LDS: a global load in the step loop would
+  // expose its full latency to the single resident wave
+  __shared__ mgn_asset_source s_src[MGN_MAX_ASSETS];
+  __shared__ double s_tgt[MGN_MAX_ASSETS + 1];
+  __shared__ double s_disc[NST ? MGN_MAX_NSTEP : 1];
+  {
+    const double* g = reinterpret_cast<const double*>(p.src);
+    double* d = reinterpret_cast<double*>(s_src);
+    const int n = p.A * (int)(sizeof(mgn_asset_source) / sizeof(double));
+    for (int i = threadIdx.x; i < n; i += BLOCK) d[i] = g[i];
+    if (p.target)
+      for (int i = threadIdx.x; i <= p.A; i += BLOCK) s_tgt[i] = p.target[i];
+    if constexpr (NST)
+      for (int i = threadIdx.x; i < p.nstep; i += BLOCK) s_disc[i] = p.disc[i];
+    __syncthreads();
+    p.src = s_src;
+    if (p.target) p.target = s_tgt;
+    if constexpr (NST) p.disc = s_disc;
+  }
   const int tid = threadIdx.x;
   const int ls = tid % S;
   const int env = blockIdx.x * EPB + tid / S;

@@ -207,11 +207,16 @@ def gather_bytes(env) -> float:
 
 
 def kernel_name(env, A: int) -> str:
+    """The step kernel as rocprofv3 names it: the two-role k_step_duo where the
+    handle's schedule picked it (mgn_get_schedule), else k_step<M, S, RQ1, NST>."""
+    from madigan_amd import _lib as L
     m = int(env.lib.mgn_get_layout(env.h))
     apad = 1 << max(0, (A - 1).bit_length())
     rq1 = "true" if env.cfg.required_margin == 1.0 else "false"
+    if int(env.lib.mgn_get_schedule(env.h)) == L.SCHED_DUO:
+        return f"mgn::k_step_duo<{apad}, {rq1}>"
     nst = "true" if env.nstep > 1 else "false"
-    return f"mgn::k_step<{m}, {apad // m}, {rq1}, {nst}>"  # as rocprofv3 names it
+    return f"mgn::k_step<{m}, {apad // m}, {rq1}, {nst}>"
 
 
 def main():
@@ -339,6 +344,7 @@ def main():
                        "n_envs_per_gpu": N, "n_assets": A, "window": 0,
                        "steps_per_launch": steps_per_launch,
                        "assets_per_lane": int(env.lib.mgn_get_layout(env.h)),
+                       "schedule": "duo" if int(env.lib.mgn_get_schedule(env.h)) == 2 else "single",
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": achieved_gbs / PEAK_HBM_GBS,

@@ -266,6 +266,14 @@ int mgn_feat_diff(const double *in_dev, double *out_dev, int64_t rows, int32_t c
  * canonical reduction tree does not depend on it); only speed changes. */
 int mgn_set_layout(mgn_env *env, int32_t assets_per_lane);
 int mgn_get_layout(const mgn_env *env);
+/* Step schedule: MGN_SCHED_SINGLE = k_step (every lane runs the whole Env
+ * step for its assets); MGN_SCHED_DUO = k_step_duo (each asset also has a lane
+ * in a generator wave that shares the SIMD; 2..8 assets, nstep 1, no replay);
+ * MGN_SCHED_AUTO (default) = DUO where eligible and the layout is one asset per
+ * lane.  Results are bit-identical; only speed changes. */
+enum { MGN_SCHED_AUTO = 0, MGN_SCHED_SINGLE = 1, MGN_SCHED_DUO = 2 };
+int mgn_set_schedule(mgn_env *env, int32_t schedule);
+int mgn_get_schedule(const mgn_env *env);
 /* DIAGNOSTIC ONLY (timing ablations, outputs become wrong): bit 0 skips the
  * Broker rounds, bit 1 the generators, bit 2 the output stores, bit 3 the
  * logarithms of the agent reward.  Never set in product or parity runs. */

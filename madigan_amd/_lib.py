@@ -28,6 +28,7 @@ REWARD_ENV_LOG, REWARD_AGENT_SUM, REWARD_AGENT_PER_ASSET = range(3)
  NORM_LOG_STANDARD_NORMAL) = range(6)
 RING_PLAIN, RING_PAIR_RATIO = range(2)
 STEP_NONE, STEP_UNITS, STEP_SINGLE = range(3)
+SCHED_AUTO, SCHED_SINGLE, SCHED_DUO = range(3)
 
 
 class MadiganError(RuntimeError):
@@ -113,6 +114,8 @@ SYMBOLS = {
     "mgn_feat_diff": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p]),
     "mgn_set_layout": (C.c_int, [C.c_void_p, C.c_int32]),
     "mgn_get_layout": (C.c_int, [C.c_void_p]),
+    "mgn_set_schedule": (C.c_int, [C.c_void_p, C.c_int32]),
+    "mgn_get_schedule": (C.c_int, [C.c_void_p]),
     "mgn_set_ablation": (C.c_int, [C.c_void_p, C.c_int32]),
     "mgn_synchronize": (C.c_int, [C.c_void_p]),
     "mgn_last_error": (C.c_char_p, [C.c_void_p]),

@@ -54,6 +54,8 @@ struct mgn_env {
   std::string err;
   int ablate = 0;
   int m = 1;  // assets per lane
+  int sched = MGN_SCHED_AUTO;  // requested step schedule
+  bool duo = false;            // the two-role kernel runs the steps
 };
 
 namespace {
@@ -231,6 +233,7 @@ void launch(void (*const* fns)(int, const Arg&), int apad, int m, const Arg& a) 
   fns[idx](m, a);
 }
 void (*const kStep[7])(int, const mgn::StepArgs&) = {mgn::launch_step_a1, mgn::launch_step_a2, mgn::launch_step_a4, mgn::launch_step_a8, mgn::launch_step_a16, mgn::launch_step_a32, mgn::launch_step_a64};
+void (*const kDuo[7])(const mgn::StepArgs&) = {mgn::launch_duo_a1, mgn::launch_duo_a2, mgn::launch_duo_a4, mgn::launch_duo_a8, mgn::launch_duo_a16, mgn::launch_duo_a32, mgn::launch_duo_a64};
 void (*const kInit[7])(int, const mgn::InitArgs&) = {mgn::launch_init_a1, mgn::launch_init_a2, mgn::launch_init_a4, mgn::launch_init_a8, mgn::launch_init_a16, mgn::launch_init_a32, mgn::launch_init_a64};
 void (*const kVal[7])(int, const mgn::ValArgs&) = {mgn::launch_val_a1, mgn::launch_val_a2, mgn::launch_val_a4, mgn::launch_val_a8, mgn::launch_val_a16, mgn::launch_val_a32, mgn::launch_val_a64};
 
@@ -242,6 +245,19 @@ void launch_val(const mgn_env* e, double* out);
 // Lane layout: as few lanes per env as keeps >= 2 waves per SIMD resident
 // (256 CUs x 4 SIMDs x 2), so large batches run thread-per-env-like (less
 // cross-lane work per env) and small batches spread each env over more lanes.
+// the two-role kernel: one lane per asset per role, padded width 2..8, one-step
+// rewards, generator sources (k_step handles replay tapes and n-step buffers)
+bool duo_eligible(const mgn_env* e) {
+  return e->apad >= 2 && e->apad <= 8 && e->cfg.nstep == 1 && !e->replay;
+}
+// automatic: where the single-role kernel would run one lane per asset (small
+// batches: one wave per SIMD), give every asset a second lane in a partner wave
+void choose_sched(mgn_env* e) {
+  if (e->sched == MGN_SCHED_SINGLE) e->duo = false;
+  else if (e->sched == MGN_SCHED_DUO) e->duo = duo_eligible(e);
+  else e->duo = duo_eligible(e) && e->m == 1;
+}
+
 int choose_m(int n_envs, int apad) {
   int m = mgn::min_m(apad);
   while (m < 8 && m < apad) {
@@ -255,6 +271,11 @@ int choose_m(int n_envs, int apad) {
 void launch_step(const mgn_env* e, const mgn_traj& out, int in_kind, const double* units,
                  const int32_t* aidx, const int8_t* act, int K) {
   mgn::StepArgs a{kparams(e), out, in_kind, units, aidx, act, K, e->stream};
+  if (e->duo) {
+    const int idx = e->apad <= 2 ? 1 : e->apad <= 4 ? 2 : 3;
+    kDuo[idx](a);
+    return;
+  }
   launch(kStep, e->apad, e->m, a);
 }
 void launch_init(const mgn_env* e, int mode, const uint8_t* mask) {
@@ -328,6 +349,7 @@ int mgn_create(const mgn_config* cfg, const mgn_asset_source* sources, void* str
   e->replay = sources[0].kind == MGN_SRC_REPLAY;
   e->apad = next_pow2(e->A);
   e->m = choose_m(e->N, e->apad);
+  choose_sched(e);
   e->stream = (hipStream_t)stream;
   const Offsets o = plan(cfg);
   e->arena_bytes = o.total;
@@ -605,6 +627,7 @@ int mgn_set_layout(mgn_env* e, int32_t assets_per_lane) {
   if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
   if (assets_per_lane == 0) {
     e->m = choose_m(e->N, e->apad);
+    choose_sched(e);
     return MGN_OK;
   }
   if (assets_per_lane != 1 && assets_per_lane != 2 && assets_per_lane != 4 && assets_per_lane != 8)
@@ -612,7 +635,23 @@ int mgn_set_layout(mgn_env* e, int32_t assets_per_lane) {
   int m = assets_per_lane < e->apad ? assets_per_lane : e->apad;
   if (m < mgn::min_m(e->apad)) m = mgn::min_m(e->apad);
   e->m = m;
+  choose_sched(e);
   return MGN_OK;
+}
+
+int mgn_set_schedule(mgn_env* e, int32_t schedule) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  if (schedule < MGN_SCHED_AUTO || schedule > MGN_SCHED_DUO)
+    return fail(e, MGN_ERR_CONFIG, "schedule must be MGN_SCHED_AUTO, _SINGLE or _DUO");
+  e->sched = schedule;
+  if (schedule == MGN_SCHED_DUO && !duo_eligible(e))
+    return fail(e, MGN_ERR_CONFIG, "the two-role kernel needs 2..8 assets, nstep 1, no replay tape");
+  choose_sched(e);
+  return MGN_OK;
+}
+
+int mgn_get_schedule(const mgn_env* e) {
+  return e ? (e->duo ? MGN_SCHED_DUO : MGN_SCHED_SINGLE) : 0;
 }
 
 int mgn_get_layout(const mgn_env* e) { return e ? e->m : 0; }

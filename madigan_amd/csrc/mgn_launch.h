@@ -5,6 +5,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include "mgn_duo.h"
 #include "mgn_kernels.h"
 
 namespace mgn {
@@ -35,6 +36,7 @@ struct ValArgs {
 constexpr int min_m(int apad) { return apad > 16 ? apad / 16 : 1; }
 
 #define MGN_DECLARE_APAD(A)                          \
+  void launch_duo_a##A(const StepArgs& a);           \
   void launch_step_a##A(int m, const StepArgs& a);   \
   void launch_init_a##A(int m, const InitArgs& a);   \
   void launch_val_a##A(int m, const ValArgs& a);

@@ -25,6 +25,19 @@ struct StepL {
     }
   }
 };
+// two-role step kernel (mgn_duo.h): S = APAD lanes per env per role
+template <int S>
+void launch_duo(const StepArgs& a) {
+  constexpr int epb = DUO_HALF / S;
+  const int grid = (a.p.N + epb - 1) / epb;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(DUO_BLOCK), 0, a.stream, a.p, a.out, a.in_kind,
+                       a.units, a.aidx, a.act, a.K);
+  };
+  if (a.p.reqm_one) go(k_step_duo<S, true>);
+  else go(k_step_duo<S, false>);
+}
+
 template <int M, int S>
 struct InitL {
   static void run(const InitArgs& a) {
@@ -62,6 +75,9 @@ void dispatch_m(int m, const Arg& a) {
 
 #define MGN_DEFINE_APAD(A)                                                                   \
   namespace mgn {                                                                            \
+  void launch_duo_a##A(const StepArgs& a) {                                                  \
+    if constexpr (A >= 2 && A <= 8) launch_duo<A>(a);                                        \
+  }                                                                                          \
   void launch_step_a##A(int m, const StepArgs& a) { dispatch_m<StepL, A>(m, a); }            \
   void launch_init_a##A(int m, const InitArgs& a) { dispatch_m<InitL, A>(m, a); }            \
   void launch_val_a##A(int m, const ValArgs& a) { dispatch_m<ValL, A>(m, a); }               \

@@ -285,3 +285,48 @@ def test_nstep_rollout(gpu, shaper, mode, n):
         ga, gb = ga[:, 0], gb[:, 0]
     close(ga, orc.scalar("shaperA"), "A")
     close(gb, orc.scalar("shaperB"), "B")
+
+
+@pytest.mark.parametrize("A,kw", [
+    (8, dict(reward_shaper="DDR")),
+    (3, dict(reward_shaper="DSR", reward_mode="agent_per_asset")),
+    (4, dict(reward_shaper="PPC", cosine_temp=0.05, window=8, norm_type="log")),
+    (2, dict(reward_shaper="sortino_shaperA", sortino_exp=2, reward_mode="agent_sum", window=5)),
+])
+def test_schedules_bit_identical(gpu, A, kw):
+    """The two-role kernel (k_step_duo: generator waves + ledger waves) and the
+    single-role k_step produce identical bits, including auto-resets, windows
+    and every step overload."""
+    from madigan_amd import BatchedEnv
+    from madigan_amd import _lib as L
+    N, K = 300, 40
+    base = dict(required_margin=0.02, maintenance_margin=0.25, transaction_cost_rel=0.02,
+                slippage_rel=1e-4, unit_size=0.9, auto_reset=True, init_cash=1e5, seed=17)
+    spec = spec_from_sources(trendou_sources(A, [0.2, 2, 6, 0.05, 0.2, 5.0, 0.15, 0.3, 0.2, 0.99]))
+    rng = np.random.default_rng(A)
+    units = rng.normal(0, 3e3, (N, A))
+    res = []
+    for sched in (L.SCHED_SINGLE, L.SCHED_DUO):
+        g = BatchedEnv(spec, N, **base, **kw)
+        L.check(g.lib.mgn_set_schedule(g.h, sched), g.h)
+        assert g.lib.mgn_get_schedule(g.h) == sched
+        acts = g.generate_actions(K, seed=9)
+        out = {k: v.cpu().numpy() for k, v in g.rollout(acts).items()}
+        g.step(units)
+        out.update({"s_" + k: v for k, v in g.host_outputs().items()})
+        g.step()
+        out.update({"n_" + k: v for k, v in g.host_outputs().items()})
+        out["ledger"] = g.ledger.cpu().numpy()
+        out["prices"] = g.prices.cpu().numpy()
+        out["cash"] = g.cash.cpu().numpy()
+        out["stats"] = g.episode_stats.cpu().numpy()
+        if g.W:
+            out.update({"w_" + str(i): t.cpu().numpy() for i, t in enumerate(g.window())})
+        res.append(out)
+    assert res[0]["done"].sum() > 0
+    for k, v in res[0].items():
+        w = res[1][k]
+        if np.asarray(v).dtype == np.float64:
+            assert_bits(w, v, f"duo vs single {k}")
+        else:
+            assert np.array_equal(np.asarray(w), np.asarray(v)), f"duo vs single {k}"

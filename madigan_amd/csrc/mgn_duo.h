@@ -15,16 +15,19 @@
 //   ledger waves (4-7): actions, Broker rounds (Broker.cpp:124-178), the
 //     post-tick sums, equity and `done` (Env.h:206-223); they publish a step
 //     record (ledger, responses, equities, cash) to LDS;
-//   generator waves (0-3): per iteration, first the previous step's record
-//     -> reward, ledgerNormedFull, agent reward, shaper, episode statistics,
-//     window row and every output store; then the source reset if one is
-//     pending and the tick (gen_tick), whose prices go to LDS.
+//   generator waves (0-3): per iteration the source reset if one is pending
+//     and the tick (gen_tick), whose prices go to LDS; then the previous
+//     step's record -> reward, ledgerNormedFull, agent reward, shaper,
+//     episode statistics, window row and every output store.
 //
-// Iteration j: [gen: record j-1 + tick j || ledger: orders of step j] barrier
-// [ledger: prices of tick j -> sums, done, record j] barrier.  Each value is
+// Iteration j: [gen: tick j || ledger: orders of step j] barrier [gen: step
+// j-1's record -> outputs || ledger: prices of tick j -> sums, done, record j
+// (records double-buffered by iteration parity)] barrier.  Each value is
 // the same expression of the same operands as in k_step, so every output is
 // bit-identical to k_step (and to the oracle); only the computing lane differs.
 // Scope: M = 1, APAD = S in {2, 4, 8}, n-step 1, no replay tape (those run k_step).
+// Diagnostic ablation bits (mgn_set_ablation): 1 Broker rounds, 2 generator
+// ticks, 4 the generator side's step finish (outputs).
 #pragma once
 
 #include "mgn_kernels.h"
@@ -36,20 +39,63 @@ constexpr int DUO_HALF = DUO_BLOCK / 2;
 
 enum { REC_STEP = 1, REC_TICK = 2, REC_DONE = 4, REC_MCALL = 8 };
 
+// step record of lane / env (ledger -> generator waves)
 template <int S>
-struct DuoShared {
+struct DuoRec {
   static constexpr int EPB = DUO_HALF / S;
-  double price[DUO_HALF];  // tick prices, lane (env_local * S + slot)
-  // step record of lane / env (ledger -> generator waves)
   double rL[DUO_HALF], rPrev[DUO_HALF], rTp[DUO_HALF], rTu[DUO_HALF], rTc[DUO_HALF];
   int32_t rRk[DUO_HALF];
   double rPrevEq[EPB], rCurEq[EPB], rCash[EPB], rLp[EPB], rB[EPB];
   int32_t rK[EPB], rFlags[EPB];
+};
+
+template <int S>
+struct DuoShared {
+  static constexpr int EPB = DUO_HALF / S;
+  double price[DUO_HALF];  // tick prices, lane (env_local * S + slot)
+  DuoRec<S> rec[2];        // record of iteration j in rec[j & 1]
   int32_t tick[EPB];   // env ticks this iteration
   int32_t reset[EPB];  // apply the source reset before the tick
   int32_t more[3];     // some env ticks next iteration, slot j % 3 (a slot is
                        // cleared two barriers after its last read)
 };
+
+// Output pointers live in VGPR pairs (in_vgpr: the compiler cannot move them
+// back into SGPRs) and their null tests in one uniform bit mask: with every
+// pointer of KParams and mgn_traj in SGPRs the kernel spilled SGPRs to VGPR
+// lanes and reloaded them with v_readlane inside the step loop.
+enum : uint32_t { O_REW = 1u, O_AREW = 2u, O_SHP = 4u, O_DONE = 8u, O_OPR = 16u, O_OPT = 32u,
+                  O_TS = 64u, O_TP = 128u, O_TU = 256u, O_TC = 512u, O_RISK = 1024u,
+                  O_MC = 2048u, O_NSH = 4096u, O_DEND = 8192u };
+__device__ __forceinline__ uint32_t traj_mask(const mgn_traj& o) {
+  return (o.reward ? O_REW : 0u) | (o.agent_reward ? O_AREW : 0u) | (o.shaped ? O_SHP : 0u) |
+         (o.done ? O_DONE : 0u) | (o.obs_price ? O_OPR : 0u) | (o.obs_port ? O_OPT : 0u) |
+         (o.timestamp ? O_TS : 0u) | (o.tprice ? O_TP : 0u) | (o.tunits ? O_TU : 0u) |
+         (o.tcost ? O_TC : 0u) | (o.risk ? O_RISK : 0u) | (o.margin_call ? O_MC : 0u) |
+         (o.n_shaped ? O_NSH : 0u) | (o.data_end ? O_DEND : 0u);
+}
+template <typename T>
+__device__ __forceinline__ T* vptr(T* q) {
+  return reinterpret_cast<T*>(in_vgpr(reinterpret_cast<uintptr_t>(q)));
+}
+__device__ __forceinline__ mgn_traj traj_vgpr(const mgn_traj& o) {
+  mgn_traj v;
+  v.reward = vptr(o.reward);
+  v.agent_reward = vptr(o.agent_reward);
+  v.shaped = vptr(o.shaped);
+  v.done = vptr(o.done);
+  v.obs_price = vptr(o.obs_price);
+  v.obs_port = vptr(o.obs_port);
+  v.timestamp = vptr(o.timestamp);
+  v.tprice = vptr(o.tprice);
+  v.tunits = vptr(o.tunits);
+  v.tcost = vptr(o.tcost);
+  v.risk = vptr(o.risk);
+  v.margin_call = vptr(o.margin_call);
+  v.n_shaped = vptr(o.n_shaped);
+  v.data_end = vptr(o.data_end);
+  return v;
+}
 
 // The generator lane's half of an Env step: everything downstream of the
 // record (Env.h:211-229, Portfolio.cpp:150-155, offpolicy_q.py:152-164,
@@ -59,10 +105,12 @@ struct GenOut {
   int32_t head, len;
 };
 
+// P, ts: the State's price and timestamp (the tick the record belongs to)
 template <int S>
-__device__ __forceinline__ void duo_finish(const DuoShared<S>& sh, const Lane<1>& s, const KParams& p,
-                                           const mgn_traj& out, int in_kind, int env, int el, int l,
-                                           int ls, uint64_t ts, bool need_ar, GenOut& g) {
+__device__ __forceinline__ void duo_finish(const DuoRec<S>& sh, const Lane<1>& s, const KParams& p,
+                                           const mgn_traj& out, uint32_t om, int in_kind, int env,
+                                           int el, int l, int ls, double P, uint64_t ts,
+                                           bool need_ar, GenOut& g) {
   constexpr int M = 1;
   const int flags = sh.rFlags[el];
   if (flags == 0) return;
@@ -70,7 +118,6 @@ __device__ __forceinline__ void duo_finish(const DuoShared<S>& sh, const Lane<1>
   const int D = p.D;
   const double cash = sh.rCash[el];
   const double Lc = sh.rL[l];
-  const double P = s.P[0];
   const bool valid = s.valid[0];
   if (flags & REC_STEP) {
     const int k = sh.rK[el];
@@ -83,8 +130,6 @@ __device__ __forceinline__ void duo_finish(const DuoShared<S>& sh, const Lane<1>
     const double ratio = curEq / prevEq;
     const double clampv = (in_kind == IN_SINGLE) ? 0.01 : 0.3;
     const double reward = log((ratio < clampv) ? clampv : ratio);
-    const double port0 = (cash - qb) / curEq;
-    const double portA = (Lc * P) / curEq;
     double ar[M];
     ar[0] = 0.;
     if (valid && need_ar) {
@@ -95,6 +140,8 @@ __device__ __forceinline__ void duo_finish(const DuoShared<S>& sh, const Lane<1>
     }
     double cos_term = 0.;
     if (p.shaper == MGN_SHAPER_PPC) {
+      const double port0 = (cash - qb) / curEq;
+      const double portA = (Lc * P) / curEq;
       double pp[M], pq[M];
       const double qv = valid ? p.target[1 + s.asset[0]] : 0.;
       const double pv = valid ? portA : 0.;
@@ -111,30 +158,19 @@ __device__ __forceinline__ void duo_finish(const DuoShared<S>& sh, const Lane<1>
     } else {
       shaped_v = valid ? shape(p.shaper, ar[0], g.shA, g.shB, p.eta, cos_term, p.sexp) : 0.;
     }
-    if (valid) {
+    if (valid && D != 1) {
       const size_t i = oNA + (size_t)env * A + s.asset[0];
-      if (out.tprice) out.tprice[i] = tp;
-      if (out.tunits) out.tunits[i] = tu;
-      if (out.tcost) out.tcost[i] = tc;
-      if (out.risk) out.risk[i] = (uint8_t)sh.rRk[l];
-      if (out.obs_port) out.obs_port[(size_t)k * p.N * (A + 1) + (size_t)env * (A + 1) + 1 + s.asset[0]] = portA;
-      if (out.obs_price) out.obs_price[(oN + env) * (size_t)p.F + s.asset[0]] = P;
-      if (D != 1) {
-        if (out.agent_reward) out.agent_reward[i] = ar[0];
-        if (out.shaped) out.shaped[i] = shaped_v;
-      }
+      if (om & O_AREW) out.agent_reward[i] = ar[0];
+      if (om & O_SHP) out.shaped[i] = shaped_v;
     }
     if (ls == 0) {
-      if (out.data_end) out.data_end[oN + env] = 0;
-      if (out.reward) out.reward[oN + env] = reward;
-      if (out.done) out.done[oN + env] = done ? 1 : 0;
-      if (out.timestamp) out.timestamp[oN + env] = ts;
-      if (out.margin_call) out.margin_call[oN + env] = (flags & REC_MCALL) ? 1 : 0;
-      if (out.n_shaped) out.n_shaped[oN + env] = 1;
-      if (out.obs_port) out.obs_port[(size_t)k * p.N * (A + 1) + (size_t)env * (A + 1)] = port0;
+      if (om & O_DEND) out.data_end[oN + env] = 0;
+      if (om & O_REW) out.reward[oN + env] = reward;
+      if (om & O_TS) out.timestamp[oN + env] = ts;
+      if (om & O_NSH) out.n_shaped[oN + env] = 1;
       if (D == 1) {
-        if (out.agent_reward) out.agent_reward[oN + env] = rin_s;
-        if (out.shaped) out.shaped[oN + env] = shaped_s;
+        if (om & O_AREW) out.agent_reward[oN + env] = rin_s;
+        if (om & O_SHP) out.shaped[oN + env] = shaped_s;
       }
     }
     g.ep_ret += reward;
@@ -176,6 +212,103 @@ __device__ __forceinline__ void duo_finish(const DuoShared<S>& sh, const Lane<1>
   }
 }
 
+// Broker::handleTransaction(units) for a segment of S lanes, one asset per
+// lane, resolved speculatively.  The serial dependency between orders (each
+// risk check sees the cash and portfolio sums the earlier orders left,
+// Broker.cpp:149-155) is only a dependency on which earlier orders executed.
+// Guess that every nonzero order executes; then each lane checks ITS order
+// against the state the guess implies -- the cash chain c_i over the earlier
+// executed orders (the same (((c + X1) - y) - Z) sequence as the serial form)
+// and the canonical trees over the leaves (executed earlier orders: post-order
+// leaves, the rest: pre-order) -- all lanes in parallel.  The checks up to the
+// first order whose outcome contradicts the guess are exact; that order's
+// outcome is taken from its check, later ones are re-guessed, repeat.  Every
+// check that is kept was evaluated on exactly the operands the serial form
+// uses, so the ledger, responses and sums are bit-identical to XRounds; an
+// unrefused batch (the common case) costs one pass instead of S dependent
+// rounds.
+template <int S, bool RQ1>
+__device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRecs<S>& er,
+                                            double& cash, const double (&uc)[1], double (&tp)[1],
+                                            double (&tu)[1], double (&tc)[1], int (&rk)[1], int ls,
+                                            Sums& after, int& any_mc) {
+  double cu2[1], me2[1], bm3[1], tpr[1], tco[1];
+  order_prep<1, S>(s, p, er, uc, ls, cu2, me2, bm3, tpr, tco);
+  const OrderRec& own = er.r[ls];
+  const int act = uc[0] != 0. ? 1 : 0;
+  const uint32_t act_bits = (uint32_t)seg_or<S>(act << ls);
+  uint32_t go_bits = act_bits;  // the guess
+  const double cash0 = cash;
+  int go = 0, mc = 0, insuff = 0;
+  double cend = cash0;
+  for (int it = 0; it <= S; ++it) {
+    // cash before this lane's order, and after the last order, under the guess
+    double c = cash0, c_own = cash0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      if (i == ls) c_own = c;
+      const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
+      const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
+      const double ci = ((c + xz.y) - yz.x) - yz.y;
+      c = ((go_bits >> i) & 1) ? ci : c;
+    }
+    cend = c;
+    // canonical sums before this lane's order: leaves of executed earlier
+    // orders after the order, the others before
+    double lv[4][S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const bool post = (j < ls) && ((go_bits >> j) & 1);
+      const d2* rv = reinterpret_cast<const d2*>(&er.r[j]) + (post ? 2 : 0);
+      const d2 a = rv[0], b = rv[1];
+      lv[0][j] = a.x;
+      lv[1][j] = a.y;
+      lv[2][j] = b.x;
+      lv[3][j] = b.y;
+    }
+    const double r0 = tree<S>(lv[0]), r1 = tree<S>(lv[1]), r2 = tree<S>(lv[2]), r3 = tree<S>(lv[3]);
+    // Portfolio::checkRisk(i, u), Portfolio.cpp:254-279 (as XRounds)
+    const double pnl = r0 - r1;
+    const double balance = c_own + r2;
+    const double bp = balance + pnl;
+    const double availM = RQ1 ? bp : bp / p.reqM;
+    const double equity = (c_own + r0) - r3;
+    const double mr = p.mainM * pnl;
+    mc = (own.need_mc != 0) & ((equity <= -mr) | (bp <= -mr));
+    insuff = (own.need_insuff != 0) & ((availM <= own.aPX) | (balance <= 0.));
+    go = act & !mc & !insuff;
+    const uint32_t bad = (uint32_t)seg_or<S>((go != (int)((go_bits >> ls) & 1)) ? (1 << ls) : 0);
+    if (bad == 0) break;
+    const int i0 = __builtin_ctz(bad);
+    const uint32_t go_now = (uint32_t)seg_or<S>(go << ls);
+    const uint32_t below = (1u << i0) - 1u;
+    go_bits = (go_bits & below) | (go_now & (1u << i0)) | (act_bits & ~(below | (1u << i0)));
+  }
+  cash = cend;
+  any_mc = seg_or<S>(act & mc) != 0;
+  rk[0] = act ? (mc ? MGN_MARGIN_CALL : (insuff ? MGN_INSUFF_MARGIN : MGN_GREEN)) : rk[0];
+  const bool go_own[1] = {go != 0};
+  // the post-transaction sums: every leaf at its final value
+  double lv[4][S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const bool post = (go_bits >> j) & 1;
+    const d2* rv = reinterpret_cast<const d2*>(&er.r[j]) + (post ? 2 : 0);
+    const d2 a = rv[0], b = rv[1];
+    lv[0][j] = a.x;
+    lv[1][j] = a.y;
+    lv[2][j] = b.x;
+    lv[3][j] = b.y;
+  }
+  after.lp = tree<S>(lv[0]);
+  after.ml = tree<S>(lv[1]);
+  after.sh = tree<S>(lv[2]);
+  after.b = tree<S>(lv[3]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  apply_orders<1>(s, go_own, cu2, me2, bm3, tpr, tco, uc, tp, tu, tc);
+}
+
 template <int S, bool RQ1>
 __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out, int in_kind,
                                                         const double* __restrict__ units_in,
@@ -208,7 +341,8 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
   if (!gen_role && ls == 0) {
     sh.tick[el] = (live && K > 0) ? 1 : 0;
     sh.reset[el] = 0;
-    sh.rFlags[el] = 0;
+    sh.rec[0].rFlags[el] = 0;
+    sh.rec[1].rFlags[el] = 0;
   }
   if (threadIdx.x == 0) {
     sh.more[0] = 0;
@@ -250,23 +384,37 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       g.cos_qn = sqrt(p.target[0] * p.target[0] + canon<M, S>(qq));
     }
     const bool need_ar = (p.reward_mode != MGN_REWARD_ENV_LOG) || (out.agent_reward != nullptr);
-    for (int j = 0;; ++j) {
-      if (live) {
-        duo_finish<S>(sh, s, p, out, in_kind, env, el, l, ls, ts, need_ar, g);
-        if (sh.tick[el]) {
-          if (sh.reset[el]) src_reset<M>(s, p);  // Env::reset -> dataSource->reset (Env.h:183)
-          gen_tick<M>(s, p, env, ts);
-          ts = ts + 1;
-          sh.price[l] = s.P[0];
-        }
+    const uint32_t om = traj_mask(out);
+    const mgn_traj ov = traj_vgpr(out);
+    // the Philox key schedule (seed + r * W, r < 10) is loop-invariant: from a
+    // VGPR seed it stays in VGPRs instead of 20 spilled SGPRs
+    p.seed = in_vgpr(p.seed);
+    p.env_offset = in_vgpr(p.env_offset);
+    p.epstats = vptr(p.epstats);
+    p.ring = vptr(p.ring);
+    p.ring_ts = vptr(p.ring_ts);
+    int j = 0;
+    for (;; ++j) {
+      // phase 1: tick j
+      const double P_prev = s.P[0];
+      const uint64_t ts_prev = ts;
+      if (live && sh.tick[el]) {
+        if (sh.reset[el]) src_reset<M>(s, p);  // Env::reset -> dataSource->reset (Env.h:183)
+        if (!(p.ablate & 2)) gen_tick<M, false>(s, p, env, ts);
+        ts = ts + 1;
+        sh.price[l] = s.P[0];
       }
       if (threadIdx.x == 0) sh.more[(j + 1) % 3] = 0;
-      __syncthreads();  // A: prices of tick j published; record j-1 consumed
+      __syncthreads();  // A: prices of tick j published
+      // phase 2: finish step j-1 (its State: the price and time before tick j)
+      if (live && j > 0 && !(p.ablate & 4))
+        duo_finish<S>(sh.rec[(j - 1) & 1], s, p, ov, om, in_kind, env, el, l, ls, P_prev, ts_prev,
+                      need_ar, g);
       __syncthreads();  // B: record j published
       if (!sh.more[j % 3]) break;
     }
     if (!live) return;
-    duo_finish<S>(sh, s, p, out, in_kind, env, el, l, ls, ts, need_ar, g);
+    duo_finish<S>(sh.rec[j & 1], s, p, ov, om, in_kind, env, el, l, ls, s.P[0], ts, need_ar, g);
     if (s.valid[0]) {
       const size_t i = (size_t)env * A + s.asset[0];
       p.P[i] = s.P[0];
@@ -297,6 +445,11 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
   }
 
   // ---------------- ledger waves
+  const uint32_t om = traj_mask(out);
+  const mgn_traj ov = traj_vgpr(out);
+  act_in = vptr(act_in);
+  units_in = vptr(units_in);
+  aidx_in = vptr(aidx_in);
   p.init_cash = in_vgpr(p.init_cash);
   p.mainM = in_vgpr(p.mainM);
   p.unit_size = in_vgpr(p.unit_size);
@@ -347,14 +500,15 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
         uc[0] = (s.valid[0] && s.asset[0] == ai) ? u : 0.;
       }
       prevVal = s.L[0] * s.P[0];
-      if (in_kind != IN_NONE) {
-        broker_x<M, S, RQ1>(s, p, recs[el], cash, s0, uc, tp, tu, tc, rk, ls, sa, any_mc);
+      if (in_kind != IN_NONE && !(p.ablate & 1)) {
+        broker_spec<S, RQ1>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, sa, any_mc);
         mcall = margin_call(sa, cash, p.mainM) ? 1 : 0;  // Broker.cpp:156-157
       }
     }
     __syncthreads();  // A: the prices of tick j are in LDS
     bool reset_now = false;
     int flags = 0;
+    DuoRec<S>& rc = sh.rec[j & 1];
     if (ticking && s.valid[0]) s.P[0] = sh.price[l];
     if (stepping) {
       // post-tick sums, equity, done (Env.h:211-223): only L*P sees the new prices
@@ -366,20 +520,38 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       }
       const double curEq = (cash + q.lp) - q.b;
       const bool done = any_mc || margin_call(q, cash, p.mainM) || (curEq < 0.1 * p.init_cash);
-      sh.rL[l] = s.L[0];
-      sh.rPrev[l] = prevVal;
-      sh.rTp[l] = tp[0];
-      sh.rTu[l] = tu[0];
-      sh.rTc[l] = tc[0];
-      sh.rRk[l] = rk[0];
+      rc.rL[l] = s.L[0];
+      rc.rPrev[l] = prevVal;
+      rc.rTp[l] = tp[0];
+      rc.rTu[l] = tu[0];
+      rc.rTc[l] = tc[0];
+      rc.rRk[l] = rk[0];
       flags = REC_STEP | (done ? REC_DONE : 0) | (mcall ? REC_MCALL : 0);
+      // the step's ledger-side outputs: BrokerResponse, State.portfolio =
+      // ledgerNormedFull (Portfolio.cpp:150-155), State.price, done, marginCall
+      if (s.valid[0]) {
+        const size_t i = oNA + (size_t)env * A + s.asset[0];
+        if (om & O_TP) ov.tprice[i] = tp[0];
+        if (om & O_TU) ov.tunits[i] = tu[0];
+        if (om & O_TC) ov.tcost[i] = tc[0];
+        if (om & O_RISK) ov.risk[i] = (uint8_t)rk[0];
+        if (om & O_OPT)
+          ov.obs_port[(size_t)k * p.N * (A + 1) + (size_t)env * (A + 1) + 1 + s.asset[0]] =
+              (s.L[0] * s.P[0]) / curEq;
+        if (om & O_OPR) ov.obs_price[(oN + env) * (size_t)p.F + s.asset[0]] = s.P[0];
+      }
       if (ls == 0) {
-        sh.rPrevEq[el] = prevEq;
-        sh.rCurEq[el] = curEq;
-        sh.rCash[el] = cash;
-        sh.rLp[el] = q.lp;
-        sh.rB[el] = q.b;
-        sh.rK[el] = k;
+        if (om & O_OPT) ov.obs_port[(size_t)k * p.N * (A + 1) + (size_t)env * (A + 1)] = (cash - q.b) / curEq;
+        if (om & O_DONE) ov.done[oN + env] = done ? 1 : 0;
+        if (om & O_MC) ov.margin_call[oN + env] = (uint8_t)mcall;
+      }
+      if (ls == 0) {
+        rc.rPrevEq[el] = prevEq;
+        rc.rCurEq[el] = curEq;
+        rc.rCash[el] = cash;
+        rc.rLp[el] = q.lp;
+        rc.rB[el] = q.b;
+        rc.rK[el] = k;
       }
       s0 = q;
       k += 1;
@@ -398,17 +570,17 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       pending -= 1;
       const Sums q = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
       if (pending == 0) s0 = q;
-      sh.rL[l] = s.L[0];
+      rc.rL[l] = s.L[0];
       flags = REC_TICK;
       if (ls == 0) {
-        sh.rCash[el] = cash;
-        sh.rLp[el] = q.lp;
-        sh.rB[el] = q.b;
+        rc.rCash[el] = cash;
+        rc.rLp[el] = q.lp;
+        rc.rB[el] = q.b;
       }
     }
     const bool next_tick = live && ((pending > 0) || (k < K));
     if (ls == 0) {
-      sh.rFlags[el] = flags;
+      rc.rFlags[el] = flags;
       sh.tick[el] = next_tick ? 1 : 0;
       sh.reset[el] = reset_now ? 1 : 0;
     }

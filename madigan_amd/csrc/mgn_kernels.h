@@ -197,9 +197,10 @@ struct Lane {
 
 // DataSource::getData for the lane's slots (DataSource.cpp:535-543, 1173-1180,
 // 1457-1493; Composite concatenation :439-451) ; tick = timestamp before ++.
-template <int M>
+// RP: the kernel may serve a replay tape (k_step); the two-role kernel never does
+template <int M, bool RP = true>
 __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, uint64_t tick) {
-  if (p.replay) {
+  if (RP && p.replay) {
     // HDFSourceSingle::getData (DataSource.cpp:391-398) on the tape: the
     // row iterCache / loadData would serve, then advance (wrap = the
     // reference's rewind to boundsIdx_.first, :368-371, :397-399)
@@ -721,18 +722,18 @@ struct XRounds {
   }
 };
 
-// The whole Broker::handleTransaction(units) (Broker.cpp:144-158) for the
-// lane's segment, exchange form.  On return the lane's slots hold the new
-// ledger, tp/tu/tc/rk the responses, `after` the canonical sums of the
-// post-transaction portfolio, and any_mc whether any order of the segment
-// was refused with MARGIN_CALL (the env's done condition, Env.h:216-218).
-template <int M, int S, bool RQ1>
-__device__ __forceinline__ void broker_x(Lane<M>& s, const KParams& p, EnvRecs<M * S>& er,
-                                         double& cash, const Sums& s0, const double (&uc)[M],
-                                         double (&tp)[M], double (&tu)[M], double (&tc)[M],
-                                         int (&rk)[M], int ls, Sums& after, int& any_mc) {
-  constexpr int APAD = M * S;
-  double cu2[M], me2[M], bm3[M], tpr[M], tco[M];
+// Per-order records of the lane's slots (the order-local half of
+// Broker::handleTransaction, Broker.cpp:128-135, and Portfolio::
+// handleTransaction, Portfolio.cpp:284-323): transaction price and cost, the
+// ledger / mean entry / borrowed the order would leave, the four sum leaves
+// before and after it, and the cash increments; published to the segment's
+// LDS records.  The risk checks and cash updates that chain the orders are
+// resolved afterwards (XRounds, or the speculative form in mgn_duo.h).
+template <int M, int S>
+__device__ __forceinline__ void order_prep(const Lane<M>& s, const KParams& p, EnvRecs<M * S>& er,
+                                           const double (&uc)[M], int ls, double (&cu2)[M],
+                                           double (&me2)[M], double (&bm3)[M], double (&tpr)[M],
+                                           double (&tco)[M]) {
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     const double u = uc[m];
@@ -792,6 +793,40 @@ __device__ __forceinline__ void broker_x(Lane<M>& s, const KParams& p, EnvRecs<M
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
+}
+
+// the orders' effect on the lane's slots once their fate is known
+template <int M>
+__device__ __forceinline__ void apply_orders(Lane<M>& s, const bool (&go_own)[M],
+                                             const double (&cu2)[M], const double (&me2)[M],
+                                             const double (&bm3)[M], const double (&tpr)[M],
+                                             const double (&tco)[M], const double (&uc)[M],
+                                             double (&tp)[M], double (&tu)[M], double (&tc)[M]) {
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const bool go = go_own[m];
+    s.L[m] = go ? cu2[m] : s.L[m];
+    s.mep[m] = go ? me2[m] : s.mep[m];
+    s.Bm[m] = go ? bm3[m] : s.Bm[m];
+    tp[m] = go ? tpr[m] : tp[m];
+    tu[m] = go ? uc[m] : tu[m];
+    tc[m] = go ? tco[m] : tc[m];
+  }
+}
+
+// The whole Broker::handleTransaction(units) (Broker.cpp:144-158) for the
+// lane's segment, exchange form.  On return the lane's slots hold the new
+// ledger, tp/tu/tc/rk the responses, `after` the canonical sums of the
+// post-transaction portfolio, and any_mc whether any order of the segment
+// was refused with MARGIN_CALL (the env's done condition, Env.h:216-218).
+template <int M, int S, bool RQ1>
+__device__ __forceinline__ void broker_x(Lane<M>& s, const KParams& p, EnvRecs<M * S>& er,
+                                         double& cash, const Sums& s0, const double (&uc)[M],
+                                         double (&tp)[M], double (&tu)[M], double (&tc)[M],
+                                         int (&rk)[M], int ls, Sums& after, int& any_mc) {
+  constexpr int APAD = M * S;
+  double cu2[M], me2[M], bm3[M], tpr[M], tco[M];
+  order_prep<M, S>(s, p, er, uc, ls, cu2, me2, bm3, tpr, tco);
   double t[4][2 * APAD];
 #pragma unroll
   for (int a = 0; a < APAD; ++a) {
@@ -816,16 +851,7 @@ __device__ __forceinline__ void broker_x(Lane<M>& s, const KParams& p, EnvRecs<M
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
 
-#pragma unroll
-  for (int m = 0; m < M; ++m) {
-    const bool go = go_own[m];
-    s.L[m] = go ? cu2[m] : s.L[m];
-    s.mep[m] = go ? me2[m] : s.mep[m];
-    s.Bm[m] = go ? bm3[m] : s.Bm[m];
-    tp[m] = go ? tpr[m] : tp[m];
-    tu[m] = go ? uc[m] : tu[m];
-    tc[m] = go ? tco[m] : tc[m];
-  }
+  apply_orders<M>(s, go_own, cu2, me2, bm3, tpr, tco, uc, tp, tu, tc);
 #pragma unroll
   for (int q = 0; q < 4; ++q) update_up<APAD, (2 * APAD - 1) / 2>(t[q]);
   after.lp = t[0][1];

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MGN_ABI_VERSION 4
+#define MGN_ABI_VERSION 5
 #define MGN_MAX_ASSETS 64
 #define MGN_MAX_NSTEP 64
 
@@ -62,7 +62,10 @@ enum { MGN_GREEN = 0, MGN_INSUFF_MARGIN = 1, MGN_MARGIN_CALL = 2, MGN_BLOWN_OUT 
 enum { MGN_SRC_EXTERNAL = 0, MGN_SRC_SINE = 1, MGN_SRC_OU = 2, MGN_SRC_TRENDOU = 3,
        MGN_SRC_REPLAY = 4 /* every asset of the env, from the attached replay tape */,
        MGN_SRC_SIMPLETREND = 5, MGN_SRC_TRENDYOU = 6, MGN_SRC_GAUSSIAN = 7,
-       MGN_SRC_SAWTOOTH = 8, MGN_SRC_TRIANGLE = 9, MGN_SRC_OUPAIR = 10 };
+       MGN_SRC_SAWTOOTH = 8, MGN_SRC_TRIANGLE = 9, MGN_SRC_OUPAIR = 10,
+       MGN_SRC_SINEADDER = 11, MGN_SRC_SINEDYNAMIC = 12, MGN_SRC_SINEDYNTREND = 13 };
+#define MGN_SRC_PARAMS 64   /* doubles of parameters per asset */
+#define MGN_AUX_WIDTH 24    /* doubles of extra source state per asset (views.aux) */
 
 /* reward shapers (nstep_buffer.py:378-408): DSR :30-98, DDR :101-169, PPC = cosine_port_shaper
  * :182-204, SHARPE = sharpe_shaper :207-239, SORTINO_A/B = sortino_shaperA/B :242-312 */
@@ -90,11 +93,24 @@ enum { MGN_STEP_NONE = 0, MGN_STEP_UNITS = 1, MGN_STEP_SINGLE = 2 };
  *  GAUSSIAN    p = {mean, var (the normal's stddev)}        DataSource.cpp:1057-1114
  *  SAWTOOTH / TRIANGLE p = as SINE                          DataSource.cpp:557-577
  *  OUPAIR      p = {theta, phi, noise, role}: role 0 / 1 = the pair's first /
- *              second asset, adjacent in asset order        DataSource.cpp:1183-1250 */
+ *              second asset, adjacent in asset order        DataSource.cpp:1183-1250
+ *  SINEADDER   p = {C, dX, noise, freq[C], mu[C], amp[C], phase[C]}, C <= 8: one
+ *              asset, the sum of C noisy sines              DataSource.cpp:582-673
+ *  SINEDYNAMIC p = {C, sampleRate, noise, tableLen[C], then per component
+ *              freqRange[3], muRange[3], ampRange[3] ({lo, hi, step})}, C <= 4:
+ *              one asset, C WaveTableOsc sines with random-walk parameters
+ *                                                           DataSource.cpp:678-845,
+ *                                                           WaveTableOsc.h
+ *  SINEDYNTREND p = SINEDYNAMIC's, then {T, per trend {minLen, maxLen, incr,
+ *              prob}}, T <= 2                               DataSource.cpp:850-1051
+ *  The multi-component kinds keep their extra state in views.aux
+ *  (N, A, MGN_AUX_WIDTH): SINEADDER x[C]; SINEDYNAMIC {phasor, freq, mu, amp}
+ *  per component; SINEDYNTREND also [16] trendComponent and per trend
+ *  [17+3t] trending, [18+3t] direction, [19+3t] remaining length. */
 typedef struct {
   int32_t kind;
   int32_t pad_;
-  double p[12];
+  double p[MGN_SRC_PARAMS];
 } mgn_asset_source;
 
 typedef struct {
@@ -125,6 +141,9 @@ typedef struct {
                                   (0 = n_assets); the feature columns of a replay source */
   int32_t pad3_;
   double sortino_exp;          /* sortino_shaperA/B exponent (shaper config "sortino_exp") */
+  int32_t aux;                 /* 1: some asset is a multi-component kind (SINEADDER,
+                                  SINEDYNAMIC, SINEDYNTREND) -> views.aux is allocated */
+  int32_t pad4_;
 } mgn_config;
 
 /* Per-step outputs.  For mgn_step they are the handle's buffers (see views);
@@ -171,6 +190,8 @@ typedef struct {
   double *nstep_ring;                                /* (N,n,D) NStepBuffer rewards */
   int32_t *nstep_len, *nstep_head;                   /* (N) fill count, oldest index */
   int64_t *replay_cursor;                            /* (N) next tape row of a replay env */
+  double *aux;                                       /* (N,A,MGN_AUX_WIDTH) multi-component
+                                                        source state (NULL if unused) */
   mgn_traj out;                                      /* mgn_step outputs */
   int32_t n_envs, n_assets, window, reward_dim, nstep, n_feats;
 } mgn_views;

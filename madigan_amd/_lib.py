@@ -12,7 +12,9 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmadigan_hip.so")
 MAX_ASSETS = 64
-ABI_VERSION = 4
+ABI_VERSION = 5
+SRC_PARAMS = 64
+AUX_WIDTH = 24
 MAX_NSTEP = 64
 
 # status codes -> the reference's exception types (DataTypes.h:36-46, pybind11)
@@ -20,7 +22,7 @@ OK, ERR_CONFIG, ERR_INDEX, ERR_LENGTH, ERR_DEVICE, ERR_ARG = range(6)
 
 GREEN, INSUFF_MARGIN, MARGIN_CALL, BLOWN_OUT = range(4)
 (SRC_EXTERNAL, SRC_SINE, SRC_OU, SRC_TRENDOU, SRC_REPLAY, SRC_SIMPLETREND, SRC_TRENDYOU, SRC_GAUSSIAN,
- SRC_SAWTOOTH, SRC_TRIANGLE, SRC_OUPAIR) = range(11)
+ SRC_SAWTOOTH, SRC_TRIANGLE, SRC_OUPAIR, SRC_SINEADDER, SRC_SINEDYNAMIC, SRC_SINEDYNTREND) = range(14)
 (SHAPER_NONE, SHAPER_DSR, SHAPER_DDR, SHAPER_PPC, SHAPER_SHARPE, SHAPER_SORTINO_A,
  SHAPER_SORTINO_B) = range(7)
 REWARD_ENV_LOG, REWARD_AGENT_SUM, REWARD_AGENT_PER_ASSET = range(3)
@@ -36,7 +38,7 @@ class MadiganError(RuntimeError):
 
 
 class AssetSource(C.Structure):
-    _fields_ = [("kind", C.c_int32), ("pad_", C.c_int32), ("p", C.c_double * 12)]
+    _fields_ = [("kind", C.c_int32), ("pad_", C.c_int32), ("p", C.c_double * SRC_PARAMS)]
 
 
 class Config(C.Structure):
@@ -51,6 +53,7 @@ class Config(C.Structure):
         ("action_atoms", C.c_int32), ("unit_size", C.c_double),
         ("nstep", C.c_int32), ("pad2_", C.c_int32), ("discount", C.c_double),
         ("n_feats", C.c_int32), ("pad3_", C.c_int32), ("sortino_exp", C.c_double),
+        ("aux", C.c_int32), ("pad4_", C.c_int32),
     ]
 
 
@@ -66,7 +69,8 @@ VIEW_PTR_FIELDS = ("ledger", "mean_entry", "borrowed", "prices", "sine_x", "ou_m
                    "trend_len", "trend_flags", "cash", "timestamp", "shaper_a", "shaper_b",
                    "ep_stats", "episode_stats", "ext_prices", "units", "asset_idx", "ring",
                    "ring_ts", "ring_head", "ring_len", "win_price", "win_port", "win_ts",
-                   "reset_mask", "nstep_ring", "nstep_len", "nstep_head", "replay_cursor")
+                   "reset_mask", "nstep_ring", "nstep_len", "nstep_head", "replay_cursor",
+                   "aux")
 
 
 class Views(C.Structure):

@@ -21,6 +21,11 @@ Mirrors the reference's config handling for the data sources on the hot path:
   HDFSourceSingle keys (filepath group_key price_key feature_key timestamp_key
               cache_size [start_time end_time])        Config.cpp:551-576,
                                                        DataSource.cpp:227-262
+  SineAdder   keys as Synth (one asset: the sum)        Config.cpp:15-28, DataSource.cpp:582-661
+  SineDynamic keys (freqRange muRange ampRange dX noise) Config.cpp:216-259,
+                                                       DataSource.cpp:678-792
+  SineDynamicTrend + (trendRange trendIncr trendProb)  Config.cpp:261-318,
+                                                       DataSource.cpp:850-992
 Errors follow the reference: missing keys -> RuntimeError (ConfigError),
 mismatched vector lengths -> ValueError (std::length_error), unknown source
 type -> RuntimeError (NotImplemented).
@@ -33,8 +38,10 @@ from typing import Any, List, Optional, Tuple
 from . import _lib as L
 
 SUPPORTED = ("Synth", "OU", "TrendOU", "Composite", "HDFSourceSingle", "SimpleTrend", "TrendyOU",
-             "Gaussian", "SawTooth", "Triangle", "OUPair")
-NOT_YET = ("SineAdder", "SineDynamic", "SineDynamicTrend")
+             "Gaussian", "SawTooth", "Triangle", "OUPair", "SineAdder", "SineDynamic",
+             "SineDynamicTrend")
+NOT_YET = ()
+AUX_KINDS = (L.SRC_SINEADDER, L.SRC_SINEDYNAMIC, L.SRC_SINEDYNTREND)
 HDF_KEYS = ("filepath", "group_key", "feature_key", "timestamp_key", "price_key", "cache_size")
 
 
@@ -161,6 +168,79 @@ def oupair_spec(theta, phi, noise) -> SourceSpec:
                       assets=["OUPair_0", "OUPair_1"])
 
 
+def sineadder_spec(freq, mu, amp, phase, dX, noise=0.0) -> SourceSpec:
+    """SineAdder::initParams (DataSource.cpp:591-661): one asset, "multi_sine",
+    the sum of the components; x starts at phase."""
+    n = _same_len("SineAdder", freq, mu, amp, phase)
+    if not 1 <= n <= 8:
+        raise ValueError(f"SineAdder supports 1..8 components on the MI355X path, got {n}")
+    p = [float(n), float(dX), float(noise)]
+    for v in (freq, mu, amp, phase):
+        p += [float(x) for x in v]
+    return SourceSpec(kinds=[L.SRC_SINEADDER], params=[p], assets=["multi_sine"])
+
+
+def _wave_table_len(sample_rate: int, base_freq: float) -> int:
+    """setSineOsc's table length (WaveTableOsc.h:129-146): the harmonic count
+    sampleRate / (3 baseFreq) + 0.5 (int), rounded up to a power of two by the
+    bit trick (unsigned 32-bit), times 2 * overSample (= 2)."""
+    max_harms = int(sample_rate / (3.0 * base_freq) + 0.5)
+    v = (max_harms - 1) & 0xFFFFFFFF
+    for sh in (1, 2, 4, 8, 16):
+        v |= v >> sh
+    v = (v + 1) & 0xFFFFFFFF
+    return v * 2 * 2
+
+
+def _sine_dynamic_params(name, freqRange, muRange, ampRange, dX, noise):
+    """SineDynamic(Trend)::initParams (DataSource.cpp:742-792, :925-983)."""
+    if not (len(freqRange) == len(muRange) == len(ampRange)):
+        raise ValueError(f"parameters passed to DataSource<PriceVector> of type {name} need to be "
+                         "vectors of same length")
+    C = len(freqRange)
+    if not 1 <= C <= 4:
+        raise ValueError(f"{name} supports 1..4 components on the MI355X path, got {C}")
+    with_dx = float(dX)
+    sample_rate = int(1.0 / with_dx) if with_dx != 0 else None
+    rows = [[float(x) for x in r] for r in (list(freqRange) + list(muRange) + list(ampRange))]
+    if any(len(r) != 3 for r in rows):
+        raise ValueError("freqRange / muRange / ampRange entries are [low, high, step]")
+    for i in range(C):
+        # sampleRate = (int)(1 / dX) must be at least the Nyquist rate (:763-776);
+        # a dX of 0 (the default constructors pass the unset member) fails the same test
+        if sample_rate is None or float(freqRange[i][1]) * 2 > sample_rate:
+            raise RuntimeError("Sampling Rate as determined by 1 / dX must be at least the nyquist "
+                               f"sampling rate relative to the largest frequency. freqRange entry #{i}")
+    p = [float(C), float(sample_rate), float(noise)]
+    p += [float(_wave_table_len(sample_rate, float(freqRange[i][0]))) for i in range(C)]
+    for i in range(C):
+        p += [float(x) for x in freqRange[i]] + [float(x) for x in muRange[i]] + \
+             [float(x) for x in ampRange[i]]
+    return p
+
+
+def sinedynamic_spec(freqRange, muRange, ampRange, dX, noise=0.0) -> SourceSpec:
+    p = _sine_dynamic_params("SineDynamic", freqRange, muRange, ampRange, dX, noise)
+    return SourceSpec(kinds=[L.SRC_SINEDYNAMIC], params=[p], assets=["sine_dynamic"])
+
+
+def sinedynamictrend_spec(freqRange, muRange, ampRange, trendRange, trendIncr, trendProb, dX,
+                          noise=0.0) -> SourceSpec:
+    if not (len(trendRange) == len(trendIncr) == len(trendProb)):
+        raise ValueError("the following parameters passed to DataSource<PriceVector>of type "
+                         "SineDynamicTrend need to be vectors of same length:trendRange\n "
+                         "trendIncr\n trendProb\n")
+    p = _sine_dynamic_params("SineDynamicTrend", freqRange, muRange, ampRange, dX, noise)
+    T = len(trendRange)
+    if T > 2:
+        raise ValueError(f"SineDynamicTrend supports at most 2 trends on the MI355X path, got {T}")
+    p.append(float(T))
+    for t in range(T):
+        p += [float(int(trendRange[t][0])), float(int(trendRange[t][1])), float(trendIncr[t]),
+              float(trendProb[t])]
+    return SourceSpec(kinds=[L.SRC_SINEDYNTREND], params=[p], assets=["sine_dynamic_trend"])
+
+
 def replay_spec(n_assets: int, n_feats: int = 0, assets=None, hdf: Optional[dict] = None) -> SourceSpec:
     """Every asset from a replay tape (HDFSourceSingle, or a tape given directly)."""
     codes = list(assets) if assets is not None else [f"asset_{i}" for i in range(n_assets)]
@@ -207,7 +287,20 @@ def default_spec(source_type: str) -> SourceSpec:
         return gaussian_spec([2., 5., 10., 15.], [1., 1., 2., 5.])
     if source_type == "OUPair":       # DataSource.cpp:1201
         return oupair_spec(.015, .01, .03)
+    if source_type == "SineAdder":    # DataSource.cpp:582-589 (dX member default .01)
+        return sineadder_spec([1., 0.3, 2., 0.5], [2., 2.1, 2.2, 2.3], [1., 1.2, 1.3, 1.],
+                              [0., 1., 2., 1.], 0.01, 0.)
+    if source_type == "SineDynamic":  # DataSource.cpp:678-687: passes the unset member dX (0)
+        return sinedynamic_spec(_SD_FREQ, _SD_MU, _SD_AMP, 0.0, 1.)
+    if source_type == "SineDynamicTrend":  # DataSource.cpp:850-862: same
+        return sinedynamictrend_spec(_SD_FREQ, _SD_MU, _SD_AMP, [[100, 500], [100, 300]],
+                                     [0.1, 0.2], [.001, .01], 0.0, 1.)
     return _not_implemented(source_type)
+
+
+_SD_FREQ = [[.1, 1., .01], [0.3, 3.0, .01], [5., 15., .1], [10., 50., .1]]
+_SD_MU = [[1., 5., .02], [.3, 3., .05], [.2, 5., .02], [.5, 5., .02]]
+_SD_AMP = [[1., 5., .01], [.3, 3., .02], [.2, 2., .04], [.5, 5., .05]]
 
 
 def _not_implemented(source_type: str):
@@ -263,6 +356,20 @@ def spec_from_config(config: Any) -> SourceSpec:
     if source_type == "OUPair":
         _require(params, ("theta", "phi", "noise"))
         return oupair_spec(params["theta"], params["phi"], params["noise"])
+    if source_type == "SineAdder":  # makeSynthConfigFromPyDict (Config.cpp:166-214)
+        _require(params, ("freq", "mu", "amp", "phase", "dX", "noise"))
+        return sineadder_spec(params["freq"], params["mu"], params["amp"], params["phase"],
+                              params["dX"], params["noise"])
+    if source_type == "SineDynamic":  # Config.cpp:216-259
+        _require(params, ("freqRange", "muRange", "ampRange", "dX", "noise"))
+        return sinedynamic_spec(params["freqRange"], params["muRange"], params["ampRange"],
+                                params["dX"], params["noise"])
+    if source_type == "SineDynamicTrend":  # Config.cpp:261-318
+        _require(params, ("freqRange", "muRange", "ampRange", "trendRange", "trendProb",
+                          "trendIncr", "dX", "noise"))
+        return sinedynamictrend_spec(params["freqRange"], params["muRange"], params["ampRange"],
+                                     params["trendRange"], params["trendIncr"],
+                                     params["trendProb"], params["dX"], params["noise"])
     if source_type in ("TrendOU", "TrendyOU"):
         _require(params, ("trend_prob", "min_period", "max_period", "dYMin", "dYMax", "start",
                           "theta", "phi", "noise_trend", "ema_alpha"))
@@ -352,6 +459,7 @@ def build_config(spec: SourceSpec, *, n_envs: int, init_cash: float = 1_000_000.
         if not float(sortino_exp) > 0:
             raise ConfigError(f"sortino_exp must be > 0, got {sortino_exp}")
     c.sortino_exp = float(sortino_exp) if sortino_exp is not None else 2.0
+    c.aux = 1 if any(k in AUX_KINDS for k in spec.kinds) else 0
     srcs = (L.AssetSource * A)()
     for i, (k, p) in enumerate(zip(spec.kinds, spec.params)):
         srcs[i].kind = k

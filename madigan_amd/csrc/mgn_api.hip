@@ -64,7 +64,7 @@ struct Offsets {
   size_t L, mep, Bm, P, sx, oum, dy, tlen, tfl, cash, ts, sA, sB, ep, epstats, ext, units, aidx,
       ring, ring_ts, rhead, rlen, wprice, wport, wts, mask, reward, areward, shaped, done, obsp,
       obsport, obsts, tprice, tunits, tcost, risk, mcall, nshaped, dend, nring, nlen, nhead, disc,
-      src, target, rcur;
+      src, target, rcur, aux;
   size_t total;
 };
 
@@ -123,6 +123,7 @@ Offsets plan(const mgn_config* c) {
   o.src = l.add(A * sizeof(mgn_asset_source));
   o.target = l.add((A + 1) * 8);
   o.rcur = l.add(N * 8);
+  o.aux = l.add(c->aux ? N * A * MGN_AUX_WIDTH * 8 : 0);
   o.total = l.total;
   return o;
 }
@@ -176,9 +177,35 @@ int validate(const mgn_config* c, const mgn_asset_source* s, std::string& msg) {
   }
   for (int i = 0; i < c->n_assets; ++i) {
     const int k = s[i].kind;
-    if (k < MGN_SRC_EXTERNAL || k > MGN_SRC_OUPAIR) {
+    if (k < MGN_SRC_EXTERNAL || k > MGN_SRC_SINEDYNTREND) {
       msg = "unknown data source kind for asset " + std::to_string(i);
       return MGN_ERR_CONFIG;
+    }
+    if (k >= MGN_SRC_SINEADDER) {
+      const int C = (int)s[i].p[0];
+      const int cmax = (k == MGN_SRC_SINEADDER) ? 8 : 4;
+      if (!c->aux) {
+        msg = "multi-component source kinds need mgn_config.aux = 1 (asset " + std::to_string(i) + ")";
+        return MGN_ERR_CONFIG;
+      }
+      if (C < 1 || C > cmax) {
+        msg = "component count out of range for asset " + std::to_string(i);
+        return MGN_ERR_LENGTH;
+      }
+      if (k != MGN_SRC_SINEADDER) {
+        for (int j = 0; j < C; ++j)
+          if (s[i].p[3 + j] < 2.0 || !(s[i].p[1] >= 1.0)) {
+            msg = "wave table length / sample rate invalid for asset " + std::to_string(i);
+            return MGN_ERR_CONFIG;
+          }
+        if (k == MGN_SRC_SINEDYNTREND) {
+          const int T = (int)s[i].p[3 + 10 * C];
+          if (T < 0 || T > 2) {
+            msg = "SineDynamicTrend supports at most 2 trends (asset " + std::to_string(i) + ")";
+            return MGN_ERR_LENGTH;
+          }
+        }
+      }
     }
     if (k == MGN_SRC_OUPAIR) {
       const bool first = s[i].p[3] == 0.0;
@@ -220,10 +247,11 @@ mgn::KParams kparams(const mgn_env* e) {
   p.cash = v.cash; p.ts = v.timestamp; p.sA = v.shaper_a; p.sB = v.shaper_b;
   p.ep = v.ep_stats; p.epstats = v.episode_stats; p.ext = v.ext_prices;
   p.ring = v.ring; p.ring_ts = v.ring_ts; p.rhead = v.ring_head; p.rlen = v.ring_len;
-  p.src = e->src_dev; p.target = e->target_dev;
+  p.src = e->src_dev; p.src_g = e->src_dev; p.target = e->target_dev;
   p.nstep = c.nstep; p.nring = v.nstep_ring; p.nlen = v.nstep_len; p.nhead = v.nstep_head;
   p.disc = e->disc_dev;
   p.rcur = e->v.replay_cursor;
+  p.aux = e->v.aux;
   return p;
 }
 
@@ -248,7 +276,7 @@ void launch_val(const mgn_env* e, double* out);
 // the two-role kernel: one lane per asset per role, padded width 2..8, one-step
 // rewards, generator sources (k_step handles replay tapes and n-step buffers)
 bool duo_eligible(const mgn_env* e) {
-  return e->apad >= 2 && e->apad <= 8 && e->cfg.nstep == 1 && !e->replay;
+  return e->apad >= 2 && e->apad <= 8 && e->cfg.nstep == 1 && !e->replay && !e->cfg.aux;
 }
 // automatic: where the single-role kernel would run one lane per asset (small
 // batches: one wave per SIMD), give every asset a second lane in a partner wave
@@ -390,6 +418,7 @@ int mgn_create(const mgn_config* cfg, const mgn_asset_source* sources, void* str
   v.out.n_shaped = (uint8_t*)(b + o.nshaped);
   v.out.data_end = (uint8_t*)(b + o.dend);
   v.replay_cursor = (int64_t*)(b + o.rcur);
+  v.aux = cfg->aux ? (double*)(b + o.aux) : nullptr;
   v.nstep_ring = cfg->nstep > 1 ? (double*)(b + o.nring) : nullptr;
   v.nstep_len = (int32_t*)(b + o.nlen); v.nstep_head = (int32_t*)(b + o.nhead);
   v.n_envs = e->N; v.n_assets = e->A; v.window = e->W; v.reward_dim = e->D;

@@ -25,7 +25,8 @@
 // (records double-buffered by iteration parity)] barrier.  Each value is
 // the same expression of the same operands as in k_step, so every output is
 // bit-identical to k_step (and to the oracle); only the computing lane differs.
-// Scope: M = 1, APAD = S in {2, 4, 8}, n-step 1, no replay tape (those run k_step).
+// Scope: M = 1, APAD = S in {2, 4, 8}, n-step 1, no replay tape, no multi-component
+// sources (those run k_step).
 // Diagnostic ablation bits (mgn_set_ablation): 1 Broker rounds, 2 generator
 // ticks, 4 the generator side's step finish (outputs).
 #pragma once
@@ -316,9 +317,10 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
                                                         const int8_t* __restrict__ act_in, int K) {
   constexpr int M = 1;
   constexpr int EPB = DUO_HALF / S;  // envs per block
+  constexpr int APADK = S;
   __shared__ DuoShared<S> sh;
   __shared__ EnvRecs<S> recs[EPB];
-  __shared__ mgn_asset_source s_src[MGN_MAX_ASSETS];
+  __shared__ mgn_asset_source s_src[APADK];  // p.A <= APADK assets
   __shared__ double s_tgt[MGN_MAX_ASSETS + 1];
   {
     const double* g = reinterpret_cast<const double*>(p.src);
@@ -399,8 +401,8 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       const double P_prev = s.P[0];
       const uint64_t ts_prev = ts;
       if (live && sh.tick[el]) {
-        if (sh.reset[el]) src_reset<M>(s, p);  // Env::reset -> dataSource->reset (Env.h:183)
-        if (!(p.ablate & 2)) gen_tick<M, false>(s, p, env, ts);
+        if (sh.reset[el]) src_reset<M, false>(s, p, env, ts);  // Env::reset -> dataSource->reset (Env.h:183)
+        if (!(p.ablate & 2)) gen_tick<M, false, false>(s, p, env, ts);
         ts = ts + 1;
         sh.price[l] = s.P[0];
       }

@@ -51,7 +51,8 @@ struct KParams {
   double *ring;
   uint64_t *ring_ts;
   int32_t *rhead, *rlen;
-  const mgn_asset_source *src;  // (A)
+  const mgn_asset_source *src;  // (A); the step kernels point it at an LDS copy
+  const mgn_asset_source *src_g;  // (A) in global memory (the noinline multi-component paths)
   const double *target;         // (A+1)
   // NStepBuffer (n > 1): ring (N,n,D), fill count / oldest index (N), gamma^i (n)
   int nstep;
@@ -66,6 +67,7 @@ struct KParams {
   const uint8_t *rp_end;
   int64_t rp_rows, rp_stride;
   int64_t *rcur;
+  double *aux;  // (N, A, MGN_AUX_WIDTH) multi-component source state
 };
 
 // ---------------------------------------------------------------------------
@@ -195,10 +197,123 @@ struct Lane {
   int64_t row;   // replay: tape row of the current State
 };
 
+// ---------------------------------------------------------------------------
+// multi-component sources (views.aux; restated identically by the oracle)
+
+// WaveTableOsc<double> as setSineOsc fills it (WaveTableOsc.h:104-174): every
+// table holds len samples sin(i*2*pi/len) with sample len = sample 0; the
+// interpolated read (getOutput :84-95) after updatePhase (:31).  Samples are
+// evaluated where read, with the statement the table was built from.
+__device__ __forceinline__ double wt_sample(int i, int len) {
+  if (i == len) i = 0;
+  return 1.0 * det_sin((double)i * 2. * 3.14159265358979323846 / len);
+}
+__device__ __forceinline__ double wt_process(double& phasor, double incr, int len) {
+  phasor += incr;
+  if (phasor >= 1.) phasor -= 1.;
+  const double temp = phasor * len;
+  const int ip = (int)temp;
+  const double frac = temp - ip;
+  const double s0 = wt_sample(ip, len), s1 = wt_sample(ip + 1, len);
+  return s0 + (s1 - s0) * frac;
+}
+// std::max(lo, std::min(hi, v))
+__device__ __forceinline__ double clamp_range(double lo, double hi, double v) {
+  const double m = (v < hi) ? v : hi;
+  return (lo < m) ? m : lo;
+}
+// SineDynamic(Trend)::updateParams (DataSource.cpp:802-813, :1002-1015)
+__device__ __noinline__ void sd_update(const double* q, double* ax, uint32_t bits) {
+  const int C = (int)q[0];
+  for (int c = 0; c < C; ++c) {
+    const double* r = q + 3 + C + 9 * c;
+    double* a = ax + 4 * c;
+    a[2] = clamp_range(r[3], r[4], a[2] + (((bits >> (3 * c)) & 1) ? r[5] : -r[5]));
+    a[3] = clamp_range(r[6], r[7], a[3] + (((bits >> (3 * c + 1)) & 1) ? r[8] : -r[8]));
+    a[1] = clamp_range(r[0], r[1], a[1] + (((bits >> (3 * c + 2)) & 1) ? r[2] : -r[2]));
+  }
+}
+// freq, mu, amp ~ U[lo, hi] per component (initParams :777-782, reset :794-800)
+__device__ __noinline__ void sd_sample(const double* q, double* ax, uint64_t seed, uint64_t genv,
+                                       uint32_t asset, uint64_t tick) {
+  const int C = (int)q[0];
+  for (int c = 0; c < C; ++c) {
+    const double* r = q + 3 + C + 9 * c;
+    const u4 x = block(seed, genv, asset, 16u + (uint32_t)c, tick);
+    ax[4 * c + 1] = (r[1] - r[0]) * ((double)x.x * TWO_M32) + r[0];
+    ax[4 * c + 2] = (r[4] - r[3]) * ((double)x.y * TWO_M32) + r[3];
+    ax[4 * c + 3] = (r[7] - r[6]) * ((double)x.z * TWO_M32) + r[6];
+  }
+}
+// SineAdder::getData (DataSource.cpp:663-673)
+__device__ __noinline__ double sineadder_tick(const double* q, double* ax, uint64_t seed,
+                                              uint64_t genv, uint32_t asset, uint64_t tick) {
+  const int C = (int)q[0];
+  const double PI2 = 3.141592653589793238463 * 2;
+  double sum = 0.;
+  for (int c = 0; c < C; ++c) {
+    double nz = 0.0;  // component c's noise: the block of counter slot c
+    if (q[2] != 0.0) nz = draw_s(seed, genv, asset, (uint32_t)c, tick).z * q[2] + 0.0;
+    sum += (nz + q[3 + C + c]) + q[3 + 2 * C + c] * det_sin(PI2 * ax[c] * q[3 + c]);
+    ax[c] += q[1];
+  }
+  return sum;
+}
+// SineDynamic::getData (DataSource.cpp:829-841) / SineDynamicTrend::getData (:1017-1047)
+__device__ __noinline__ double sinedyn_tick(const double* q, double* ax, bool trend, uint64_t seed,
+                                            uint64_t genv, uint32_t asset, uint64_t tick) {
+  const int C = (int)q[0];
+  const u4 x0 = block(seed, genv, asset, 0, tick);
+  sd_update(q, ax, x0.w);
+  double tc = ax[16];
+  double sum = 0.;
+  for (int c = 0; c < C; ++c) {
+    double* a = ax + 4 * c;
+    const double out = wt_process(a[0], a[1] / q[1], (int)q[3 + c]);  // setFreq(freq / sampleRate)
+    if (trend) sum += tc * (a[2] + a[3] * out);
+    else sum += a[2] + a[3] * out;
+  }
+  double nz = 0.0;
+  if (q[2] != 0.0) nz = draw_from(x0).z * q[2] + 0.0;
+  if (!trend) return sum + nz;
+  const double* tq = q + 3 + 10 * C;  // T, then per trend {minLen, maxLen, incr, prob}
+  const int T = (int)tq[0];
+  u4 x1 = {0u, 0u, 0u, 0u};
+  bool have1 = false;
+  for (int t = 0; t < T; ++t) {
+    const double* r = tq + 1 + 4 * t;
+    double* st = ax + 17 + 3 * t;  // trending, direction, length
+    if (st[0] != 0.) {
+      tc += (tc * r[2]) * st[1];
+      st[2] -= 1.;
+      if (st[2] == 0.) st[0] = 0.;
+    } else {
+      if (!have1) {
+        x1 = block(seed, genv, asset, 1, tick);
+        have1 = true;
+      }
+      const double u = (double)(t == 0 ? x1.x : x1.y) * TWO_M32;
+      if (u < r[3]) {
+        st[0] = 1.;
+        st[1] = ((x0.w >> (12 + t)) & 1) ? -1. : 1.;
+        const int lo = (int)r[0], hi = (int)r[1];
+        const int len = lo + (int)(((double)(t == 0 ? x1.z : x1.w) * TWO_M32) * (double)(hi - lo + 1));
+        st[2] = (double)(len > hi ? hi : len);
+      }
+    }
+    if (tc <= .1) st[1] = 1.;
+    tc = (0.01 < tc) ? tc : 0.01;
+  }
+  ax[16] = tc;
+  return (sum + tc) + tc * nz;
+}
+
 // DataSource::getData for the lane's slots (DataSource.cpp:535-543, 1173-1180,
 // 1457-1493; Composite concatenation :439-451) ; tick = timestamp before ++.
-// RP: the kernel may serve a replay tape (k_step); the two-role kernel never does
-template <int M, bool RP = true>
+// RP: the kernel may serve a replay tape (k_step); AUX: multi-component kinds
+// (views.aux).  The two-role kernel compiles neither (their calls would cost
+// the hot generator registers) and is not selected for such handles.
+template <int M, bool RP = true, bool AUX = true>
 __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, uint64_t tick) {
   if (RP && p.replay) {
     // HDFSourceSingle::getData (DataSource.cpp:391-398) on the tape: the
@@ -333,6 +448,12 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
       x += (q[0] * (mean - x)) + mean * z;
       s.P[m] = x;
       s.oum[m] = mean;
+    } else if (AUX && kind == MGN_SRC_SINEADDER) {
+      s.P[m] = sineadder_tick(p.src_g[a].p, p.aux + ((size_t)env * p.A + a) * MGN_AUX_WIDTH, p.seed, genv,
+                              (uint32_t)a, tick);
+    } else if (AUX && (kind == MGN_SRC_SINEDYNAMIC || kind == MGN_SRC_SINEDYNTREND)) {
+      s.P[m] = sinedyn_tick(p.src_g[a].p, p.aux + ((size_t)env * p.A + a) * MGN_AUX_WIDTH,
+                            kind == MGN_SRC_SINEDYNTREND, p.seed, genv, (uint32_t)a, tick);
     } else {
       s.P[m] = p.ext[(size_t)env * p.A + a];
     }
@@ -368,8 +489,8 @@ __device__ __forceinline__ void put_feats(const Lane<M>& s, const KParams& p, in
 
 // source reset (DataSource.h:466, :232; DataSource.cpp:1495-1502; the replay
 // source carries on, DataSource.cpp:200-206)
-template <int M>
-__device__ __forceinline__ void src_reset(Lane<M>& s, const KParams& p) {
+template <int M, bool AUX = true>
+__device__ __forceinline__ void src_reset(Lane<M>& s, const KParams& p, int env, uint64_t tick) {
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     if (!s.valid[m]) continue;
@@ -393,6 +514,9 @@ __device__ __forceinline__ void src_reset(Lane<M>& s, const KParams& p) {
     } else if (kind == MGN_SRC_OUPAIR) {       // DataSource.cpp:1246-1250
       s.P[m] = 10.;
       s.oum[m] = 10.;
+    } else if (AUX && (kind == MGN_SRC_SINEDYNAMIC || kind == MGN_SRC_SINEDYNTREND)) {  // :794-800, :994-1000
+      sd_sample(p.src_g[s.asset[m]].p, p.aux + ((size_t)env * p.A + s.asset[m]) * MGN_AUX_WIDTH, p.seed,
+                (uint64_t)(p.env_offset + env), (uint32_t)s.asset[m], tick);
     }
   }
 }
@@ -423,7 +547,7 @@ __device__ __forceinline__ void ring_push(const Lane<M>& s, const KParams& p, in
 template <int M, int S>
 __device__ __forceinline__ void env_reset(Lane<M>& s, const KParams& p, int env, int ls,
                                           double& cash, uint64_t& ts, int32_t& head, int32_t& len) {
-  src_reset<M>(s, p);
+  src_reset<M>(s, p, env, ts);
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     s.L[m] = 0.;
@@ -1047,13 +1171,14 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
   p.cos_temp = in_vgpr(p.cos_temp);
   p.unit_size = in_vgpr(p.unit_size);
   constexpr int EPB = BLOCK / S;  // envs per block
+  constexpr int APADK = M * S;
   // exchange-form Broker rounds (LDS: M * 28 KB per block)
   constexpr bool XCH = (M * S <= 16) && (M <= 2) && (S >= 2);
   __shared__ EnvRecs<XCH ? M * S : 1> recs[XCH ? EPB : 1];
   // loop-invariant tables read every step (generator parameters, PPC target,
   // n-step discounts) are staged in LDS: a global load in the step loop would
   // expose its full latency to the single resident wave
-  __shared__ mgn_asset_source s_src[MGN_MAX_ASSETS];
+  __shared__ mgn_asset_source s_src[APADK];  // p.A <= APADK assets
   __shared__ double s_tgt[MGN_MAX_ASSETS + 1];
   __shared__ double s_disc[NST ? MGN_MAX_NSTEP : 1];
   {
@@ -1352,7 +1477,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
       if (done && p.auto_reset) {
         // Env::reset (Env.h:181-187): source reset + fresh Broker; its getData
         // and initialize_history's no-action ticks run as pending ticks
-        src_reset<M>(s, p);
+        src_reset<M>(s, p, env, ts);
 #pragma unroll
         for (int m = 0; m < M; ++m) {
           s.L[m] = 0.;
@@ -1443,6 +1568,16 @@ __global__ __launch_bounds__(BLOCK) void k_init_reset(KParams p, int mode,
       else if (kd == MGN_SRC_OUPAIR) {
         s.P[m] = 10.;
         s.oum[m] = 10.;
+      } else if (kd == MGN_SRC_SINEADDER) {  // DataSource.cpp:645-661: x = phase
+        double* ax = p.aux + ((size_t)env * p.A + a) * MGN_AUX_WIDTH;
+        const int C = (int)q[0];
+        for (int c = 0; c < C; ++c) ax[c] = q[3 + 3 * C + c];
+      } else if (kd == MGN_SRC_SINEDYNAMIC || kd == MGN_SRC_SINEDYNTREND) {  // :742-792, :925-992
+        double* ax = p.aux + ((size_t)env * p.A + a) * MGN_AUX_WIDTH;
+        for (int k = 0; k < MGN_AUX_WIDTH; ++k) ax[k] = 0.;
+        sd_sample(p.src_g[a].p, ax, p.seed, (uint64_t)(p.env_offset + env), (uint32_t)a, 0);
+        ax[16] = 1.;                                    // trendComponent
+        for (int t = 0; t < 2; ++t) ax[18 + 3 * t] = 1.;  // currentDirection
       }
     }
     ts = 0;

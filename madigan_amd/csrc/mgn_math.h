@@ -173,9 +173,7 @@ struct Draw {
   uint32_t dbit;
 };
 
-__device__ __forceinline__ Draw draw_s(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot,
-                                      uint64_t tick) {
-  const u4 x = block(seed, env, asset, slot, tick);
+__device__ __forceinline__ Draw draw_from(const u4& x) {
   const uint64_t a = (((uint64_t)x.y << 32) | x.x) >> 11;
   const double u1 = (double)(a + 1) * TWO_M53;
   const double u2 = (double)x.z * TWO_M32;
@@ -184,6 +182,11 @@ __device__ __forceinline__ Draw draw_s(uint64_t seed, uint64_t env, uint32_t ass
   d.ut = (double)x.w * TWO_M32;
   d.dbit = x.x & 1u;
   return d;
+}
+
+__device__ __forceinline__ Draw draw_s(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot,
+                                      uint64_t tick) {
+  return draw_from(block(seed, env, asset, slot, tick));
 }
 
 __device__ __forceinline__ Draw draw0(uint64_t seed, uint64_t env, uint32_t asset, uint64_t tick) {

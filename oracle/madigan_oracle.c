@@ -314,6 +314,7 @@ struct orc_batch {
   int N, A;
   orc_env *envs;
   double *ext;  /* (N,A) external prices */
+  double *aux;  /* (N,A,ORC_AUX_WIDTH) multi-component source state, or NULL */
   orc_ring ring; /* StackerDiscrete deques (preprocessor.py:150-152), F, P = A+1 */
   int F;         /* State.price width: A, or the replay source's feature count */
   int replay;
@@ -497,6 +498,72 @@ static const double *state_price(const orc_batch *b, const orc_env *s) {
   return b->replay ? s->feat : s->P;
 }
 
+/* the raw Philox block of counter slot `slot` */
+static void block_slot(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot, uint64_t tick,
+                       uint32_t x[4]) {
+  uint32_t ctr[4] = {(uint32_t)tick, (uint32_t)env, asset | (slot << 16),
+                     (uint32_t)(tick >> 32) ^ (uint32_t)(env >> 32)};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  orc_philox4x32_10(ctr, key, x);
+}
+
+/* WaveTableOsc<double> of setSineOsc (WaveTableOsc.h:104-174): every table of
+ * the oscillator holds the same len samples sin(i*2*pi/len) (scale stays 1),
+ * with sample len = sample 0; the interpolated read of getOutput (:84-95)
+ * after updatePhase (:31).  Samples are evaluated where read, with the
+ * statement the table was built from. */
+static double wt_sample(int i, int len) {
+  if (i == len) i = 0;
+  return 1.0 * orc_sin((double)i * 2. * 3.14159265358979323846 / len);
+}
+static double wt_process(double *phasor, double incr, int len) {
+  *phasor += incr;
+  if (*phasor >= 1.) *phasor -= 1.;
+  double temp = *phasor * len;
+  int ip = (int)temp;
+  double frac = temp - ip;
+  double s0 = wt_sample(ip, len), s1 = wt_sample(ip + 1, len);
+  return s0 + (s1 - s0) * frac;
+}
+static double clampd(double lo, double hi, double v) { /* std::max(lo, std::min(hi, v)) */
+  double m = (v < hi) ? v : hi;
+  return (lo < m) ? m : lo;
+}
+
+/* SineDynamic(Trend)::updateParams (DataSource.cpp:802-813, :1002-1015): a
+ * +-step random walk of mu, amp, freq per component, clamped to the ranges;
+ * the steps' signs are bits 3c, 3c+1, 3c+2 of the slot-0 block's word 3 */
+static void sd_update(const double *p, double *ax, uint32_t bits) {
+  int C = (int)p[0];
+  for (int c = 0; c < C; ++c) {
+    const double *r = p + 3 + C + 9 * c;  /* freqRange, muRange, ampRange */
+    double *a = ax + 4 * c;             /* phasor, freq, mu, amp */
+    a[2] = clampd(r[3], r[4], a[2] + (((bits >> (3 * c)) & 1) ? r[5] : -r[5]));
+    a[3] = clampd(r[6], r[7], a[3] + (((bits >> (3 * c + 1)) & 1) ? r[8] : -r[8]));
+    a[1] = clampd(r[0], r[1], a[1] + (((bits >> (3 * c + 2)) & 1) ? r[2] : -r[2]));
+  }
+}
+/* freq, mu, amp of every component ~ U[lo, hi] (initParams :777-782, reset
+ * :794-800), from the slot 16 + c block of the tick */
+static void sd_sample(const double *p, double *ax, uint64_t seed, uint64_t env, uint32_t asset,
+                      uint64_t tick) {
+  int C = (int)p[0];
+  for (int c = 0; c < C; ++c) {
+    const double *r = p + 3 + C + 9 * c;
+    uint32_t x[4];
+    block_slot(seed, env, asset, 16u + (uint32_t)c, tick, x);
+    ax[4 * c + 1] = (r[1] - r[0]) * ((double)x[0] * TWO_M32) + r[0];
+    ax[4 * c + 2] = (r[4] - r[3]) * ((double)x[1] * TWO_M32) + r[3];
+    ax[4 * c + 3] = (r[7] - r[6]) * ((double)x[2] * TWO_M32) + r[6];
+  }
+}
+static double normal_of(const uint32_t x[4]) {
+  uint64_t a = (((uint64_t)x[1] << 32) | x[0]) >> 11;
+  double u1 = (double)(a + 1) * TWO_M53;
+  double u2 = (double)x[2] * TWO_M32;
+  return sqrt(-2.0 * orc_log(u1)) * orc_cos2pi(u2);
+}
+
 static void src_get_data(orc_batch *b, int e) {
   orc_env *s = &b->envs[e];
   if (b->replay) {
@@ -658,6 +725,76 @@ static void src_get_data(orc_batch *b, int e) {
         }
         break;
       }
+      case ORC_SRC_SINEADDER: { /* SineAdder::getData, DataSource.cpp:663-673 */
+        double *ax = b->aux + ((size_t)e * b->A + i) * ORC_AUX_WIDTH;
+        const int C = (int)p[0];
+        const double PI2 = 3.141592653589793238463 * 2;
+        double sum = 0.;
+        for (int c = 0; c < C; ++c) {
+          double nz = 0.0;  /* component c's noise: the block of counter slot c */
+          if (p[2] != 0.0) {
+            double z, u;
+            uint32_t bb;
+            draw_slot(seed, genv, (uint32_t)i, (uint32_t)c, tick, &z, &u, &bb);
+            nz = z * p[2] + 0.0;
+          }
+          sum += (nz + p[3 + C + c]) + p[3 + 2 * C + c] * orc_sin(PI2 * ax[c] * p[3 + c]);
+          ax[c] += p[1];
+        }
+        s->P[i] = sum;
+        break;
+      }
+      case ORC_SRC_SINEDYNAMIC:    /* SineDynamic::getData, DataSource.cpp:829-841 */
+      case ORC_SRC_SINEDYNTREND: { /* SineDynamicTrend::getData, :1017-1047 */
+        double *ax = b->aux + ((size_t)e * b->A + i) * ORC_AUX_WIDTH;
+        const int C = (int)p[0];
+        const int trend = b->src[i].kind == ORC_SRC_SINEDYNTREND;
+        uint32_t x0[4];
+        block_slot(seed, genv, (uint32_t)i, 0, tick, x0);
+        sd_update(p, ax, x0[3]);
+        double tc = ax[16];
+        double sum = 0.;
+        for (int c = 0; c < C; ++c) {
+          double *a = ax + 4 * c;
+          double out = wt_process(&a[0], a[1] / p[1], (int)p[3 + c]);  /* setFreq(freq / sampleRate) */
+          if (trend) sum += tc * (a[2] + a[3] * out);
+          else sum += a[2] + a[3] * out;
+        }
+        double nz = 0.0;
+        if (p[2] != 0.0) nz = normal_of(x0) * p[2] + 0.0;
+        if (!trend) {
+          s->P[i] = sum + nz;
+          break;
+        }
+        const double *tp = p + 3 + 10 * C;  /* T, then per trend {minLen, maxLen, incr, prob} */
+        const int T = (int)tp[0];
+        uint32_t x1[4];
+        int have1 = 0;
+        for (int t = 0; t < T; ++t) {
+          const double *q = tp + 1 + 4 * t;
+          double *st = ax + 17 + 3 * t;  /* trending, direction, length */
+          if (st[0] != 0.) {
+            tc += (tc * q[2]) * st[1];
+            st[2] -= 1.;
+            if (st[2] == 0.) st[0] = 0.;
+          } else {
+            if (!have1) { block_slot(seed, genv, (uint32_t)i, 1, tick, x1); have1 = 1; }
+            double u = (double)x1[t] * TWO_M32;
+            if (u < q[3]) {
+              st[0] = 1.;
+              st[1] = ((x0[3] >> (12 + t)) & 1) ? -1. : 1.;
+              int lo = (int)q[0], hi = (int)q[1];
+              int len = lo + (int)(((double)x1[2 + t] * TWO_M32) * (double)(hi - lo + 1));
+              st[2] = (double)(len > hi ? hi : len);
+            }
+          }
+          if (tc <= .1) st[1] = 1.;
+          tc = (0.01 < tc) ? tc : 0.01;
+        }
+        ax[16] = tc;
+        s->P[i] = (sum + tc) + tc * nz;
+        break;
+      }
       default: /* external replay: prices supplied via orc_set_prices */
         s->P[i] = b->ext[(size_t)e * b->A + i];
         break;
@@ -688,7 +825,11 @@ static void src_reset(orc_batch *b, int e) {
       case ORC_SRC_OUPAIR:      /* DataSource.cpp:1246-1250 */
         s->P[i] = 10.; s->ouMean[i] = 10.;
         break;
-      default: break;           /* Synth family, OU, Gaussian: no-op */
+      case ORC_SRC_SINEDYNAMIC: case ORC_SRC_SINEDYNTREND:  /* :794-800, :994-1000 */
+        sd_sample(p, b->aux + ((size_t)e * b->A + i) * ORC_AUX_WIDTH, b->cfg.seed,
+                  (uint64_t)(b->cfg.env_offset + e), (uint32_t)i, s->ts);
+        break;
+      default: break;           /* Synth family, SineAdder, OU, Gaussian: no-op */
     }
   }
 }
@@ -713,6 +854,22 @@ static void src_init(orc_batch *b, int e) {
       case ORC_SRC_GAUSSIAN: s->P[i] = p[0]; break;                     /* :1067 */
       case ORC_SRC_SAWTOOTH: case ORC_SRC_TRIANGLE: s->x[i] = p[3]; s->P[i] = 0.0; break;
       case ORC_SRC_OUPAIR: s->P[i] = 10.; s->ouMean[i] = 10.; break;   /* :1191-1196 */
+      case ORC_SRC_SINEADDER: {                                         /* :645-661: x = phase */
+        double *ax = b->aux + ((size_t)e * b->A + i) * ORC_AUX_WIDTH;
+        const int C = (int)p[0];
+        for (int c = 0; c < C; ++c) ax[c] = p[3 + 3 * C + c];
+        s->P[i] = 0.0;
+        break;
+      }
+      case ORC_SRC_SINEDYNAMIC: case ORC_SRC_SINEDYNTREND: {            /* :742-792, :925-992 */
+        double *ax = b->aux + ((size_t)e * b->A + i) * ORC_AUX_WIDTH;
+        for (int k = 0; k < ORC_AUX_WIDTH; ++k) ax[k] = 0.;
+        sd_sample(p, ax, b->cfg.seed, (uint64_t)(b->cfg.env_offset + e), (uint32_t)i, 0);
+        ax[16] = 1.;                                                    /* trendComponent */
+        for (int t = 0; t < 2; ++t) ax[18 + 3 * t] = 1.;                /* currentDirection */
+        s->P[i] = 0.0;
+        break;
+      }
       default: s->P[i] = 0.0; break;
     }
   }
@@ -919,6 +1076,9 @@ orc_batch *orc_create(const orc_config *cfg, const orc_asset_src *srcs) {
   b->replay = srcs[0].kind == ORC_SRC_REPLAY;
   b->F = (b->replay && cfg->n_feats > 0) ? cfg->n_feats : b->A;
   b->ext = (double *)calloc((size_t)b->N * b->A, sizeof(double));
+  for (int i = 0; i < b->A; ++i)
+    if (srcs[i].kind >= ORC_SRC_SINEADDER && !b->aux)
+      b->aux = (double *)calloc((size_t)b->N * b->A * ORC_AUX_WIDTH, sizeof(double));
   {
     int D = (cfg->reward_mode == ORC_REWARD_AGENT_PER_ASSET) ? b->A : 1;
     b->nring = (double *)calloc((size_t)b->N * cfg->nstep * D, sizeof(double));
@@ -989,6 +1149,7 @@ void orc_destroy(orc_batch *b) {
   free(b->ring.ring); free(b->ring.ring_ts); free(b->ring.head); free(b->ring.len);
   free(b->envs);
   free(b->ext);
+  free(b->aux);
   free(b->rp_price); free(b->rp_feat); free(b->rp_ts);
   free(b->nring);
   free(b->nlen);

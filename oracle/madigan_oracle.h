@@ -38,7 +38,10 @@ enum { ORC_GREEN = 0, ORC_INSUFF_MARGIN = 1, ORC_MARGIN_CALL = 2, ORC_BLOWN_OUT 
 enum { ORC_SRC_EXTERNAL = 0, ORC_SRC_SINE = 1, ORC_SRC_OU = 2, ORC_SRC_TRENDOU = 3,
        ORC_SRC_REPLAY = 4 /* HDFSourceSingle over in-memory arrays (all assets) */,
        ORC_SRC_SIMPLETREND = 5, ORC_SRC_TRENDYOU = 6, ORC_SRC_GAUSSIAN = 7,
-       ORC_SRC_SAWTOOTH = 8, ORC_SRC_TRIANGLE = 9, ORC_SRC_OUPAIR = 10 };
+       ORC_SRC_SAWTOOTH = 8, ORC_SRC_TRIANGLE = 9, ORC_SRC_OUPAIR = 10,
+       ORC_SRC_SINEADDER = 11, ORC_SRC_SINEDYNAMIC = 12, ORC_SRC_SINEDYNTREND = 13 };
+#define ORC_SRC_PARAMS 64   /* doubles of parameters per asset */
+#define ORC_AUX_WIDTH 24    /* doubles of extra source state per asset (multi-component kinds) */
 
 /* reward shapers (nstep_buffer.py:378-408) */
 enum { ORC_SHAPER_NONE = 0, ORC_SHAPER_DSR = 1, ORC_SHAPER_DDR = 2, ORC_SHAPER_PPC = 3,
@@ -67,11 +70,19 @@ enum { ORC_STEP_NONE = 0, ORC_STEP_UNITS = 1, ORC_STEP_SINGLE = 2 };
  *  SAWTOOTH / TRIANGLE p = as SINE
  *  OUPAIR      p = {theta, phi, noise, role}: role 0 / 1 = first / second
  *              asset of the pair, adjacent in asset order
+ *  SINEADDER   p = {C, dX, noise, freq[C], mu[C], amp[C], phase[C]}, C <= 8
+ *  SINEDYNAMIC p = {C, sampleRate, noise, tableLen[C], then per component
+ *              freqRange[3], muRange[3], ampRange[3]}, C <= 4
+ *  SINEDYNTREND p = SINEDYNAMIC's, then {T, per trend: minLen, maxLen, incr,
+ *              prob}, T <= 2
+ *  aux state (ORC_AUX_WIDTH per asset): SINEADDER x[C]; SINEDYNAMIC per
+ *  component {phasor, freq, mu, amp}; SINEDYNTREND also [16] trendComponent,
+ *  per trend [17+3t] trending, [18+3t] direction, [19+3t] remaining length
  */
 typedef struct {
   int32_t kind;
   int32_t pad_;
-  double p[12];
+  double p[ORC_SRC_PARAMS];
 } orc_asset_src;
 
 typedef struct {

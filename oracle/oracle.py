@@ -21,7 +21,8 @@ MAXA = 64
 
 GREEN, INSUFF_MARGIN, MARGIN_CALL, BLOWN_OUT = 0, 1, 2, 3
 (SRC_EXTERNAL, SRC_SINE, SRC_OU, SRC_TRENDOU, SRC_REPLAY, SRC_SIMPLETREND, SRC_TRENDYOU,
- SRC_GAUSSIAN, SRC_SAWTOOTH, SRC_TRIANGLE, SRC_OUPAIR) = range(11)
+ SRC_GAUSSIAN, SRC_SAWTOOTH, SRC_TRIANGLE, SRC_OUPAIR, SRC_SINEADDER, SRC_SINEDYNAMIC,
+ SRC_SINEDYNTREND) = range(14)
 SHAPERS = {"none": 0, None: 0, "None": 0, "sum_default": 0, "DSR": 1, "DDR": 2, "PPC": 3,
            "cosine": 3, "cosine_similarity": 3, "cosine_port_shaper": 3, "sharpe_shaper": 4,
            "sortino_shaperA": 5, "sortino_shaperB": 6}
@@ -38,7 +39,7 @@ S_NAMES = ["cash", "equity", "pnl", "balance", "availableMargin", "usedMargin", 
 
 
 class AssetSrc(C.Structure):
-    _fields_ = [("kind", C.c_int32), ("pad_", C.c_int32), ("p", C.c_double * 12)]
+    _fields_ = [("kind", C.c_int32), ("pad_", C.c_int32), ("p", C.c_double * 64)]
 
 
 class Config(C.Structure):

@@ -60,3 +60,8 @@ def oupair_sources(theta=0.015, phi=0.01, noise=0.03):
 
 def wave_sources(kind, freq, mu, amp, phase, dX=0.01, noise=0.0):
     return [(kind, [f, m, a, p, dX, noise]) for f, m, a, p in zip(freq, mu, amp, phase)]
+
+
+def sources_from_spec(spec):
+    """the oracle's (kind, params) list of a madigan_amd SourceSpec"""
+    return [(k, list(p)) for k, p in zip(spec.kinds, spec.params)]

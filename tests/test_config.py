@@ -69,7 +69,7 @@ def test_defaults_match_reference_default_constructors():
 
 
 def test_unsupported_sources_raise_runtime_error():
-    with pytest.raises(RuntimeError, match="not implemented"):
+    with pytest.raises(RuntimeError, match="nyquist"):  # default ctor passes dX = 0 (DataSource.cpp:686)
         default_spec("SineDynamic")
     with pytest.raises(RuntimeError, match="not implemented"):
         spec_from_config({"data_source_type": "Bogus", "data_source_config": {}})

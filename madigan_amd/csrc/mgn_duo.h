@@ -242,6 +242,7 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
   const double cash0 = cash;
   int go = 0, mc = 0, insuff = 0;
   double cend = cash0;
+  double lv[4][S];  // this lane's leaves of the last (consistent) pass
   for (int it = 0; it <= S; ++it) {
     // cash before this lane's order, and after the last order, under the guess
     double c = cash0, c_own = cash0;
@@ -256,7 +257,6 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
     cend = c;
     // canonical sums before this lane's order: leaves of executed earlier
     // orders after the order, the others before
-    double lv[4][S];
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       const bool post = (j < ls) && ((go_bits >> j) & 1);
@@ -289,22 +289,20 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
   any_mc = seg_or<S>(act & mc) != 0;
   rk[0] = act ? (mc ? MGN_MARGIN_CALL : (insuff ? MGN_INSUFF_MARGIN : MGN_GREEN)) : rk[0];
   const bool go_own[1] = {go != 0};
-  // the post-transaction sums: every leaf at its final value
-  double lv[4][S];
-#pragma unroll
-  for (int j = 0; j < S; ++j) {
-    const bool post = (go_bits >> j) & 1;
-    const d2* rv = reinterpret_cast<const d2*>(&er.r[j]) + (post ? 2 : 0);
+  // the post-transaction sums: the last lane's leaves are final but its own;
+  // settle that one and broadcast its trees to the segment
+  if (ls == S - 1 && go) {
+    const d2* rv = reinterpret_cast<const d2*>(&er.r[S - 1]) + 2;
     const d2 a = rv[0], b = rv[1];
-    lv[0][j] = a.x;
-    lv[1][j] = a.y;
-    lv[2][j] = b.x;
-    lv[3][j] = b.y;
+    lv[0][S - 1] = a.x;
+    lv[1][S - 1] = a.y;
+    lv[2][S - 1] = b.x;
+    lv[3][S - 1] = b.y;
   }
-  after.lp = tree<S>(lv[0]);
-  after.ml = tree<S>(lv[1]);
-  after.sh = tree<S>(lv[2]);
-  after.b = tree<S>(lv[3]);
+  after.lp = seg_bcast<S, S - 1>(tree<S>(lv[0]));
+  after.ml = seg_bcast<S, S - 1>(tree<S>(lv[1]));
+  after.sh = seg_bcast<S, S - 1>(tree<S>(lv[2]));
+  after.b = seg_bcast<S, S - 1>(tree<S>(lv[3]));
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   apply_orders<1>(s, go_own, cu2, me2, bm3, tpr, tco, uc, tp, tu, tc);

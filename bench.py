@@ -214,7 +214,7 @@ def kernel_name(env, A: int) -> str:
     apad = 1 << max(0, (A - 1).bit_length())
     rq1 = "true" if env.cfg.required_margin == 1.0 else "false"
     if int(env.lib.mgn_get_schedule(env.h)) == L.SCHED_DUO:
-        return f"mgn::k_step_duo<{apad}, {rq1}>"
+        return f"mgn::k_step_duo<{apad}, {rq1}, false>"
     nst = "true" if env.nstep > 1 else "false"
     return f"mgn::k_step<{m}, {apad // m}, {rq1}, {nst}>"
 

@@ -308,7 +308,9 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
   apply_orders<1>(s, go_own, cu2, me2, bm3, tpr, tco, uc, tp, tu, tc);
 }
 
-template <int S, bool RQ1>
+// ABL: the diagnostic ablation build (mgn_set_ablation != 0); the product
+// instantiation carries no ablation branches
+template <int S, bool RQ1, bool ABL>
 __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out, int in_kind,
                                                         const double* __restrict__ units_in,
                                                         const int32_t* __restrict__ aidx_in,
@@ -400,14 +402,14 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       const uint64_t ts_prev = ts;
       if (live && sh.tick[el]) {
         if (sh.reset[el]) src_reset<M, false>(s, p, env, ts);  // Env::reset -> dataSource->reset (Env.h:183)
-        if (!(p.ablate & 2)) gen_tick<M, false, false>(s, p, env, ts);
+        if (!(ABL && (p.ablate & 2))) gen_tick<M, false, false>(s, p, env, ts);
         ts = ts + 1;
         sh.price[l] = s.P[0];
       }
       if (threadIdx.x == 0) sh.more[(j + 1) % 3] = 0;
       __syncthreads();  // A: prices of tick j published
       // phase 2: finish step j-1 (its State: the price and time before tick j)
-      if (live && j > 0 && !(p.ablate & 4))
+      if (live && j > 0 && !(ABL && (p.ablate & 4)))
         duo_finish<S>(sh.rec[(j - 1) & 1], s, p, ov, om, in_kind, env, el, l, ls, P_prev, ts_prev,
                       need_ar, g);
       __syncthreads();  // B: record j published
@@ -500,7 +502,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
         uc[0] = (s.valid[0] && s.asset[0] == ai) ? u : 0.;
       }
       prevVal = s.L[0] * s.P[0];
-      if (in_kind != IN_NONE && !(p.ablate & 1)) {
+      if (in_kind != IN_NONE && !(ABL && (p.ablate & 1))) {
         broker_spec<S, RQ1>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, sa, any_mc);
         mcall = margin_call(sa, cash, p.mainM) ? 1 : 0;  // Broker.cpp:156-157
       }

@@ -34,8 +34,13 @@ void launch_duo(const StepArgs& a) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(DUO_BLOCK), 0, a.stream, a.p, a.out, a.in_kind,
                        a.units, a.aidx, a.act, a.K);
   };
-  if (a.p.reqm_one) go(k_step_duo<S, true>);
-  else go(k_step_duo<S, false>);
+  if (a.p.ablate) {
+    if (a.p.reqm_one) go(k_step_duo<S, true, true>);
+    else go(k_step_duo<S, false, true>);
+  } else {
+    if (a.p.reqm_one) go(k_step_duo<S, true, false>);
+    else go(k_step_duo<S, false, false>);
+  }
 }
 
 template <int M, int S>

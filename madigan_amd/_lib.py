@@ -129,11 +129,13 @@ SYMBOLS = {
 _lib = None
 
 
-def load(path: str = LIB_PATH):
-    """Load the HIP extension (no GPU needed to load it)."""
+def load(path: str = ""):
+    """Load the HIP extension (no GPU needed to load it).  MADIGAN_LIB_PATH
+    selects a diagnostic build of the same sources (tools/build_variant.py)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("MADIGAN_LIB_PATH") or LIB_PATH
     if not os.path.exists(path):
         raise ImportError(
             f"{path} is missing: build it with `python -m madigan_amd.build` "

@@ -36,6 +36,15 @@
 namespace mgn {
 
 constexpr int DUO_BLOCK = 512;
+
+#ifdef MGN_STAMPS
+// diagnostic build only: per role, cycles of [work 1, wait A, work 2, wait B]
+// summed over one wave per role and block, then the iteration count
+__device__ unsigned long long g_duo_stamps[16];
+#define MGN_T(v) v = __builtin_amdgcn_s_memtime()
+#else
+#define MGN_T(v)
+#endif
 constexpr int DUO_HALF = DUO_BLOCK / 2;
 
 enum { REC_STEP = 1, REC_TICK = 2, REC_DONE = 4, REC_MCALL = 8 };
@@ -212,6 +221,10 @@ __device__ __forceinline__ void duo_finish(const DuoRec<S>& sh, const Lane<1>& s
     }
   }
 }
+
+#ifndef MGN_DUO_VAR
+#define MGN_DUO_VAR 0
+#endif
 
 // Broker::handleTransaction(units) for a segment of S lanes, one asset per
 // lane, resolved speculatively.  The serial dependency between orders (each
@@ -396,7 +409,15 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
     p.ring = vptr(p.ring);
     p.ring_ts = vptr(p.ring_ts);
     int j = 0;
+#ifdef MGN_STAMPS
+    unsigned long long T0 = 0, T1 = 0, T2 = 0, T3 = 0, T4 = 0, acc[4] = {0, 0, 0, 0};
+#endif
     for (;; ++j) {
+      MGN_T(T0);
+      // issue priority to the role on the critical path of the phase: the
+      // ledger's orders in phase 1, the generator's step finish in phase 2
+      // (VALU issue between the two waves of a SIMD goes by priority, then age)
+      __builtin_amdgcn_s_setprio(0);
       // phase 1: tick j
       const double P_prev = s.P[0];
       const uint64_t ts_prev = ts;
@@ -407,14 +428,28 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
         sh.price[l] = s.P[0];
       }
       if (threadIdx.x == 0) sh.more[(j + 1) % 3] = 0;
+      MGN_T(T1);
       __syncthreads();  // A: prices of tick j published
+      MGN_T(T2);
+      __builtin_amdgcn_s_setprio(2);
       // phase 2: finish step j-1 (its State: the price and time before tick j)
       if (live && j > 0 && !(ABL && (p.ablate & 4)))
         duo_finish<S>(sh.rec[(j - 1) & 1], s, p, ov, om, in_kind, env, el, l, ls, P_prev, ts_prev,
                       need_ar, g);
+      MGN_T(T3);
       __syncthreads();  // B: record j published
+      MGN_T(T4);
+#ifdef MGN_STAMPS
+      acc[0] += T1 - T0; acc[1] += T2 - T1; acc[2] += T3 - T2; acc[3] += T4 - T3;
+#endif
       if (!sh.more[j % 3]) break;
     }
+#ifdef MGN_STAMPS
+    if (threadIdx.x == 0) {
+      for (int i = 0; i < 4; ++i) atomicAdd(&g_duo_stamps[i], acc[i]);
+      atomicAdd(&g_duo_stamps[8], (unsigned long long)j);
+    }
+#endif
     if (!live) return;
     duo_finish<S>(sh.rec[j & 1], s, p, ov, om, in_kind, env, el, l, ls, s.P[0], ts, need_ar, g);
     if (s.valid[0]) {
@@ -465,7 +500,17 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
 
   int k = 0;
   int pending = 0;
+#ifdef MGN_STAMPS
+  unsigned long long T0 = 0, T1 = 0, T2 = 0, T3 = 0, T4 = 0, acc[4] = {0, 0, 0, 0};
+  unsigned long long Ta = 0, Tb = 0, accb[2] = {0, 0};
+  int jn = 0;
+#endif
   for (int j = 0;; ++j) {
+    MGN_T(T0);
+#ifdef MGN_STAMPS
+    jn = j;
+#endif
+    __builtin_amdgcn_s_setprio(2);
     const bool stepping = live && (pending == 0) && (k < K);
     const bool ticking = live && (stepping || (pending > 0));
     const size_t oN = (size_t)k * p.N, oNA = (size_t)k * p.N * A;
@@ -502,12 +547,21 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
         uc[0] = (s.valid[0] && s.asset[0] == ai) ? u : 0.;
       }
       prevVal = s.L[0] * s.P[0];
+      MGN_T(Ta);
       if (in_kind != IN_NONE && !(ABL && (p.ablate & 1))) {
         broker_spec<S, RQ1>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, sa, any_mc);
         mcall = margin_call(sa, cash, p.mainM) ? 1 : 0;  // Broker.cpp:156-157
       }
+      MGN_T(Tb);
+#ifdef MGN_STAMPS
+      accb[0] += Ta - T0;
+      accb[1] += Tb - Ta;
+#endif
     }
+    MGN_T(T1);
     __syncthreads();  // A: the prices of tick j are in LDS
+    MGN_T(T2);
+    __builtin_amdgcn_s_setprio(0);
     bool reset_now = false;
     int flags = 0;
     DuoRec<S>& rc = sh.rec[j & 1];
@@ -587,9 +641,23 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       sh.reset[el] = reset_now ? 1 : 0;
     }
     if (next_tick) sh.more[j % 3] = 1;
+    MGN_T(T3);
     __syncthreads();  // B: record j published
+    MGN_T(T4);
+#ifdef MGN_STAMPS
+    acc[0] += T1 - T0; acc[1] += T2 - T1; acc[2] += T3 - T2; acc[3] += T4 - T3;
+#endif
     if (!sh.more[j % 3]) break;
   }
+#ifdef MGN_STAMPS
+  if (threadIdx.x == DUO_HALF) {
+    for (int i = 0; i < 4; ++i) atomicAdd(&g_duo_stamps[4 + i], acc[i]);
+    atomicAdd(&g_duo_stamps[9], (unsigned long long)jn);
+    atomicAdd(&g_duo_stamps[10], 1ull);
+    atomicAdd(&g_duo_stamps[11], accb[0]);
+    atomicAdd(&g_duo_stamps[12], accb[1]);
+  }
+#endif
 
   if (!live) return;
   if (s.valid[0]) {

@@ -1,3 +1,11 @@
 // launchers for APAD = 8 (see mgn_launch.h)
 #include "mgn_launch_impl.h"
 MGN_DEFINE_APAD(8)
+#ifdef MGN_STAMPS
+extern "C" int mgn_diag_stamps(unsigned long long* h) {
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(mgn::g_duo_stamps), 16 * sizeof(unsigned long long)) != hipSuccess)
+    return 1;
+  unsigned long long z[16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(mgn::g_duo_stamps), z, sizeof(z)) != hipSuccess;
+}
+#endif

@@ -1,0 +1,46 @@
+"""Build a diagnostic variant of libmadigan_hip.so with extra defines.
+
+    python tools/build_variant.py NAME [-DMGN_STAMPS ...]
+
+Recompiles mgn_api.hip and mgn_launch_a8.hip (the A = 8 step kernels) with the
+extra flags, links them with the product objects of the other APAD units into
+tools/_var/NAME/libmadigan_hip.so; select it with MADIGAN_LIB_PATH.  Development
+tool only: the product library is madigan_amd/libmadigan_hip.so.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from madigan_amd import build as B  # noqa: E402
+
+
+def main():
+    name, extra = sys.argv[1], sys.argv[2:]
+    B.build()
+    out_dir = os.path.join(ROOT, "tools", "_var", name)
+    os.makedirs(out_dir, exist_ok=True)
+    cc = B.hipcc()
+    redo = {"mgn_api.hip", "mgn_launch_a8.hip"}
+
+    def one(src):
+        base = os.path.basename(src)
+        if base not in redo:
+            return os.path.join(B.OBJ, base.replace(".hip", ".o"))
+        obj = os.path.join(out_dir, base.replace(".hip", ".o"))
+        subprocess.run([cc, *B.FLAGS, *extra, "-c", "-o", obj, src], check=True)
+        return obj
+
+    with ThreadPoolExecutor(4) as ex:
+        objs = list(ex.map(one, B.sources()))
+    lib = os.path.join(out_dir, "libmadigan_hip.so")
+    subprocess.run([cc, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", lib, *objs], check=True)
+    print(lib)
+
+
+if __name__ == "__main__":
+    main()

@@ -55,7 +55,7 @@ struct DuoRec {
   static constexpr int EPB = DUO_HALF / S;
   double rL[DUO_HALF], rPrev[DUO_HALF], rTp[DUO_HALF], rTu[DUO_HALF], rTc[DUO_HALF];
   int32_t rRk[DUO_HALF];
-  double rPrevEq[EPB], rCurEq[EPB], rCash[EPB], rLp[EPB], rB[EPB];
+  double rPrevEq[EPB], rCurEq[EPB], rCash[EPB], rLp[EPB], rB[EPB], rRew[EPB];
   int32_t rK[EPB], rFlags[EPB];
 };
 
@@ -112,6 +112,7 @@ __device__ __forceinline__ mgn_traj traj_vgpr(const mgn_traj& o) {
 // nstep_buffer.py n = 1, preprocessor.py:172-175)
 struct GenOut {
   double shA, shB, ep_ret, ep_len, cos_qn;
+  DdrPre ddr;  // DDR's reward-independent operands, from the current A, B
   int32_t head, len;
 };
 
@@ -137,16 +138,14 @@ __device__ __forceinline__ void duo_finish(const DuoRec<S>& sh, const Lane<1>& s
     const double qb = sh.rB[el];
     const double tp = sh.rTp[l], tu = sh.rTu[l], tc = sh.rTc[l];
     const bool done = (flags & REC_DONE) != 0;
-    const double ratio = curEq / prevEq;
-    const double clampv = (in_kind == IN_SINGLE) ? 0.01 : 0.3;
-    const double reward = log((ratio < clampv) ? clampv : ratio);
+    const double reward = sh.rRew[el];  // the ledger side's log(max(curEq / prevEq, clamp))
     double ar[M];
     ar[0] = 0.;
     if (valid && need_ar) {
       double v = (((Lc * P) - sh.rPrev[l]) - (tu * tp + tc)) / prevEq;
       v += 1;
       v = (v < .35) ? .35 : v;
-      ar[0] = log(v);
+      ar[0] = log_ratio(v);
     }
     double cos_term = 0.;
     if (p.shaper == MGN_SHAPER_PPC) {
@@ -164,7 +163,16 @@ __device__ __forceinline__ void duo_finish(const DuoRec<S>& sh, const Lane<1>& s
     double shaped_s = 0., rin_s = 0., shaped_v = 0.;
     if (D == 1) {
       rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
-      shaped_s = shape(p.shaper, rin_s, g.shA, g.shB, p.eta, cos_term, p.sexp);
+      if (p.shaper == MGN_SHAPER_DDR) {  // shape() for DDR (nstep_buffer.py:128-162) on g.ddr
+        const double r = rin_s;
+        shaped_s = clip1((0.0 + 1.0 * ddr_one_pre(r, g.shA, g.shB, g.ddr)) / 1);
+        double m = r < 0. ? r : 0.;
+        if (r != r) m = r;
+        g.shA += p.eta * (r - g.shA);
+        g.shB += p.eta * (m * m - g.shB);
+      } else {
+        shaped_s = shape(p.shaper, rin_s, g.shA, g.shB, p.eta, cos_term, p.sexp);
+      }
     } else {
       shaped_v = valid ? shape(p.shaper, ar[0], g.shA, g.shB, p.eta, cos_term, p.sexp) : 0.;
     }
@@ -427,6 +435,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
         ts = ts + 1;
         sh.price[l] = s.P[0];
       }
+      if (D == 1 && p.shaper == MGN_SHAPER_DDR) g.ddr = ddr_pre(g.shA, g.shB);
       if (threadIdx.x == 0) sh.more[(j + 1) % 3] = 0;
       MGN_T(T1);
       __syncthreads();  // A: prices of tick j published
@@ -451,6 +460,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
     }
 #endif
     if (!live) return;
+    if (D == 1 && p.shaper == MGN_SHAPER_DDR) g.ddr = ddr_pre(g.shA, g.shB);
     duo_finish<S>(sh.rec[j & 1], s, p, ov, om, in_kind, env, el, l, ls, s.P[0], ts, need_ar, g);
     if (s.valid[0]) {
       const size_t i = (size_t)env * A + s.asset[0];
@@ -575,6 +585,11 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
         q.lp = canon<M, S>(tlp);
       }
       const double curEq = (cash + q.lp) - q.b;
+      // Env.h:211-212 (0.01 clamp for step(i, u), Env.h:238); on this side, whose
+      // phase 2 has slack, for the generator side's step finish
+      const double ratio = curEq / prevEq;
+      const double clampv = (in_kind == IN_SINGLE) ? 0.01 : 0.3;
+      const double reward = log_ratio((ratio < clampv) ? clampv : ratio);
       const bool done = any_mc || margin_call(q, cash, p.mainM) || (curEq < 0.1 * p.init_cash);
       rc.rL[l] = s.L[0];
       rc.rPrev[l] = prevVal;
@@ -604,6 +619,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       if (ls == 0) {
         rc.rPrevEq[el] = prevEq;
         rc.rCurEq[el] = curEq;
+        rc.rRew[el] = reward;
         rc.rCash[el] = cash;
         rc.rLp[el] = q.lp;
         rc.rB[el] = q.b;

@@ -1006,6 +1006,22 @@ __device__ __forceinline__ double ddr_one(double r, double A, double B) {
   const double den = (pos ? sB : B * sB) + 1.1920928955078125e-07;
   return num / den;
 }
+// ddr_one with its reward-independent operands (A/2 and the two
+// denominators) evaluated ahead of the reward: the same operations on the
+// same operands, so the same result
+struct DdrPre {
+  double hA, dpos, dneg;
+};
+__device__ __forceinline__ DdrPre ddr_pre(double A, double B) {
+  const double sB = sqrt(B);
+  return DdrPre{A / 2, sB + 1.1920928955078125e-07, B * sB + 1.1920928955078125e-07};
+}
+__device__ __forceinline__ double ddr_one_pre(double r, double A, double B, const DdrPre& q) {
+  const double h = r - q.hA;
+  const bool pos = r > 0.;
+  const double num = pos ? h : (B * h - (A * (r * r)) / 2);
+  return num / (pos ? q.dpos : q.dneg);
+}
 __device__ __forceinline__ double clip1(double v) { return v < -1. ? -1. : (v > 1. ? 1. : v); }
 
 // naive shapers (nstep_buffer.py:207-312), benchmark 0.  x**e and x**(1/e) as
@@ -1344,7 +1360,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
       const double curEq = (cash + q.lp) - q.b;
       const double ratio = curEq / prevEq;
       const double clampv = (in_kind == IN_SINGLE) ? 0.01 : 0.3;
-      const double reward = log((ratio < clampv) ? clampv : ratio);
+      const double reward = log_ratio((ratio < clampv) ? clampv : ratio);
       int bad = 0;
       if constexpr (XCH) {
         bad = any_mc;  // every lane saw every round's risk
@@ -1372,7 +1388,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
         double v = (((s.L[m] * s.P[m]) - prevVal[m]) - (tu[m] * tp[m] + tc[m])) / prevEq;
         v += 1;
         v = (v < .35) ? .35 : v;
-        ar[m] = (p.ablate & 8) ? v : log(v);
+        ar[m] = (p.ablate & 8) ? v : log_ratio(v);
       }
       // ---- reward shaping
       double cos_term = 0.;

@@ -199,11 +199,15 @@ def workload_env(name, N, A, rank, dev):
     raise SystemExit(f"unknown workload {name}")
 
 
-def gather_bytes(env) -> float:
-    """Algorithmic bytes of one window gather launch: per env read the ring
-    W*(F+A+1)*8 + its timestamps W*8, write the same (price, portfolio, ts)."""
-    C = env.F + env.A + 1
-    return env.N * 2.0 * env.W * (C + 1) * 8
+def gather_bytes(env, K: int) -> float:
+    """Algorithmic bytes of one k_hist_gather launch (K windows per env): write
+    every step's window, W*(F+A+2)*8 per env-step (price, portfolio,
+    timestamps), and read each history row once, (W + K)*(F+A+2)*8 per env
+    (the window before the launch plus one row per step; reset refill rows,
+    which add to it, are not counted).  The kernel re-reads the rows that
+    consecutive windows share; those re-reads are not algorithmic bytes."""
+    C1 = env.F + env.A + 2
+    return env.N * 8.0 * C1 * (K * env.W + env.W + K)
 
 
 def kernel_name(env, A: int) -> str:
@@ -225,6 +229,8 @@ def main():
     ap.add_argument("--steps", type=int, default=2048)
     ap.add_argument("--warmup", type=int, default=256)
     ap.add_argument("--fuse", type=int, default=64)
+    ap.add_argument("--win-fuse", type=int, default=64,
+                    help="steps per launch of the windowed workloads (capped by --fuse)")
     ap.add_argument("--n-envs", type=int, default=8192, help="envs per GPU")
     ap.add_argument("--assets", type=int, default=8)
     ap.add_argument("--layout", type=int, default=0, help="assets per lane (0 = auto)")
@@ -362,42 +368,61 @@ def main():
 
 
 def windowed(args, world, rank, dev):
-    """C2 / C4 / C5: per step one K = 1 step launch + the window gather."""
+    """C2 / C4 / C5: per launch `fuse` steps, each followed by its window
+    (StackerDiscrete.current_data) -- mgn_rollout_hist (the K steps, every
+    ring push kept in the launch history) then mgn_window_hist (all K windows
+    to (K,N,W,·)).  Every step's window is materialised, as the agent reads one
+    per step."""
     import torch
     import torch.distributed as dist
     wl = args.workload
     N = {"C2": 4096}.get(wl, args.n_envs)
     A = {"C2": 4, "C4": 8, "C5": 16}[wl]
     env, desc, W = workload_env(wl, N, A, rank, dev)
+    Kf = max(1, min(args.fuse, args.win_fuse))
+    n_warm = max(1, -(-args.warmup // Kf))
+    n_time = max(1, -(-args.steps // Kf))
+    args.warmup, args.steps = n_warm * Kf, n_time * Kf
     total = args.warmup + args.steps
     actions = env.generate_actions(total, seed=0x6D6164)
-    traj = env.alloc_traj(1, fields=["reward", "shaped", "done", "obs_price", "obs_port",
-                                     "timestamp", "tprice", "tunits", "tcost", "risk",
-                                     "margin_call", "data_end"])
+    traj = env.alloc_traj(Kf, fields=["reward", "shaped", "done", "obs_price", "obs_port",
+                                      "timestamp", "tprice", "tunits", "tcost", "risk",
+                                      "margin_call", "data_end"])
+    wp = torch.empty((Kf, N, W, env.F), dtype=torch.float64, device=dev)
+    wo = torch.empty((Kf, N, W, A + 1), dtype=torch.float64, device=dev)
+    wt = torch.empty((Kf, N, W), dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
+    # one ctypes call per kernel group, arguments built once
+    import ctypes as C
+    from madigan_amd import _lib as L
+    lib, h = env.lib, env.h
+    tstruct = C.byref(env._traj_struct(traj))
+    per = env.N * env.A
+    base = actions.data_ptr()
+    wptr = [C.c_void_p(x.data_ptr()) for x in (wp, wo, wt)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(n_time)] for _ in range(3)]
 
-    def run(k0, k1, ev=None):
-        for k in range(k0, k1):
+    def run(l0, l1, ev=None):
+        rc = 0
+        for l in range(l0, l1):
             if ev is not None:
-                ev[0].append(torch.cuda.Event(enable_timing=True))
-                ev[0][-1].record(stream)
-            env.rollout(actions[k:k + 1], out=traj)
+                ev[0][l - l0].record(stream)
+            rc |= lib.mgn_rollout_hist(h, C.c_void_p(base + l * Kf * per), Kf, tstruct)
             if ev is not None:
-                ev[1].append(torch.cuda.Event(enable_timing=True))
-                ev[1][-1].record(stream)
-            env.window()
+                ev[1][l - l0].record(stream)
+            rc |= lib.mgn_window_hist(h, *wptr)
             if ev is not None:
-                ev[2].append(torch.cuda.Event(enable_timing=True))
-                ev[2][-1].record(stream)
+                ev[2][l - l0].record(stream)
+        L.check(rc, h)
 
-    run(0, args.warmup)
+    run(0, n_warm)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ev = ([], [], [])
+    ev = evs
     t0 = time.perf_counter()
-    run(args.warmup, total, ev)
+    run(n_warm, n_warm + n_time, ev)
     stats = env.episode_stats
     if world > 1:
         gathered = torch.empty((world * N, 4), dtype=torch.float64, device=dev)
@@ -415,7 +440,7 @@ def windowed(args, world, rank, dev):
         elapsed = float(t.item())
     step_us = float(np.mean([a.elapsed_time(b) for a, b in zip(ev[0], ev[1])])) * 1e3
     gather_us = float(np.mean([b.elapsed_time(c) for b, c in zip(ev[1], ev[2])])) * 1e3
-    gb = gather_bytes(env)
+    gb = gather_bytes(env, Kf)
     achieved = gb / (gather_us * 1e-6) / 1e9
     value = world * N * args.steps / elapsed
     if rank == 0:
@@ -426,16 +451,16 @@ def windowed(args, world, rank, dev):
             "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": desc, "n_envs_per_gpu": N, "n_assets": A, "n_feats": env.F,
-                       "window": W, "steps_per_launch": 1,
+                       "window": W, "steps_per_launch": Kf,
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                          "traffic": load_pmc_traffic(f"{wl}_gather_{N}x{A}_W{W}"),
-                         "kernel": "mgn::k_ring_gather_elem" if env.cfg.norm_type != 3
-                         else "mgn::k_ring_gather",
-                         "bytes_per_env_step": 2.0 * W * (C + 1) * 8,
+                         "kernel": "mgn::k_hist_gather",
+                         "bytes_per_env_step": gb / (N * Kf),
                          "avg_launch_us": gather_us},
-            "step_kernel_avg_us": step_us,
+            "step_launch_avg_us": step_us,
+            "step_launch_note": "history prefix copy + the K-step step kernel",
             "episodes_completed": int(gathered[:, 3].sum().item()),
         }
         if wl == "C5":

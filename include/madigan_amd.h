@@ -260,6 +260,19 @@ int mgn_window_push(mgn_env *env, const double *price_dev, const double *port_de
 int mgn_window_clear(mgn_env *env, const uint8_t *mask_dev);
 /* StackerDiscrete.current_data into caller buffers (NULL: views.win_*) */
 int mgn_window(mgn_env *env, double *price_dev, double *port_dev, uint64_t *ts_dev);
+/* the agent loop of a windowed env with K steps in one launch: every step k
+ * of mgn_rollout (offpolicy_q.py:143 env.step) followed by
+ * preprocessor.stream_state / current_data (offpolicy_q.py:193-194,
+ * preprocessor.py:172-189).  mgn_rollout_hist runs the K steps and keeps
+ * every ring push of the launch in a handle-owned history (W + K*(W+1) rows
+ * per env, allocated on first use); mgn_window_hist then writes all K windows
+ * to (K,N,W,F) / (K,N,W,A+1) / (K,N,W) caller buffers (any may be NULL;
+ * element-wise normalisers only).  mgn_rollout_window: per_step 1 = both;
+ * per_step 0 = mgn_rollout + mgn_window (the last window only). */
+int mgn_rollout_hist(mgn_env *env, const int8_t *actions_dev, int32_t k_steps, const mgn_traj *out);
+int mgn_window_hist(mgn_env *env, double *price_dev, double *port_dev, uint64_t *ts_dev);
+int mgn_rollout_window(mgn_env *env, const int8_t *actions_dev, int32_t k_steps, const mgn_traj *out,
+                       double *price_dev, double *port_dev, uint64_t *ts_dev, int32_t per_step);
 /* uniform discrete actions U{0..atoms-1} (K,N,A) from Philox (benchmark input) */
 int mgn_generate_actions(mgn_env *env, int8_t *actions_dev, int32_t k_steps, uint64_t seed);
 /* Portfolio accessors for every env into out_dev (N,10): {cash, equity, pnl,

@@ -109,6 +109,10 @@ SYMBOLS = {
     "mgn_window_push": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mgn_window_clear": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mgn_window": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mgn_rollout_hist": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(Traj)]),
+    "mgn_window_hist": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mgn_rollout_window": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(Traj),
+                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32]),
     "mgn_generate_actions": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_uint64]),
     "mgn_valuation": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mgn_set_broker": (C.c_int, [C.c_void_p] + [C.c_double] * 6),

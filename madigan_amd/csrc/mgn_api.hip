@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <new>
 #include <string>
 
@@ -16,6 +17,12 @@
 #include "mgn_launch.h"
 
 namespace {
+
+// window gather: LDS staging per workgroup (bytes)
+constexpr size_t kGatherLdsTarget = 40 * 1024;
+constexpr size_t kGatherLdsBudget = 64 * 1024;
+// launch-history gather: windows (steps) per workgroup
+constexpr int kHistStepsPerGroup = 16;
 
 thread_local std::string g_error;
 
@@ -56,6 +63,15 @@ struct mgn_env {
   int m = 1;  // assets per lane
   int sched = MGN_SCHED_AUTO;  // requested step schedule
   bool duo = false;            // the two-role kernel runs the steps
+  // launch history (mgn_rollout_hist): grown on demand, owned by the handle
+  double* hist = nullptr;
+  uint64_t* hist_ts = nullptr;
+  int32_t* hend = nullptr;
+  int32_t* hlen = nullptr;
+  size_t hist_rows_cap = 0, hist_k_cap = 0;
+  int hist_rows = 0;  // rows per env of the last mgn_rollout_hist
+  int hist_k = 0;     // its step count (0: none yet)
+  bool hist_on = false;  // kparams() hands the history to the step kernel
 };
 
 namespace {
@@ -252,6 +268,11 @@ mgn::KParams kparams(const mgn_env* e) {
   p.disc = e->disc_dev;
   p.rcur = e->v.replay_cursor;
   p.aux = e->v.aux;
+  p.hist = e->hist_on ? e->hist : nullptr;
+  p.hist_ts = e->hist_ts;
+  p.hend = e->hend;
+  p.hlen = e->hlen;
+  p.hrows = e->hist_rows;
   return p;
 }
 
@@ -335,6 +356,17 @@ void launch_gather(const mgn::RingDesc& r, double* price, double* port, uint64_t
     const int64_t threads = (int64_t)r.N * C;
     hipLaunchKernelGGL(mgn::k_ring_gather, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
                        stream, r, price, port, ts);
+  } else if (r.W % 2 == 0 && (size_t)r.W * (C + 1) * 8 <= kGatherLdsBudget) {
+    // LDS-staged: envs per workgroup so the staged rows fill ~40 KB (4 per CU)
+    const size_t per_env = (size_t)r.W * (C + 1) * 8;
+    mgn::GatherLds g;
+    g.epb = (int)std::min<size_t>(64, std::max<size_t>(1, kGatherLdsTarget / per_env));
+    g.inv_f = 1.0f / (float)r.F;
+    g.inv_p = 1.0f / (float)r.Pn;
+    g.inv_w = 1.0f / (float)r.W;
+    const unsigned blocks = (unsigned)((r.N + g.epb - 1) / g.epb);
+    hipLaunchKernelGGL(mgn::k_ring_gather_lds, dim3(blocks), dim3(256), per_env * g.epb, stream,
+                       r, price, port, ts, g);
   } else if ((int64_t)r.N * r.W * C < ((int64_t)1 << 31) && r.W % 2 == 0) {
     const uint32_t pairs = (uint32_t)((int64_t)r.N * r.W * C / 2);
     const uint32_t per_block = 256 * mgn::GATHER_U;
@@ -460,6 +492,10 @@ int mgn_destroy(mgn_env* e) {
   if (!e) return MGN_ERR_ARG;
   (void)hipStreamSynchronize(e->stream);
   if (e->own_arena) (void)hipFree(e->arena);
+  if (e->hist) (void)hipFree(e->hist);
+  if (e->hist_ts) (void)hipFree(e->hist_ts);
+  if (e->hend) (void)hipFree(e->hend);
+  if (e->hlen) (void)hipFree(e->hlen);
   delete e;
   return MGN_OK;
 }
@@ -565,6 +601,92 @@ int mgn_window(mgn_env* e, double* price_dev, double* port_dev, uint64_t* ts_dev
   launch_gather(ring_desc(e), price_dev ? price_dev : e->v.win_price,
                 port_dev ? port_dev : e->v.win_port, ts_dev ? ts_dev : e->v.win_ts, e->stream);
   return check_hip(e, hipGetLastError(), "mgn_window");
+}
+
+int mgn_rollout_hist(mgn_env* e, const int8_t* actions_dev, int32_t k_steps, const mgn_traj* out) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  if (!actions_dev || !out) return fail(e, MGN_ERR_ARG, "null actions/out");
+  if (k_steps < 1) return fail(e, MGN_ERR_LENGTH, "k_steps must be >= 1");
+  if (e->W == 0) return fail(e, MGN_ERR_CONFIG, "handle has no window (window_length = 0)");
+  if (e->W % 2) return fail(e, MGN_ERR_CONFIG, "the launch history needs an even window length");
+  if (k_steps > mgn::HIST_KMAX) return fail(e, MGN_ERR_LENGTH, "the launch history holds at most 64 steps");
+  if (need_tape(e) != MGN_OK) return MGN_ERR_CONFIG;
+  const int C = e->F + e->A + 1;
+  const size_t rows = (size_t)e->W + (size_t)k_steps * (e->W + 1);
+  if ((size_t)e->N * rows * C >= ((size_t)1 << 31))
+    return fail(e, MGN_ERR_LENGTH, "launch history exceeds 2^31 elements: fewer steps per call");
+  if (rows > e->hist_rows_cap) {  // grow (first use / more steps): synchronous
+    (void)hipStreamSynchronize(e->stream);
+    if (e->hist) (void)hipFree(e->hist);
+    if (e->hist_ts) (void)hipFree(e->hist_ts);
+    e->hist = nullptr;
+    e->hist_ts = nullptr;
+    e->hist_rows_cap = 0;
+    int st = check_hip(e, hipMalloc((void**)&e->hist, (size_t)e->N * rows * C * 8), "history alloc");
+    if (st == MGN_OK) st = check_hip(e, hipMalloc((void**)&e->hist_ts, (size_t)e->N * rows * 8), "history alloc");
+    if (st != MGN_OK) return st;
+    e->hist_rows_cap = rows;
+  }
+  if ((size_t)k_steps > e->hist_k_cap) {
+    (void)hipStreamSynchronize(e->stream);
+    if (e->hend) (void)hipFree(e->hend);
+    if (e->hlen) (void)hipFree(e->hlen);
+    e->hend = nullptr;
+    e->hlen = nullptr;
+    e->hist_k_cap = 0;
+    int st = check_hip(e, hipMalloc((void**)&e->hend, (size_t)k_steps * e->N * 4), "history alloc");
+    if (st == MGN_OK) st = check_hip(e, hipMalloc((void**)&e->hlen, (size_t)k_steps * e->N * 4), "history alloc");
+    if (st != MGN_OK) return st;
+    e->hist_k_cap = (size_t)k_steps;
+  }
+  e->hist_rows = (int)rows;
+  const mgn::RingDesc r = ring_desc(e);
+  const int64_t pt = (int64_t)e->N * e->W * C;
+  hipLaunchKernelGGL(mgn::k_hist_prefix, dim3((unsigned)((pt + 255) / 256)), dim3(256), 0, e->stream,
+                     r, e->hist, e->hist_ts, (int)rows);
+  e->hist_on = true;
+  launch_step(e, *out, mgn::IN_DISCRETE, nullptr, nullptr, actions_dev, (int)k_steps);
+  e->hist_on = false;
+  e->hist_k = k_steps;
+  return check_hip(e, hipGetLastError(), "mgn_rollout_hist");
+}
+
+int mgn_window_hist(mgn_env* e, double* price_dev, double* port_dev, uint64_t* ts_dev) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  if (e->hist_k == 0) return fail(e, MGN_ERR_CONFIG, "no mgn_rollout_hist to gather from");
+  if (!price_dev && !port_dev && !ts_dev) return MGN_OK;
+  const int C = e->F + e->A + 1;
+  mgn::HistDesc h;
+  h.N = e->N; h.F = e->F; h.Pn = e->A + 1; h.W = e->W; h.K = e->hist_k; h.hrows = e->hist_rows;
+  h.norm = e->cfg.norm_type;
+  h.prelog = e->cfg.norm_type == MGN_NORM_LOG;
+  h.hist = e->hist; h.hist_ts = e->hist_ts; h.hend = e->hend; h.hlen = e->hlen;
+  if (h.norm == MGN_NORM_STANDARD_NORMAL || h.norm == MGN_NORM_LOG_STANDARD_NORMAL)
+    return fail(e, MGN_ERR_CONFIG, "mgn_window_hist: element-wise normalisers only (none, log, lookback, lookback_log)");
+  if (h.K > mgn::HIST_KMAX) return fail(e, MGN_ERR_LENGTH, "mgn_window_hist: at most 64 steps per launch history");
+  // LDS rows: the window before the launch, one row per step and one reset's
+  // refill; a longer span reads the history directly
+  const int ks = std::min(h.K, kHistStepsPerGroup);
+  const int kb = (h.K + ks - 1) / ks;
+  const int lds_rows = std::min(e->W + ks + (e->W + 1), (int)(kGatherLdsBudget / ((size_t)(C + 1) * 8)));
+  const size_t lds = (size_t)lds_rows * (C + 1) * 8;
+  const float wf = (float)(e->W * e->F), wp = (float)(e->W * (e->A + 1));
+  hipLaunchKernelGGL(mgn::k_hist_gather, dim3((unsigned)(e->N * kb)), dim3(256), lds, e->stream, h,
+                     price_dev, port_dev, ts_dev, ks, lds_rows, 1.0f / (float)e->F, 1.0f / (float)(e->A + 1),
+                     1.0f / (float)e->W, 1.0f / wf, 1.0f / wp);
+  return check_hip(e, hipGetLastError(), "mgn_window_hist");
+}
+
+int mgn_rollout_window(mgn_env* e, const int8_t* actions_dev, int32_t k_steps, const mgn_traj* out,
+                       double* price_dev, double* port_dev, uint64_t* ts_dev, int32_t per_step) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  if (per_step) {
+    if (!price_dev || !port_dev) return fail(e, MGN_ERR_ARG, "per_step windows need caller price/port buffers");
+    const int st = mgn_rollout_hist(e, actions_dev, k_steps, out);
+    return st != MGN_OK ? st : mgn_window_hist(e, price_dev, port_dev, ts_dev);
+  }
+  const int st = mgn_rollout(e, actions_dev, k_steps, out);
+  return st != MGN_OK ? st : mgn_window(e, price_dev, port_dev, ts_dev);
 }
 
 int mgn_generate_actions(mgn_env* e, int8_t* actions_dev, int32_t k_steps, uint64_t seed) {

@@ -215,6 +215,272 @@ __global__ __launch_bounds__(BLOCK) void k_ring_gather_elem(RingDesc r, double* 
   }
 }
 
+// current_data for the element-wise normalisers, LDS-staged: a workgroup owns
+// `epb` consecutive envs, whose ring rows (epb, W, C) and timestamps (epb, W)
+// are one contiguous range of the arena each, and whose outputs price
+// (epb, W, F), portfolio (epb, W, P) and timestamps (epb, W) are contiguous
+// too.  Phase 1 copies the ring range into LDS with 16-B loads (U in flight
+// per lane); phase 2 walks the three outputs in 16-B pairs, each element read
+// from LDS at its logical row (head - len + 1 + w) mod W, normalised, and
+// stored coalesced.  Every HBM byte is read once and written once with full
+// 16-B accesses.  Local indices are < 2^24, so the divisions are one fp32
+// reciprocal multiply plus a correction.
+__device__ __forceinline__ void divmod_small(uint32_t n, uint32_t d, float inv, uint32_t& q,
+                                             uint32_t& r) {
+  q = (uint32_t)((float)n * inv);
+  int32_t rr = (int32_t)(n - q * d);
+  while (rr < 0) { q -= 1; rr += (int32_t)d; }
+  while (rr >= (int32_t)d) { q += 1; rr -= (int32_t)d; }
+  r = (uint32_t)rr;
+}
+
+struct GatherLds {
+  int epb;                        // envs per workgroup
+  float inv_f, inv_p, inv_w;      // 1/F, 1/P, 1/W
+};
+
+__global__ __launch_bounds__(BLOCK) void k_ring_gather_lds(RingDesc r, double* __restrict__ price_out,
+                                                           double* __restrict__ port_out,
+                                                           uint64_t* __restrict__ ts_out,
+                                                           GatherLds g) {
+  extern __shared__ d2 s_buf[];
+  const int F = r.F, P = r.Pn, W = r.W, C = F + P;
+  const int env0 = blockIdx.x * g.epb;
+  const int ne = min(g.epb, r.N - env0);
+  const int ring_pairs = ne * W * C / 2;   // W even: whole pairs
+  const int ts_pairs = ne * W / 2;
+  d2* s_ring = s_buf;
+  d2* s_ts = s_buf + g.epb * W * C / 2;
+  __shared__ int s_hd[64], s_len[64];
+  if (threadIdx.x < ne) {
+    s_hd[threadIdx.x] = r.head[env0 + threadIdx.x];
+    s_len[threadIdx.x] = r.len[env0 + threadIdx.x];
+  }
+  {
+    const d2* gr = reinterpret_cast<const d2*>(r.ring + (size_t)env0 * W * C);
+    const d2* gt = reinterpret_cast<const d2*>(r.ring_ts + (size_t)env0 * W);
+    const int total = ring_pairs + (ts_out ? ts_pairs : 0);
+    constexpr int U = 4;
+    for (int i0 = threadIdx.x; i0 < total; i0 += U * BLOCK) {
+      d2 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * BLOCK;
+        if (i < ring_pairs) v[u] = __builtin_nontemporal_load(gr + i);
+        else if (i < total) v[u] = __builtin_nontemporal_load(gt + (i - ring_pairs));
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * BLOCK;
+        if (i < ring_pairs) s_ring[i] = v[u];
+        else if (i < total) s_ts[i - ring_pairs] = v[u];
+      }
+    }
+  }
+  __syncthreads();
+  const double* sr = reinterpret_cast<const double*>(s_ring);
+  const int nt = r.norm;
+  // one element of the logical window: env-local row R = e*W + w, column c
+  auto elem = [&](uint32_t R, int c, bool is_price) -> double {
+    uint32_t e, w;
+    divmod_small(R, (uint32_t)W, g.inv_w, e, w);
+    const int len = s_len[e], hd = s_hd[e];
+    if ((int)w >= len) return 0.;
+    int row = hd - len + 1 + (int)w;
+    if (row < 0) row += W;
+    const double* base = sr + (size_t)e * W * C;
+    double x = base[row * C + c];
+    if (is_price) {
+      if (nt == MGN_NORM_LOG && !r.prelog) {
+        x = log((x < 1e-5) ? 1e-5 : x);
+      } else if (nt == MGN_NORM_LOOKBACK || nt == MGN_NORM_LOOKBACK_LOG) {
+        x = x / base[hd * C + c];
+        if (nt == MGN_NORM_LOOKBACK_LOG) x = log(x);
+      }
+    }
+    return x;
+  };
+  if (price_out) {
+    d2* o = reinterpret_cast<d2*>(price_out + (size_t)env0 * W * F);
+    const int n = ne * W * F / 2;
+    for (int q = threadIdx.x; q < n; q += BLOCK) {
+      uint32_t R, c;
+      divmod_small(2u * q, (uint32_t)F, g.inv_f, R, c);
+      d2 v;
+      v.x = elem(R, (int)c, true);
+      if (++c == (uint32_t)F) { c = 0; ++R; }
+      v.y = elem(R, (int)c, true);
+      __builtin_nontemporal_store(v, o + q);
+    }
+  }
+  if (port_out) {
+    d2* o = reinterpret_cast<d2*>(port_out + (size_t)env0 * W * P);
+    const int n = ne * W * P / 2;
+    for (int q = threadIdx.x; q < n; q += BLOCK) {
+      uint32_t R, c;
+      divmod_small(2u * q, (uint32_t)P, g.inv_p, R, c);
+      d2 v;
+      v.x = elem(R, F + (int)c, false);
+      if (++c == (uint32_t)P) { c = 0; ++R; }
+      v.y = elem(R, F + (int)c, false);
+      __builtin_nontemporal_store(v, o + q);
+    }
+  }
+  if (ts_out) {
+    const uint64_t* st = reinterpret_cast<const uint64_t*>(s_ts);
+    ulong2* o = reinterpret_cast<ulong2*>(ts_out + (size_t)env0 * W);
+    for (int q = threadIdx.x; q < ts_pairs; q += BLOCK) {
+      uint64_t t[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        uint32_t e, w;
+        divmod_small(2u * q + h, (uint32_t)W, g.inv_w, e, w);
+        const int len = s_len[e], hd = s_hd[e];
+        int row = hd - len + 1 + (int)w;
+        if (row < 0) row += W;
+        t[h] = ((int)w < len) ? st[e * W + row] : 0;
+      }
+      o[q] = make_ulong2(t[0], t[1]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Launch history (mgn_rollout_hist / mgn_window_hist): K steps in one launch
+// with every step's window.  The step kernel appends each ring push to a
+// linear per-env history, so step k's window is the contiguous row range
+// [hend - hlen, hend) -- no modulo, no rotation.  Sized W + K*(W+1) rows per
+// env (each step pushes one row, plus W refill rows when it ends an episode).
+struct HistDesc {
+  int N, F, Pn, W, K, hrows, norm, prelog;
+  const double* hist;
+  const uint64_t* hist_ts;
+  const int32_t* hend;
+  const int32_t* hlen;
+};
+
+// rows [W - len, W) of every env's history := its ring window, oldest first
+__global__ __launch_bounds__(BLOCK) void k_hist_prefix(RingDesc r, double* __restrict__ hist,
+                                                       uint64_t* __restrict__ hist_ts, int hrows) {
+  const int C = r.F + r.Pn;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (int64_t)r.N * r.W * C) return;
+  const int env = (int)(gid / ((int64_t)r.W * C));
+  const int rem = (int)(gid - (int64_t)env * r.W * C);
+  const int i = rem / C, c = rem - (rem / C) * C;
+  const int len = r.len[env];
+  if (i >= len) return;
+  int row = r.head[env] - len + 1 + i;
+  if (row < 0) row += r.W;
+  const int dst = r.W - len + i;
+  hist[((size_t)env * hrows + dst) * C + c] = r.ring[((size_t)env * r.W + row) * C + c];
+  if (c == 0) hist_ts[(size_t)env * hrows + dst] = r.ring_ts[(size_t)env * r.W + row];
+}
+
+// every step's StackerDiscrete.current_data: a workgroup per (env, ks
+// consecutive steps) writes those windows (outputs (K,N,W,F), (K,N,W,P), (K,N,W); element-wise normalisers as
+// k_ring_gather_elem).  The history rows the K windows span, [hend[0] -
+// hlen[0], hend[K-1]), are staged once into LDS (they are shared by
+// consecutive windows: W + K rows when no episode ends), so HBM sees each row
+// read once and every output byte written once with 16-B stores; a span
+// larger than the LDS budget reads the history directly (L2-resident within
+// the workgroup).  Splitting an env's K windows over workgroups of ks keeps
+// the grid fine-grained (no tail of a few long workgroups).
+constexpr int HIST_KMAX = 64;
+
+__global__ __launch_bounds__(BLOCK) void k_hist_gather(HistDesc h, double* __restrict__ price_out,
+                                                       double* __restrict__ port_out,
+                                                       uint64_t* __restrict__ ts_out, int ks, int lds_rows,
+                                                       float inv_f, float inv_p, float inv_w,
+                                                       float inv_wf, float inv_wp) {
+  extern __shared__ double s_rows[];  // (lds_rows, C) then lds_rows timestamps
+  const int F = h.F, P = h.Pn, W = h.W, C = F + P;
+  // workgroup: env, steps [k0, k0 + K) of the launch (ks steps per workgroup)
+  const int kb = (h.K + ks - 1) / ks;
+  const int env = blockIdx.x / kb;
+  const int k0 = (blockIdx.x - env * kb) * ks;
+  const int K = min(ks, h.K - k0);
+  __shared__ int s_start[HIST_KMAX], s_len[HIST_KMAX];
+  if (threadIdx.x < K) {
+    const size_t t = (size_t)(k0 + threadIdx.x) * h.N + env;
+    s_start[threadIdx.x] = h.hend[t] - h.hlen[t];
+    s_len[threadIdx.x] = h.hlen[t];
+  }
+  __syncthreads();
+  const int r0 = s_start[0];
+  const int r1 = s_start[K - 1] + s_len[K - 1];
+  const int nrows = r1 - r0;
+  const bool staged = nrows <= lds_rows;
+  const double* grow = h.hist + ((size_t)env * h.hrows + r0) * C;  // row r0 of this env
+  const uint64_t* gts = h.hist_ts + (size_t)env * h.hrows + r0;
+  uint64_t* s_ts = reinterpret_cast<uint64_t*>(s_rows + (size_t)lds_rows * C);
+  if (staged) {
+    constexpr int U = 8;
+    const int n = nrows * C;
+    for (int i0 = threadIdx.x; i0 < n; i0 += U * BLOCK) {
+      double v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = (i0 + u * BLOCK < n) ? grow[i0 + u * BLOCK] : 0.;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (i0 + u * BLOCK < n) s_rows[i0 + u * BLOCK] = v[u];
+    }
+    if (ts_out)
+      for (int i = threadIdx.x; i < nrows; i += BLOCK) s_ts[i] = gts[i];
+    __syncthreads();
+  }
+  const double* rows = staged ? s_rows : grow;
+  const int nt = h.norm;
+  auto block_out = [&](double* __restrict__ out_base, int ncol, int col0, float inv_n, float inv_wn,
+                       bool is_price) {
+    const uint32_t WN = (uint32_t)(W * ncol);
+    const int n = K * W * ncol / 2;  // pairs (W even: never across windows)
+    for (int q = threadIdx.x; q < n; q += BLOCK) {
+      uint32_t k, rem, w, c;
+      divmod_small(2u * q, WN, inv_wn, k, rem);
+      divmod_small(rem, (uint32_t)ncol, inv_n, w, c);
+      const int len = s_len[k];
+      const int rs = s_start[k] - r0;
+      d2 v;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        double x = 0.;
+        if ((int)w < len) {
+          x = rows[(rs + (int)w) * C + col0 + (int)c];
+          if (is_price) {
+            if (nt == MGN_NORM_LOG && !h.prelog) {
+              x = log((x < 1e-5) ? 1e-5 : x);
+            } else if (nt == MGN_NORM_LOOKBACK || nt == MGN_NORM_LOOKBACK_LOG) {
+              x = x / rows[(rs + len - 1) * C + col0 + (int)c];
+              if (nt == MGN_NORM_LOOKBACK_LOG) x = log(x);
+            }
+          }
+        }
+        if (hh) v.y = x; else v.x = x;
+        if (++c == (uint32_t)ncol) { c = 0; ++w; }
+      }
+      d2* o = reinterpret_cast<d2*>(out_base + ((size_t)(k0 + k) * h.N + env) * WN);
+      __builtin_nontemporal_store(v, o + (rem >> 1));
+    }
+  };
+  if (price_out) block_out(price_out, F, 0, inv_f, inv_wf, true);
+  if (port_out) block_out(port_out, P, F, inv_p, inv_wp, false);
+  if (ts_out) {
+    const uint64_t* tsrc = staged ? s_ts : gts;
+    const int n = K * W / 2;
+    for (int q = threadIdx.x; q < n; q += BLOCK) {
+      uint32_t k, w;
+      divmod_small(2u * q, (uint32_t)W, inv_w, k, w);
+      const int len = s_len[k];
+      const int rs = s_start[k] - r0;
+      const uint64_t a = ((int)w < len) ? tsrc[rs + (int)w] : 0;
+      const uint64_t b = ((int)w + 1 < len) ? tsrc[rs + (int)w + 1] : 0;
+      ulong2* o = reinterpret_cast<ulong2*>(ts_out + ((size_t)(k0 + k) * h.N + env) * W);
+      o[w >> 1] = make_ulong2(a, b);
+    }
+  }
+}
+
 // StackerDiscreteReturns' np.diff along the last axis: out (rows, cols-1)
 __global__ __launch_bounds__(BLOCK) void k_feat_diff(const double* __restrict__ in,
                                                      double* __restrict__ out, int64_t rows,

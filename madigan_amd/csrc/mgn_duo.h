@@ -114,6 +114,7 @@ struct GenOut {
   double shA, shB, ep_ret, ep_len, cos_qn;
   DdrPre ddr;  // DDR's reward-independent operands, from the current A, B
   int32_t head, len;
+  int32_t hcnt, klast;  // launch history: next row, the step its rows belong to
 };
 
 // P, ts: the State's price and timestamp (the tick the record belongs to)
@@ -213,13 +214,30 @@ __device__ __forceinline__ void duo_finish(const DuoRec<S>& sh, const Lane<1>& s
     if (g.len < p.W) g.len += 1;
     const int R = p.F + p.A + 1;
     double* row = p.ring + ((size_t)env * p.W + g.head) * R;
+    double* hrow = p.hist ? p.hist + ((size_t)env * p.hrows + g.hcnt) * R : nullptr;
     if (valid) {
-      row[s.asset[0]] = p.ring_log ? log_norm(P) : P;
-      row[p.F + 1 + s.asset[0]] = (Lc * P) / eq;
+      const double pv = p.ring_log ? log_norm(P) : P;
+      const double lv = (Lc * P) / eq;
+      row[s.asset[0]] = pv;
+      row[p.F + 1 + s.asset[0]] = lv;
+      if (hrow) {
+        hrow[s.asset[0]] = pv;
+        hrow[p.F + 1 + s.asset[0]] = lv;
+      }
     }
     if (ls == 0) {
-      row[p.F] = (cash - sh.rB[el]) / eq;
+      const double cv = (cash - sh.rB[el]) / eq;
+      row[p.F] = cv;
       p.ring_ts[(size_t)env * p.W + g.head] = ts;
+      if (hrow) {
+        hrow[p.F] = cv;
+        p.hist_ts[(size_t)env * p.hrows + g.hcnt] = ts;
+      }
+    }
+    if (hrow) {
+      // a reset's refill rows belong to the step that ended the episode
+      if (flags & REC_STEP) g.klast = sh.rK[el];
+      hist_mark(p, env, ls, g.hcnt, g.len, g.klast);
     }
     // a reset empties the window before the refill ticks (Env.h:181-187 +
     // initialize_history); the ledger side flags it on the step that ends
@@ -395,6 +413,8 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
     g.ep_len = p.ep[(size_t)envc * 2 + 1];
     g.head = 0;
     g.len = 0;
+    g.hcnt = p.W;
+    g.klast = 0;
     if (p.W > 0) {
       g.head = p.rhead[envc];
       g.len = p.rlen[envc];

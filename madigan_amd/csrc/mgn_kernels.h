@@ -68,6 +68,15 @@ struct KParams {
   int64_t rp_rows, rp_stride;
   int64_t *rcur;
   double *aux;  // (N, A, MGN_AUX_WIDTH) multi-component source state
+  // per-launch window history (mgn_rollout_hist; null otherwise): every ring
+  // push of the launch is also appended to hist (N, hrows, F+A+1) / hist_ts
+  // (N, hrows) from row W on (rows [W-len0, W) hold the window before the
+  // launch); after step k (and its reset refill) hend[k*N+env] = rows so far,
+  // hlen[k*N+env] = the window's fill
+  double *hist;
+  uint64_t *hist_ts;
+  int32_t *hend, *hlen;
+  int hrows;
 };
 
 // ---------------------------------------------------------------------------
@@ -522,24 +531,45 @@ __device__ __forceinline__ void src_reset(Lane<M>& s, const KParams& p, int env,
 }
 
 // StackerDiscrete.stream_state of the current State (preprocessor.py:172-175)
+// (with a launch history, the same row is appended at history row hcnt)
 template <int M, int S>
 __device__ __forceinline__ void ring_push(const Lane<M>& s, const KParams& p, int env, int ls,
-                                          double cash, uint64_t ts, int32_t& head, int32_t& len) {
+                                          double cash, uint64_t ts, int32_t& head, int32_t& len,
+                                          int hcnt = -1) {
   const Sums q = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
   const double eq = (cash + q.lp) - q.b;
   head = (head + 1) % p.W;
   if (len < p.W) len += 1;
   const int R = p.F + p.A + 1;
   double* row = p.ring + ((size_t)env * p.W + head) * R;
+  double* hrow = (hcnt >= 0) ? p.hist + ((size_t)env * p.hrows + hcnt) * R : nullptr;
   put_feats<M, S>(s, p, ls, row, p.ring_log != 0);
+  if (hrow) put_feats<M, S>(s, p, ls, hrow, p.ring_log != 0);
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     if (!s.valid[m]) continue;
-    row[p.F + 1 + s.asset[m]] = (s.L[m] * s.P[m]) / eq;
+    const double v = (s.L[m] * s.P[m]) / eq;
+    row[p.F + 1 + s.asset[m]] = v;
+    if (hrow) hrow[p.F + 1 + s.asset[m]] = v;
   }
   if (ls == 0) {
-    row[p.F] = (cash - q.b) / eq;
+    const double c = (cash - q.b) / eq;
+    row[p.F] = c;
     p.ring_ts[(size_t)env * p.W + head] = ts;
+    if (hrow) {
+      hrow[p.F] = c;
+      p.hist_ts[(size_t)env * p.hrows + hcnt] = ts;
+    }
+  }
+}
+
+// after a history row: count it and mark step k's window end and fill
+__device__ __forceinline__ void hist_mark(const KParams& p, int env, int ls, int& hcnt, int len,
+                                          int k) {
+  hcnt += 1;
+  if (ls == 0) {
+    p.hend[(size_t)k * p.N + env] = hcnt;
+    p.hlen[(size_t)k * p.N + env] = len;
   }
 }
 
@@ -1275,6 +1305,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
   // `pending` of them), so one inlined getData serves both paths.
   int k = 0;
   int pending = 0;
+  int hcnt = p.W;  // next launch-history row
   while (true) {
     const bool stepping = (pending == 0) && (k < K);
     const bool ticking = stepping || (pending > 0);
@@ -1487,7 +1518,10 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
         ep_len = 0;
       }
       // ---- window; agent reset (offpolicy_q.py:199-201)
-      if (p.W > 0) ring_push<M, S>(s, p, env, ls, cash, ts, head, len);
+      if (p.W > 0) {
+        ring_push<M, S>(s, p, env, ls, cash, ts, head, len, p.hist ? hcnt : -1);
+        if (p.hist) hist_mark(p, env, ls, hcnt, len, k);
+      }
       s0 = q;
       k += 1;
       if (done && p.auto_reset) {
@@ -1509,7 +1543,10 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
       }
     } else if (pending > 0) {
       // ---- a reset tick: stream the State (preprocessor.py:172-194)
-      if (p.W > 0) ring_push<M, S>(s, p, env, ls, cash, ts, head, len);
+      if (p.W > 0) {
+        ring_push<M, S>(s, p, env, ls, cash, ts, head, len, p.hist ? hcnt : -1);
+        if (p.hist) hist_mark(p, env, ls, hcnt, len, k - 1);
+      }
       pending -= 1;
       if (pending == 0) s0 = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
     }

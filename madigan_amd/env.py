@@ -433,6 +433,36 @@ class BatchedEnv:
         L.check(self.lib.mgn_window(self.h, None, None, None), self.h)
         return self.win_price, self.win_port, self.win_ts
 
+    def rollout_window(self, actions, out: Optional[dict] = None, per_step: bool = False):
+        """The agent loop of a windowed env in one native call (mgn_rollout_window):
+        per step k, step k of `rollout(actions)` then `window()`.  Returns the
+        trajectory and the window: the last step's (N,W,·) views of the handle's
+        buffers, or with per_step=True fresh (K,N,W,·) tensors of every step's."""
+        torch = _torch()
+        if not self.W:
+            raise RuntimeError("env built with window=0")
+        if not (isinstance(actions, torch.Tensor) and actions.device == self.device
+                and actions.dtype == torch.int8 and actions.is_contiguous()):
+            actions = torch.as_tensor(actions).to(self.device, torch.int8).contiguous()
+        if actions.dim() != 3 or actions.shape[1] != self.N or actions.shape[2] != self.A:
+            raise ValueError(f"actions must be (K, {self.N}, {self.A}), got {tuple(actions.shape)}")
+        K = int(actions.shape[0])
+        out = self.alloc_traj(K) if out is None else out
+        self._check_traj(out, K)
+        t = self._traj_struct(out)
+        if per_step:
+            wp = torch.empty((K,) + tuple(self.win_price.shape), dtype=torch.float64, device=self.device)
+            wo = torch.empty((K,) + tuple(self.win_port.shape), dtype=torch.float64, device=self.device)
+            wt = torch.empty((K,) + tuple(self.win_ts.shape), dtype=self.win_ts.dtype, device=self.device)
+            ptrs = [C.c_void_p(x.data_ptr()) for x in (wp, wo, wt)]
+            win = (wp, wo, wt)
+        else:
+            ptrs = [None, None, None]
+            win = (self.win_price, self.win_port, self.win_ts)
+        L.check(self.lib.mgn_rollout_window(self.h, C.c_void_p(actions.data_ptr()), K, C.byref(t),
+                                            *ptrs, int(per_step)), self.h)
+        return out, win
+
     def window_push(self, price=None, port=None, ts=None):
         ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
         L.check(self.lib.mgn_window_push(self.h, ptr(price), ptr(port), ptr(ts)), self.h)

@@ -330,3 +330,63 @@ def test_schedules_bit_identical(gpu, A, kw):
             assert_bits(w, v, f"duo vs single {k}")
         else:
             assert np.array_equal(np.asarray(w), np.asarray(v)), f"duo vs single {k}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("norm,W,N,sched", [(None, 8, 96, "duo"), ("log", 8, 96, "duo"),
+                                            ("lookback", 6, 50, "single"), ("log", 8, 70, "single"),
+                                            (None, 256, 20, "duo"), ("lookback_log", 1024, 12, "duo")])
+def test_rollout_window_per_step(gpu, norm, W, N, sched):
+    """mgn_rollout_window per_step (K steps in one launch, the launch history,
+    then every step's window) against the oracle's window after every step;
+    both step schedules, windows partly filled, frequent margin calls so the
+    auto-reset refill rows land inside the launch, N not a multiple of the
+    gather's windows per workgroup."""
+    from madigan_amd import _lib as L
+    A, K = 4, 24
+    kw = dict(required_margin=0.02, maintenance_margin=0.25, transaction_cost_rel=0.02,
+              slippage_rel=1e-4, unit_size=0.9, init_cash=1e5, reward_shaper="DSR",
+              window=W, norm_type=norm, auto_reset=1)
+    src = trendou_sources(A, [0.2, 2, 6, 0.05, 0.2, 5.0, 0.15, 0.3, 0.2, 0.99])
+
+    def handle():
+        g, orc = make_pair(src, N, **kw)
+        L.check(g.lib.mgn_set_schedule(g.h, L.SCHED_DUO if sched == "duo" else L.SCHED_SINGLE), g.h)
+        g.reset()
+        orc.reset()
+        return g, orc
+
+    g, orc = handle()
+    acts = g.generate_actions(K, seed=11)
+    out, (wp, wo, wt) = g.rollout_window(acts, per_step=True)
+    a = acts.cpu().numpy()
+    dones = 0
+    for k in range(K):
+        r = orc.rollout(a[k:k + 1])
+        dones += int(r["done"].sum())
+        rpr, rpo, rts = orc.window()
+        if norm is None:
+            assert_bits(wp[k].cpu().numpy(), rpr, f"window price step {k}")
+        else:
+            close(wp[k].cpu().numpy(), rpr, f"window price step {k}",
+                  rtol=1e-14 if norm == "lookback" else 1e-12)
+        assert_bits(wo[k].cpu().numpy(), rpo, f"window portfolio step {k}")
+        assert np.array_equal(wt[k].cpu().numpy().astype(np.uint64), rts), f"window ts step {k}"
+    assert dones > 0, "the case should exercise auto-reset refills inside the launch"
+    # the trajectory equals a plain rollout of the same actions
+    h, _ = handle()
+    o2 = h.rollout(acts)
+    for f in ("reward", "shaped", "done", "obs_price", "obs_port", "tunits", "tcost"):
+        assert_bits(out[f].cpu().numpy(), o2[f].cpu().numpy(), f)
+    # per_step=False: one rollout, the last window in the handle's buffers
+    h2, _ = handle()
+    _, (lp, lo, lt) = h2.rollout_window(acts)
+    assert_bits(lp.cpu().numpy(), wp[-1].cpu().numpy(), "last window price")
+    assert_bits(lo.cpu().numpy(), wo[-1].cpu().numpy(), "last window portfolio")
+    # a second call continues from the ring (history prefix = the window so far)
+    out3, (wp3, wo3, wt3) = g.rollout_window(acts[:5], per_step=True)
+    for k in range(5):
+        orc.rollout(a[k:k + 1])
+        rpr, rpo, rts = orc.window()
+        assert_bits(wo3[k].cpu().numpy(), rpo, f"second call window portfolio step {k}")
+        assert np.array_equal(wt3[k].cpu().numpy().astype(np.uint64), rts)

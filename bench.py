@@ -231,6 +231,8 @@ def main():
     ap.add_argument("--fuse", type=int, default=64)
     ap.add_argument("--win-fuse", type=int, default=64,
                     help="steps per launch of the windowed workloads (capped by --fuse)")
+    ap.add_argument("--win-overlap", action="store_true",
+                    help="windowed workloads: gather on a second stream beside the next step launch")
     ap.add_argument("--n-envs", type=int, default=8192, help="envs per GPU")
     ap.add_argument("--assets", type=int, default=8)
     ap.add_argument("--layout", type=int, default=0, help="assets per lane (0 = auto)")
@@ -391,28 +393,26 @@ def windowed(args, world, rank, dev):
     wp = torch.empty((Kf, N, W, env.F), dtype=torch.float64, device=dev)
     wo = torch.empty((Kf, N, W, A + 1), dtype=torch.float64, device=dev)
     wt = torch.empty((Kf, N, W), dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    # one ctypes call per kernel group, arguments built once
     import ctypes as C
     from madigan_amd import _lib as L
     lib, h = env.lib, env.h
+    if args.win_overlap:
+        # gathers on a second stream, the history double-buffered: launch L's
+        # gather (HBM-bound) runs beside launch L+1's steps (latency-bound).
+        # Measured: +7 % at C4, -5 % at C5 (the step kernel's latency rises
+        # under the gather's traffic), so it is off by default.
+        wstream = torch.cuda.Stream(dev)
+        L.check(lib.mgn_set_window_stream(h, C.c_void_p(wstream.cuda_stream)), h)
     tstruct = C.byref(env._traj_struct(traj))
     per = env.N * env.A
     base = actions.data_ptr()
     wptr = [C.c_void_p(x.data_ptr()) for x in (wp, wo, wt)]
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(n_time)] for _ in range(3)]
 
-    def run(l0, l1, ev=None):
+    def run(l0, l1):
         rc = 0
         for l in range(l0, l1):
-            if ev is not None:
-                ev[0][l - l0].record(stream)
             rc |= lib.mgn_rollout_hist(h, C.c_void_p(base + l * Kf * per), Kf, tstruct)
-            if ev is not None:
-                ev[1][l - l0].record(stream)
             rc |= lib.mgn_window_hist(h, *wptr)
-            if ev is not None:
-                ev[2][l - l0].record(stream)
         L.check(rc, h)
 
     run(0, n_warm)
@@ -420,9 +420,10 @@ def windowed(args, world, rank, dev):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ev = evs
+    # kernel durations: HIP events on each kernel's own stream (mgn_set_timing)
+    L.check(lib.mgn_set_timing(h, 1), h)
     t0 = time.perf_counter()
-    run(n_warm, n_warm + n_time, ev)
+    run(n_warm, n_warm + n_time)
     stats = env.episode_stats
     if world > 1:
         gathered = torch.empty((world * N, 4), dtype=torch.float64, device=dev)
@@ -438,8 +439,11 @@ def windowed(args, world, rank, dev):
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    step_us = float(np.mean([a.elapsed_time(b) for a, b in zip(ev[0], ev[1])])) * 1e3
-    gather_us = float(np.mean([b.elapsed_time(c) for b, c in zip(ev[1], ev[2])])) * 1e3
+    tm = (C.c_double * 4)()
+    L.check(lib.mgn_get_timing(h, tm), h)
+    L.check(lib.mgn_set_timing(h, 0), h)
+    step_us = tm[0] / max(tm[1], 1) * 1e3
+    gather_us = tm[2] / max(tm[3], 1) * 1e3
     gb = gather_bytes(env, Kf)
     achieved = gb / (gather_us * 1e-6) / 1e9
     value = world * N * args.steps / elapsed
@@ -460,7 +464,9 @@ def windowed(args, world, rank, dev):
                          "bytes_per_env_step": gb / (N * Kf),
                          "avg_launch_us": gather_us},
             "step_launch_avg_us": step_us,
-            "step_launch_note": "history prefix copy + the K-step step kernel",
+            "step_launch_note": "the K-step step kernel" + (
+                " (the previous launch's k_hist_gather runs beside it on a second stream)"
+                if args.win_overlap else ""),
             "episodes_completed": int(gathered[:, 3].sum().item()),
         }
         if wl == "C5":

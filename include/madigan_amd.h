@@ -273,6 +273,17 @@ int mgn_rollout_hist(mgn_env *env, const int8_t *actions_dev, int32_t k_steps, c
 int mgn_window_hist(mgn_env *env, double *price_dev, double *port_dev, uint64_t *ts_dev);
 int mgn_rollout_window(mgn_env *env, const int8_t *actions_dev, int32_t k_steps, const mgn_traj *out,
                        double *price_dev, double *port_dev, uint64_t *ts_dev, int32_t per_step);
+/* run mgn_window_hist on `stream` (NULL: the handle's stream): the history
+ * is then double-buffered, so the gather of launch L overlaps the step launch
+ * L+1 (ordered by events; the caller's window buffers of launch L are
+ * complete once `stream` has passed the gather) */
+int mgn_set_window_stream(mgn_env *env, void *stream);
+/* kernel timing with HIP events on each kernel's own stream: on != 0 starts
+ * (and clears) recording around the step kernel of mgn_rollout_hist and the
+ * gather of mgn_window_hist; mgn_get_timing waits for them and returns
+ * {step ms total, step launches, gather ms total, gather launches} */
+int mgn_set_timing(mgn_env *env, int32_t on);
+int mgn_get_timing(mgn_env *env, double *out4);
 /* uniform discrete actions U{0..atoms-1} (K,N,A) from Philox (benchmark input) */
 int mgn_generate_actions(mgn_env *env, int8_t *actions_dev, int32_t k_steps, uint64_t seed);
 /* Portfolio accessors for every env into out_dev (N,10): {cash, equity, pnl,

@@ -111,6 +111,9 @@ SYMBOLS = {
     "mgn_window": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mgn_rollout_hist": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(Traj)]),
     "mgn_window_hist": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mgn_set_window_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mgn_set_timing": (C.c_int, [C.c_void_p, C.c_int32]),
+    "mgn_get_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
     "mgn_rollout_window": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(Traj),
                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32]),
     "mgn_generate_actions": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_uint64]),

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "../../include/madigan_amd.h"
 #include "mgn_aux_kernels.h"
@@ -63,14 +64,25 @@ struct mgn_env {
   int m = 1;  // assets per lane
   int sched = MGN_SCHED_AUTO;  // requested step schedule
   bool duo = false;            // the two-role kernel runs the steps
-  // launch history (mgn_rollout_hist): grown on demand, owned by the handle
-  double* hist = nullptr;
-  uint64_t* hist_ts = nullptr;
-  int32_t* hend = nullptr;
-  int32_t* hlen = nullptr;
-  size_t hist_rows_cap = 0, hist_k_cap = 0;
-  int hist_rows = 0;  // rows per env of the last mgn_rollout_hist
-  int hist_k = 0;     // its step count (0: none yet)
+  // launch history (mgn_rollout_hist): grown on demand, owned by the handle;
+  // two buffers when the gathers run on a window stream (one is written by
+  // the next step launch while the other is gathered)
+  struct HistBuf {
+    double* hist = nullptr;
+    uint64_t* ts = nullptr;
+    int32_t* hend = nullptr;
+    int32_t* hlen = nullptr;
+    size_t rows_cap = 0, k_cap = 0;
+    int rows = 0;  // rows per env of its last mgn_rollout_hist
+    int k = 0;     // its step count (0: none yet)
+    hipEvent_t ready = nullptr;  // written (main stream)
+    hipEvent_t read = nullptr;   // gathered (window stream)
+  } hb[2];
+  int hcur = 0;
+  hipStream_t wstream = nullptr;  // window stream (mgn_set_window_stream), null: the handle's
+  // kernel timing (mgn_set_timing): start/stop event pairs on each kernel's stream
+  bool timing = false;
+  std::vector<hipEvent_t> t_step, t_gather;
   bool hist_on = false;  // kparams() hands the history to the step kernel
 };
 
@@ -268,11 +280,12 @@ mgn::KParams kparams(const mgn_env* e) {
   p.disc = e->disc_dev;
   p.rcur = e->v.replay_cursor;
   p.aux = e->v.aux;
-  p.hist = e->hist_on ? e->hist : nullptr;
-  p.hist_ts = e->hist_ts;
-  p.hend = e->hend;
-  p.hlen = e->hlen;
-  p.hrows = e->hist_rows;
+  const auto& hb = e->hb[e->hcur];
+  p.hist = e->hist_on ? hb.hist : nullptr;
+  p.hist_ts = hb.ts;
+  p.hend = hb.hend;
+  p.hlen = hb.hlen;
+  p.hrows = hb.rows;
   return p;
 }
 
@@ -492,10 +505,17 @@ int mgn_destroy(mgn_env* e) {
   if (!e) return MGN_ERR_ARG;
   (void)hipStreamSynchronize(e->stream);
   if (e->own_arena) (void)hipFree(e->arena);
-  if (e->hist) (void)hipFree(e->hist);
-  if (e->hist_ts) (void)hipFree(e->hist_ts);
-  if (e->hend) (void)hipFree(e->hend);
-  if (e->hlen) (void)hipFree(e->hlen);
+  if (e->wstream) (void)hipStreamSynchronize(e->wstream);
+  for (auto& b : e->hb) {
+    if (b.hist) (void)hipFree(b.hist);
+    if (b.ts) (void)hipFree(b.ts);
+    if (b.hend) (void)hipFree(b.hend);
+    if (b.hlen) (void)hipFree(b.hlen);
+    if (b.ready) (void)hipEventDestroy(b.ready);
+    if (b.read) (void)hipEventDestroy(b.read);
+  }
+  for (hipEvent_t ev : e->t_step) (void)hipEventDestroy(ev);
+  for (hipEvent_t ev : e->t_gather) (void)hipEventDestroy(ev);
   delete e;
   return MGN_OK;
 }
@@ -603,6 +623,63 @@ int mgn_window(mgn_env* e, double* price_dev, double* port_dev, uint64_t* ts_dev
   return check_hip(e, hipGetLastError(), "mgn_window");
 }
 
+static void time_mark(mgn_env* e, std::vector<hipEvent_t>& v, hipStream_t st) {
+  if (!e->timing) return;
+  hipEvent_t ev;
+  if (hipEventCreate(&ev) != hipSuccess) return;
+  (void)hipEventRecord(ev, st);
+  v.push_back(ev);
+}
+
+static int grow(mgn_env* e, void** p, size_t bytes) {
+  (void)hipDeviceSynchronize();  // first use / larger K only
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  return check_hip(e, hipMalloc(p, bytes), "history alloc");
+}
+
+int mgn_set_window_stream(mgn_env* e, void* stream) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  (void)hipStreamSynchronize(e->stream);
+  if (e->wstream) (void)hipStreamSynchronize(e->wstream);
+  e->wstream = (hipStream_t)stream;
+  for (auto& b : e->hb) {
+    if (!b.ready && hipEventCreateWithFlags(&b.ready, hipEventDisableTiming) != hipSuccess)
+      return fail(e, MGN_ERR_DEVICE, "event create");
+    if (!b.read && hipEventCreateWithFlags(&b.read, hipEventDisableTiming) != hipSuccess)
+      return fail(e, MGN_ERR_DEVICE, "event create");
+  }
+  return MGN_OK;
+}
+
+int mgn_set_timing(mgn_env* e, int32_t on) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  (void)hipDeviceSynchronize();
+  for (hipEvent_t ev : e->t_step) (void)hipEventDestroy(ev);
+  for (hipEvent_t ev : e->t_gather) (void)hipEventDestroy(ev);
+  e->t_step.clear();
+  e->t_gather.clear();
+  e->timing = on != 0;
+  return MGN_OK;
+}
+
+int mgn_get_timing(mgn_env* e, double* out4) {
+  if (!e || !out4) return fail(e, MGN_ERR_ARG, "null handle/out");
+  const std::vector<hipEvent_t>* v[2] = {&e->t_step, &e->t_gather};
+  for (int i = 0; i < 2; ++i) {
+    double ms = 0.;
+    const size_t n = v[i]->size() / 2;
+    for (size_t j = 0; j < n; ++j) {
+      float t = 0.f;
+      (void)hipEventSynchronize((*v[i])[2 * j + 1]);
+      if (hipEventElapsedTime(&t, (*v[i])[2 * j], (*v[i])[2 * j + 1]) == hipSuccess) ms += t;
+    }
+    out4[2 * i] = ms;
+    out4[2 * i + 1] = (double)n;
+  }
+  return MGN_OK;
+}
+
 int mgn_rollout_hist(mgn_env* e, const int8_t* actions_dev, int32_t k_steps, const mgn_traj* out) {
   if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
   if (!actions_dev || !out) return fail(e, MGN_ERR_ARG, "null actions/out");
@@ -615,55 +692,55 @@ int mgn_rollout_hist(mgn_env* e, const int8_t* actions_dev, int32_t k_steps, con
   const size_t rows = (size_t)e->W + (size_t)k_steps * (e->W + 1);
   if ((size_t)e->N * rows * C >= ((size_t)1 << 31))
     return fail(e, MGN_ERR_LENGTH, "launch history exceeds 2^31 elements: fewer steps per call");
-  if (rows > e->hist_rows_cap) {  // grow (first use / more steps): synchronous
-    (void)hipStreamSynchronize(e->stream);
-    if (e->hist) (void)hipFree(e->hist);
-    if (e->hist_ts) (void)hipFree(e->hist_ts);
-    e->hist = nullptr;
-    e->hist_ts = nullptr;
-    e->hist_rows_cap = 0;
-    int st = check_hip(e, hipMalloc((void**)&e->hist, (size_t)e->N * rows * C * 8), "history alloc");
-    if (st == MGN_OK) st = check_hip(e, hipMalloc((void**)&e->hist_ts, (size_t)e->N * rows * 8), "history alloc");
+  // with a window stream, alternate buffers; the step launch waits until the
+  // gather that last read its buffer has finished
+  const int b = e->wstream ? (e->hcur ^ 1) : 0;
+  auto& hb = e->hb[b];
+  int st = MGN_OK;
+  if (rows > hb.rows_cap) {
+    hb.rows_cap = 0;
+    st = grow(e, (void**)&hb.hist, (size_t)e->N * rows * C * 8);
+    if (st == MGN_OK) st = grow(e, (void**)&hb.ts, (size_t)e->N * rows * 8);
     if (st != MGN_OK) return st;
-    e->hist_rows_cap = rows;
+    hb.rows_cap = rows;
   }
-  if ((size_t)k_steps > e->hist_k_cap) {
-    (void)hipStreamSynchronize(e->stream);
-    if (e->hend) (void)hipFree(e->hend);
-    if (e->hlen) (void)hipFree(e->hlen);
-    e->hend = nullptr;
-    e->hlen = nullptr;
-    e->hist_k_cap = 0;
-    int st = check_hip(e, hipMalloc((void**)&e->hend, (size_t)k_steps * e->N * 4), "history alloc");
-    if (st == MGN_OK) st = check_hip(e, hipMalloc((void**)&e->hlen, (size_t)k_steps * e->N * 4), "history alloc");
+  if ((size_t)k_steps > hb.k_cap) {
+    hb.k_cap = 0;
+    st = grow(e, (void**)&hb.hend, (size_t)k_steps * e->N * 4);
+    if (st == MGN_OK) st = grow(e, (void**)&hb.hlen, (size_t)k_steps * e->N * 4);
     if (st != MGN_OK) return st;
-    e->hist_k_cap = (size_t)k_steps;
+    hb.k_cap = (size_t)k_steps;
   }
-  e->hist_rows = (int)rows;
+  if (e->wstream && hb.k > 0) (void)hipStreamWaitEvent(e->stream, hb.read, 0);
+  e->hcur = b;
+  hb.rows = (int)rows;
   const mgn::RingDesc r = ring_desc(e);
   const int64_t pt = (int64_t)e->N * e->W * C;
   hipLaunchKernelGGL(mgn::k_hist_prefix, dim3((unsigned)((pt + 255) / 256)), dim3(256), 0, e->stream,
-                     r, e->hist, e->hist_ts, (int)rows);
+                     r, hb.hist, hb.ts, (int)rows);
+  time_mark(e, e->t_step, e->stream);
   e->hist_on = true;
   launch_step(e, *out, mgn::IN_DISCRETE, nullptr, nullptr, actions_dev, (int)k_steps);
   e->hist_on = false;
-  e->hist_k = k_steps;
+  time_mark(e, e->t_step, e->stream);
+  hb.k = k_steps;
+  if (e->wstream) (void)hipEventRecord(hb.ready, e->stream);
   return check_hip(e, hipGetLastError(), "mgn_rollout_hist");
 }
 
 int mgn_window_hist(mgn_env* e, double* price_dev, double* port_dev, uint64_t* ts_dev) {
   if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
-  if (e->hist_k == 0) return fail(e, MGN_ERR_CONFIG, "no mgn_rollout_hist to gather from");
+  auto& hb = e->hb[e->hcur];
+  if (hb.k == 0) return fail(e, MGN_ERR_CONFIG, "no mgn_rollout_hist to gather from");
   if (!price_dev && !port_dev && !ts_dev) return MGN_OK;
   const int C = e->F + e->A + 1;
   mgn::HistDesc h;
-  h.N = e->N; h.F = e->F; h.Pn = e->A + 1; h.W = e->W; h.K = e->hist_k; h.hrows = e->hist_rows;
+  h.N = e->N; h.F = e->F; h.Pn = e->A + 1; h.W = e->W; h.K = hb.k; h.hrows = hb.rows;
   h.norm = e->cfg.norm_type;
   h.prelog = e->cfg.norm_type == MGN_NORM_LOG;
-  h.hist = e->hist; h.hist_ts = e->hist_ts; h.hend = e->hend; h.hlen = e->hlen;
+  h.hist = hb.hist; h.hist_ts = hb.ts; h.hend = hb.hend; h.hlen = hb.hlen;
   if (h.norm == MGN_NORM_STANDARD_NORMAL || h.norm == MGN_NORM_LOG_STANDARD_NORMAL)
     return fail(e, MGN_ERR_CONFIG, "mgn_window_hist: element-wise normalisers only (none, log, lookback, lookback_log)");
-  if (h.K > mgn::HIST_KMAX) return fail(e, MGN_ERR_LENGTH, "mgn_window_hist: at most 64 steps per launch history");
   // LDS rows: the window before the launch, one row per step and one reset's
   // refill; a longer span reads the history directly
   const int ks = std::min(h.K, kHistStepsPerGroup);
@@ -671,9 +748,14 @@ int mgn_window_hist(mgn_env* e, double* price_dev, double* port_dev, uint64_t* t
   const int lds_rows = std::min(e->W + ks + (e->W + 1), (int)(kGatherLdsBudget / ((size_t)(C + 1) * 8)));
   const size_t lds = (size_t)lds_rows * (C + 1) * 8;
   const float wf = (float)(e->W * e->F), wp = (float)(e->W * (e->A + 1));
-  hipLaunchKernelGGL(mgn::k_hist_gather, dim3((unsigned)(e->N * kb)), dim3(256), lds, e->stream, h,
+  hipStream_t st = e->wstream ? e->wstream : e->stream;
+  if (e->wstream) (void)hipStreamWaitEvent(st, hb.ready, 0);
+  time_mark(e, e->t_gather, st);
+  hipLaunchKernelGGL(mgn::k_hist_gather, dim3((unsigned)(e->N * kb)), dim3(256), lds, st, h,
                      price_dev, port_dev, ts_dev, ks, lds_rows, 1.0f / (float)e->F, 1.0f / (float)(e->A + 1),
                      1.0f / (float)e->W, 1.0f / wf, 1.0f / wp);
+  time_mark(e, e->t_gather, st);
+  if (e->wstream) (void)hipEventRecord(hb.read, st);
   return check_hip(e, hipGetLastError(), "mgn_window_hist");
 }
 

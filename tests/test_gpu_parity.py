@@ -390,3 +390,56 @@ def test_rollout_window_per_step(gpu, norm, W, N, sched):
         rpr, rpo, rts = orc.window()
         assert_bits(wo3[k].cpu().numpy(), rpo, f"second call window portfolio step {k}")
         assert np.array_equal(wt3[k].cpu().numpy().astype(np.uint64), rts)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sched", ["duo", "single"])
+def test_window_stream_overlap(gpu, sched):
+    """Gathers on a second stream (mgn_set_window_stream): the launch history
+    alternates buffers, launch L's gather overlaps launch L+1's steps; every
+    window of three back-to-back launches equals the oracle's, and the
+    timing API reports one step kernel and one gather per launch."""
+    import ctypes as C
+    import torch
+    from madigan_amd import _lib as L
+    A, N, W, K, n_launch = 4, 160, 8, 8, 3
+    kw = dict(required_margin=0.02, maintenance_margin=0.25, transaction_cost_rel=0.02,
+              slippage_rel=1e-4, unit_size=0.9, init_cash=1e5, reward_shaper="DSR",
+              window=W, norm_type=None, auto_reset=1)
+    src = trendou_sources(A, [0.2, 2, 6, 0.05, 0.2, 5.0, 0.15, 0.3, 0.2, 0.99])
+    g, orc = make_pair(src, N, **kw)
+    L.check(g.lib.mgn_set_schedule(g.h, L.SCHED_DUO if sched == "duo" else L.SCHED_SINGLE), g.h)
+    g.reset()
+    orc.reset()
+    ws = torch.cuda.Stream(g.device)
+    L.check(g.lib.mgn_set_window_stream(g.h, C.c_void_p(ws.cuda_stream)), g.h)
+    L.check(g.lib.mgn_set_timing(g.h, 1), g.h)
+    acts = g.generate_actions(K * n_launch, seed=21)
+    outs = []
+    for l in range(n_launch):
+        traj = g.alloc_traj(K)
+        wp = torch.empty((K, N, W, A), dtype=torch.float64, device=g.device)
+        wo = torch.empty((K, N, W, A + 1), dtype=torch.float64, device=g.device)
+        wt = torch.empty((K, N, W), dtype=torch.int64, device=g.device)
+        t = g._traj_struct(traj)
+        L.check(g.lib.mgn_rollout_hist(g.h, C.c_void_p(acts[l * K:(l + 1) * K].data_ptr()), K,
+                                       C.byref(t)), g.h)
+        L.check(g.lib.mgn_window_hist(g.h, *[C.c_void_p(x.data_ptr()) for x in (wp, wo, wt)]), g.h)
+        outs.append((traj, wp, wo, wt))
+    torch.cuda.synchronize()
+    tm = (C.c_double * 4)()
+    L.check(g.lib.mgn_get_timing(g.h, tm), g.h)
+    assert tm[1] == n_launch and tm[3] == n_launch and tm[0] > 0 and tm[2] > 0
+    L.check(g.lib.mgn_set_timing(g.h, 0), g.h)
+    a = acts.cpu().numpy()
+    dones = 0
+    for l, (traj, wp, wo, wt) in enumerate(outs):
+        for k in range(K):
+            r = orc.rollout(a[l * K + k:l * K + k + 1])
+            dones += int(r["done"].sum())
+            close(traj["reward"][k].cpu().numpy(), r["reward"][0], f"reward {l}/{k}")
+            rpr, rpo, rts = orc.window()
+            assert_bits(wp[k].cpu().numpy(), rpr, f"window price launch {l} step {k}")
+            assert_bits(wo[k].cpu().numpy(), rpo, f"window portfolio launch {l} step {k}")
+            assert np.array_equal(wt[k].cpu().numpy().astype(np.uint64), rts)
+    assert dones > 0

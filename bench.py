@@ -10,18 +10,20 @@ U{0,1,2} (Philox, pre-generated on device) turned into units by DQN's
 action_to_transaction (unit_size .05 of available margin), in-kernel
 auto-reset.  A "step" advances every env by one tick and materialises every
 per-step output of the reference's Env.step (State row, reward, done,
-BrokerResponse) plus the shaped reward; `--fuse` steps run per launch with the
-state held in registers.
+BrokerResponse) plus the shaped reward; `--fuse` (256) steps run per launch
+with the state held in registers (every step's outputs are written to a
+(K, N, ...) trajectory).
 
 For N>1 (torchrun, one process per GPU) envs are sharded by global index
 (env_offset) with no per-step collective; one RCCL all-gather of the
 per-env episode statistics closes the timed region.  Prints one JSON line.
 
 The other BASELINE.json configs (SURVEY 8d) are selectable with --workload;
-they carry a W = 64 sliding window, so a step there is one Env step (K = 1
-launch, ring row written in-kernel) plus StackerDiscrete.current_data of every
-env (the window gather kernel), as the agent needs the observation before it
-acts:
+they carry a W = 64 sliding window, so a step there is one Env step plus
+StackerDiscrete.current_data of every env, as the agent reads one window per
+step: `--win-fuse` (64) steps per launch append every ring push to a launch
+history, and a second kernel writes all K windows (mgn_rollout_hist /
+mgn_window_hist):
   C2  4096 envs x 4 OU (mu 10, theta .08, phi .04), 2% cost, DSR, norm none
   C4  8192 envs/GPU x 8 Composite (Synth 2 + OU 3 + TrendOU 3), 2% cost,
       PPC (target [1,0..0], alpha .01) over the env log reward, norm log
@@ -228,7 +230,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2048)
     ap.add_argument("--warmup", type=int, default=256)
-    ap.add_argument("--fuse", type=int, default=64)
+    ap.add_argument("--fuse", type=int, default=256)
     ap.add_argument("--win-fuse", type=int, default=64,
                     help="steps per launch of the windowed workloads (capped by --fuse)")
     ap.add_argument("--win-overlap", action="store_true",

@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo; cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
-B="python bench.py --steps 256 --warmup 64 --no-cpu-baseline"
+B="python bench.py --steps 512 --warmup 256 --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- $B > $OUT/kt.log 2>&1 || { echo "kt failed"; tail -20 $OUT/kt.log; exit 1; }
 timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM --output-format csv -d $OUT/pmc1 -o pmc1 -- $B > $OUT/pmc1.log 2>&1 || { echo "pmc1 failed"; tail -20 $OUT/pmc1.log; exit 1; }

@@ -204,6 +204,12 @@ struct Lane {
   bool valid[M];
   int64_t rcur;  // replay: next tape row (same in every lane of the segment)
   int64_t row;   // replay: tape row of the current State
+  // replay prefetch: row rcur's prices (and this lane's feature column fcol,
+  // when every feature has a lane) are loaded one tick ahead, so a tick's
+  // tape reads leave the step's dependency chain
+  double pfP[M], pfF, curF;
+  int fcol = -1;       // feature column of this lane (-1: features read per row)
+  bool pf_ok = false;  // pfP / pfF hold row rcur
 };
 
 // ---------------------------------------------------------------------------
@@ -329,11 +335,19 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
     // row iterCache / loadData would serve, then advance (wrap = the
     // reference's rewind to boundsIdx_.first, :368-371, :397-399)
     const int64_t row = s.rcur;
+    const bool fown = s.fcol >= 0 && s.fcol < p.F;
 #pragma unroll
     for (int m = 0; m < M; ++m)
-      if (s.valid[m]) s.P[m] = p.rp_price[(size_t)row * p.A + s.asset[m]];
+      if (s.valid[m]) s.P[m] = s.pf_ok ? s.pfP[m] : p.rp_price[(size_t)row * p.A + s.asset[m]];
+    if (fown) s.curF = s.pf_ok ? s.pfF : p.rp_feat[(size_t)row * p.F + s.fcol];
     s.row = row;
     s.rcur = (row + 1 == p.rp_rows) ? 0 : row + 1;
+    // the next tick reads row rcur (a source reset keeps the cursor)
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+      if (s.valid[m]) s.pfP[m] = p.rp_price[(size_t)s.rcur * p.A + s.asset[m]];
+    if (fown) s.pfF = p.rp_feat[(size_t)s.rcur * p.F + s.fcol];
+    s.pf_ok = true;
     return;
   }
   const uint64_t genv = (uint64_t)(p.env_offset + env);
@@ -484,7 +498,9 @@ __device__ __forceinline__ double log_norm(double x) { return log((x < 1e-5) ? 1
 template <int M, int S>
 __device__ __forceinline__ void put_feats(const Lane<M>& s, const KParams& p, int ls,
                                           double* __restrict__ dst, bool lg = false) {
-  if (p.replay) {
+  if (p.replay && s.fcol >= 0) {
+    if (s.fcol < p.F) dst[s.fcol] = lg ? log_norm(s.curF) : s.curF;
+  } else if (p.replay) {
     for (int f = ls; f < p.F; f += S) {
       const double v = p.rp_feat[(size_t)s.row * p.F + f];
       dst[f] = lg ? log_norm(v) : v;
@@ -627,6 +643,8 @@ __device__ __forceinline__ void load_lane(Lane<M>& s, const KParams& p, int env,
   }
   s.rcur = p.replay ? p.rcur[env] : 0;
   s.row = 0;
+  s.pf_ok = false;
+  s.fcol = -1;
 }
 
 template <int M>
@@ -1199,6 +1217,13 @@ __device__ __forceinline__ void nstep_column(const KParams& p, double* out, int 
 // step(assetIdx, units) / discrete actions via action_to_transaction.
 // RQ1: required_margin == 1.0, where x / required_margin == x exactly and the
 // divisions are skipped.  NST: n-step aggregation (nstep > 1) compiled in.
+// speculative Broker resolution for one asset per lane (defined in mgn_duo.h)
+template <int S, bool RQ1>
+__device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRecs<S>& er,
+                                            double& cash, const double (&uc)[1], double (&tp)[1],
+                                            double (&tu)[1], double (&tc)[1], int (&rk)[1], int ls,
+                                            Sums& after, int& any_mc);
+
 template <int M, int S, bool RQ1, bool NST>
 __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_kind,
                                                 const double* __restrict__ units_in,
@@ -1250,6 +1275,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
 
   Lane<M> s;
   load_lane<M>(s, p, env, ls);
+  if (p.replay && p.F <= S) s.fcol = ls;  // one feature column per lane: prefetched
   double cash = p.cash[env];
   uint64_t ts = p.ts[env];
   double shA[M], shB[M];  // shaper state: slot values for D==A, [0] for D==1
@@ -1363,7 +1389,13 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
       if (in_kind != IN_NONE) {
         if constexpr (XCH) {
           if (!(p.ablate & 1)) {
-            broker_x<M, S, RQ1>(s, p, recs[tid / S], cash, s0, uc, tp, tu, tc, rk, ls, sa, any_mc);
+            if constexpr (M == 1) {
+              // one asset per lane: the speculative resolution of the two-role
+              // kernel (mgn_duo.h) -- one pass when no order is refused
+              broker_spec<S, RQ1>(s, p, recs[tid / S], cash, uc, tp, tu, tc, rk, ls, sa, any_mc);
+            } else {
+              broker_x<M, S, RQ1>(s, p, recs[tid / S], cash, s0, uc, tp, tu, tc, rk, ls, sa, any_mc);
+            }
           }
         } else {
           if (!(p.ablate & 1)) Rounds<M, S, 0>::run(s, p, cash, uc, tp, tu, tc, rk, ls);

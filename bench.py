@@ -243,7 +243,7 @@ def main():
                     help="also time 1/16/64/256 steps per launch (separate launches; keep it off "
                          "when profiling, so the kernel's rocprof average is the headline's)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--workload", default="C3", choices=["C2", "C3", "C4", "C5"])
+    ap.add_argument("--workload", default="C3", choices=["C1", "C2", "C3", "C4", "C5"])
     args = ap.parse_args()
 
     import torch
@@ -258,6 +258,8 @@ def main():
     dev = torch.device(f"cuda:{local_rank}")
     torch.cuda.set_device(dev)
 
+    if args.workload == "C1":
+        return c1_latency(args, world, rank, dev)
     if args.workload != "C3":
         return windowed(args, world, rank, dev)
     N, A, F = args.n_envs, args.assets, args.fuse
@@ -369,6 +371,53 @@ def main():
         print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()
+
+
+def c1_latency(args, world, rank, dev):
+    """C1: the Python-level Env.step latency of one env -- the
+    drop-in madigan_amd.Env (one 1-asset sine, no costs, env log reward)
+    called per step from Python as the reference agent calls its pybind11 Env
+    (each step returns host State / reward / done / EnvInfo, so it launches
+    and synchronises once per step).  Beside it the oracle's one-env step
+    through ctypes on one host core.  Rank 0 only; latency, lower is better."""
+    import torch
+    from madigan_amd import Env
+    if rank != 0:
+        return
+    T = max(1000, args.steps * 5)
+    cfg = {"data_source_type": "Synth",
+           "data_source_config": {"freq": [1.0], "mu": [2.0], "amp": [1.0], "phase": [0.0],
+                                  "dX": 0.01, "noise": 0.0}}
+    env = Env("Synth", 1_000_000.0, cfg, device=dev, seed=0x6D6165)
+    rng = np.random.default_rng(1)
+    units = rng.integers(-1, 2, size=(T + 200, 1)).astype(np.float64) * 10.0
+    for t in range(200):
+        env.step(units[t])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(T):
+        env.step(units[200 + t])
+    torch.cuda.synchronize()
+    us = (time.perf_counter() - t0) / T * 1e6
+    res = {"metric": "Env.step latency (C1: 1 env x 1 asset, Python per-step call)", "value": us,
+           "unit": "us/step", "n_gpus": 1, "steps": T, "warmup": 200, "ms_per_step": us / 1e3,
+           "higher_is_better": False, "scaling": "none", "vs_baseline": None, "dtype": "f64",
+           "data": "synthetic",
+           "config": {"workload": "C1: Synth sine freq 1 mu 2 amp 1 phase 0 dX .01 noise 0, no costs, "
+                                  "env log reward, Env.step(units) from Python"}}
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, ROOT)
+        from oracle import oracle as O
+        orc = O.OracleBatch(dict(n_envs=1, seed=0x6D6165), [(O.SRC_SINE, [1.0, 2.0, 1.0, 0.0, 0.01, 0.0])])
+        for t in range(200):
+            orc.step(units[t].reshape(1, 1))
+        t0 = time.perf_counter()
+        for t in range(T):
+            orc.step(units[200 + t].reshape(1, 1))
+        cus = (time.perf_counter() - t0) / T * 1e6
+        res["cpu_baseline"] = {"value": cus, "unit": "us/step", "cores": 1, "kind": "port",
+                               "sample": f"C1, {T} steps of the oracle's one-env step through ctypes"}
+    print(json.dumps(res))
 
 
 def windowed(args, world, rank, dev):

@@ -82,6 +82,32 @@ def load_pmc_traffic(workload: str):
         return None
 
 
+# MI355X: 256 CUs x 4 SIMDs; a wave64 VALU instruction occupies its SIMD for
+# at least 4 cycles (16 lanes per cycle; fp64 FMA at full rate, transcendental
+# and fp64 divide / sqrt steps longer); peak engine clock 2.4 GHz
+N_SIMD = 1024
+SIMD_CYCLES_PER_VALU = 4
+CLOCK_HZ = 2.4e9
+
+
+def valu_issue(workload: str, launch_s: float):
+    """The step kernel's VALU issue against the SIMDs' capacity, from the
+    committed rocprofv3 PMC SQ_INSTS_VALU per launch (profiles/pmc_valu.json):
+    a lower bound on the fraction of SIMD cycles spent issuing VALU work (the
+    bound that limits this kernel; the HBM roofline above is far from it)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_valu.json")) as f:
+            n = json.load(f).get(workload)
+    except (OSError, ValueError):
+        n = None
+    if not n:
+        return None
+    busy = n * SIMD_CYCLES_PER_VALU / N_SIMD / (launch_s * CLOCK_HZ)
+    return {"valu_wave_insts_per_launch": n, "simd_cycles_per_launch": launch_s * CLOCK_HZ,
+            "valu_busy_frac_lower_bound": busy,
+            "note": "SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x launch cycles at 2.4 GHz)"}
+
+
 def host_threads() -> int:
     """The host-core share this process may use (OMP_NUM_THREADS on the GPU
     box, which is 16 there; else the affinity mask)."""
@@ -361,7 +387,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": achieved_gbs / PEAK_HBM_GBS,
                          "traffic": traffic, "kernel": kernel_name(env, A),
-                         "bytes_per_env_step": bpes, "avg_launch_us": avg_launch_s * 1e6},
+                         "bytes_per_env_step": bpes, "avg_launch_us": avg_launch_s * 1e6,
+                         "compute_issue": valu_issue(workload, avg_launch_s)},
             "episodes_completed": episodes,
         }
         if sweep:

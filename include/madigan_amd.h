@@ -25,6 +25,10 @@
  *                     staged by libmadigan_hdf.so (include/madigan_hdf.h)
  *   mgn_window*       StackerDiscrete.stream_state / current_data
  *                     (madigan/utils/preprocessor.py:143-199)
+ *   mgn_rollout_hist  K x { env.step; preprocessor.stream_state; current_data }
+ *   mgn_window_hist   of the agent loop (madigan/modelling/algorithm/
+ *   mgn_rollout_window offpolicy_q.py:143, 193-194): K steps in one launch,
+ *                     then every step's window
  *   mgn_get_views     zero-copy property views (env.cpp:897-913)
  *   mgn_last_error    pybind11 exception translation (DataTypes.h:36-46)
  *

@@ -715,9 +715,8 @@ int mgn_rollout_hist(mgn_env* e, const int8_t* actions_dev, int32_t k_steps, con
   e->hcur = b;
   hb.rows = (int)rows;
   const mgn::RingDesc r = ring_desc(e);
-  const int64_t pt = (int64_t)e->N * e->W * C;
-  hipLaunchKernelGGL(mgn::k_hist_prefix, dim3((unsigned)((pt + 255) / 256)), dim3(256), 0, e->stream,
-                     r, hb.hist, hb.ts, (int)rows);
+  hipLaunchKernelGGL(mgn::k_hist_prefix, dim3((unsigned)e->N), dim3(256), 0, e->stream, r, hb.hist,
+                     hb.ts, (int)rows);
   time_mark(e, e->t_step, e->stream);
   e->hist_on = true;
   launch_step(e, *out, mgn::IN_DISCRETE, nullptr, nullptr, actions_dev, (int)k_steps);

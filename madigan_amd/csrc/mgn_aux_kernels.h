@@ -359,22 +359,26 @@ struct HistDesc {
   const int32_t* hlen;
 };
 
-// rows [W - len, W) of every env's history := its ring window, oldest first
+// rows [W - len, W) of every env's history := its ring window, oldest first.
+// A workgroup per env: the window is at most two contiguous runs of the ring
+// (before and after the wrap), so the copy is two coalesced streams, no
+// per-element division.
 __global__ __launch_bounds__(BLOCK) void k_hist_prefix(RingDesc r, double* __restrict__ hist,
                                                        uint64_t* __restrict__ hist_ts, int hrows) {
-  const int C = r.F + r.Pn;
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (int64_t)r.N * r.W * C) return;
-  const int env = (int)(gid / ((int64_t)r.W * C));
-  const int rem = (int)(gid - (int64_t)env * r.W * C);
-  const int i = rem / C, c = rem - (rem / C) * C;
+  const int C = r.F + r.Pn, W = r.W;
+  const int env = blockIdx.x;
   const int len = r.len[env];
-  if (i >= len) return;
-  int row = r.head[env] - len + 1 + i;
-  if (row < 0) row += r.W;
-  const int dst = r.W - len + i;
-  hist[((size_t)env * hrows + dst) * C + c] = r.ring[((size_t)env * r.W + row) * C + c];
-  if (c == 0) hist_ts[(size_t)env * hrows + dst] = r.ring_ts[(size_t)env * r.W + row];
+  if (len <= 0) return;
+  const int first = (r.head[env] - len + 1 + W) % W;  // oldest row
+  const int nA = min(len, W - first);                 // rows before the wrap
+  const double* src = r.ring + (size_t)env * W * C;
+  double* dst = hist + ((size_t)env * hrows + (W - len)) * C;
+  const int n = len * C, na = nA * C;
+  for (int i = threadIdx.x; i < n; i += BLOCK)
+    dst[i] = (i < na) ? src[first * C + i] : src[i - na];
+  const uint64_t* tsrc = r.ring_ts + (size_t)env * W;
+  uint64_t* tdst = hist_ts + (size_t)env * hrows + (W - len);
+  for (int i = threadIdx.x; i < len; i += BLOCK) tdst[i] = (i < nA) ? tsrc[first + i] : tsrc[i - nA];
 }
 
 // every step's StackerDiscrete.current_data: a workgroup per (env, ks

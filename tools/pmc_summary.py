@@ -61,6 +61,10 @@ def main():
         json.dump(d, open(tj, "w"), indent=1, sort_keys=True)
     if "SQ_WAVES" in c and "SQ_INSTS_VALU" in c:
         summary["valu_insts_per_wave"] = c["SQ_INSTS_VALU"] / c["SQ_WAVES"]
+        vj = os.path.join(out, "pmc_valu.json")
+        d = json.load(open(vj)) if os.path.exists(vj) else {}
+        d[a.workload] = c["SQ_INSTS_VALU"]  # wave-level VALU instructions per launch
+        json.dump(d, open(vj, "w"), indent=1, sort_keys=True)
     json.dump(summary, open(os.path.join(out, f"{a.tag}_pmc_summary.json"), "w"), indent=1)
     print(json.dumps(summary, indent=1))
 

@@ -149,3 +149,43 @@ def test_replay_tape_given_directly_and_sharding(gpu):
     cur = full.replay_cursor.cpu().numpy()
     steps = 1 + K + (of["done"].cpu().numpy().sum(axis=0))  # each auto-reset ticks once
     assert np.array_equal(cur, (np.arange(N) * 13 + steps) % P)
+
+
+@pytest.mark.parametrize("A,F,window,norm", [(16, 16, 8, None), (4, 3, 6, "log"), (3, 5, 8, "lookback")])
+def test_replay_window_history(gpu, tmp_path, A, F, window, norm):
+    """The windowed agent loop on a replay source (the C5 path): K steps in one
+    launch with every step's window (mgn_rollout_hist / mgn_window_hist) equal
+    the oracle's window after each step; feature columns come from the tape
+    (prefetched one tick ahead when every feature has a lane)."""
+    from madigan_amd import BatchedEnv
+    from madigan_amd.config import spec_from_config
+    path, price, feats, ts = replay_file(tmp_path, T=400, A=A, F=F, seed=A + 1)
+    start, end = int(ts[3]) + 1, int(ts[-5])
+    spec = spec_from_config(hdf_config(path, 50, start, end))
+    N, K = 48, 20
+    kw = dict(required_margin=0.1, maintenance_margin=0.25, slippage_rel=1e-4,
+              transaction_cost_rel=0.002, reward_shaper="DDR", adaptation_rate=0.001,
+              unit_size=0.5, auto_reset=True, window=window, norm_type=norm, seed=5)
+    g = BatchedEnv(spec, N, device=gpu, replay_stride=13, **kw)
+    first, second, _, _ = O.hdf_bounds(ts, start, end)
+    okw = dict(kw, n_envs=N, n_feats=F, auto_reset=1)
+    orc = O.OracleBatch(okw, [(O.SRC_REPLAY, [])] * A)
+    orc.set_replay(price, feats, ts, first, second, 50, 13)
+    acts = g.generate_actions(2 * K, seed=4)
+    a = acts.cpu().numpy()
+    dones = 0
+    for half in range(2):  # two launches: the second starts from the first's ring
+        out, (wp, wo, wt) = g.rollout_window(acts[half * K:(half + 1) * K], per_step=True)
+        for k in range(K):
+            r = orc.rollout(a[half * K + k:half * K + k + 1])
+            dones += int(r["done"].sum())
+            assert_bits(out["obs_price"][k].cpu().numpy(), r["obs_price"][0], f"obs_price {half}/{k}")
+            rpr, rpo, rts = orc.window()
+            if norm is None:
+                assert_bits(wp[k].cpu().numpy(), rpr, f"window price {half}/{k}")
+            else:
+                close(wp[k].cpu().numpy(), rpr, f"window price {half}/{k}",
+                      rtol=1e-14 if norm == "lookback" else 1e-12)
+            assert_bits(wo[k].cpu().numpy(), rpo, f"window portfolio {half}/{k}")
+            assert np.array_equal(wt[k].cpu().numpy().astype(np.uint64), rts)
+    assert dones > 0 or A == 1

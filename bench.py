@@ -71,15 +71,54 @@ def bytes_per_env_step(A: int, fuse: int, D: int = 1, agent_reward: bool = False
     return per_step + state / fuse
 
 
+def survey_bytes_per_env_step(env) -> float:
+    """SURVEY 8d's algorithmic bytes per env-step: per asset 113 (ledger,
+    meanEntry, borrowed, price read + write 64; action 8; broker response 25;
+    observation row + ledgerNormedFull entry 16) plus the generator's state
+    (OU 0, Sine 16, TrendOU 48), per env 105 (cash r/w 16, DSR/DDR A,B 32,
+    reward 8, done 1, ledgerNormedFull cash entry 8, timestamp r/w 16, episode
+    stats 24).  C3: 8 x (113 + 48) + 105 = 1393."""
+    from madigan_amd import _lib as L
+    extra = {L.SRC_OU: 0, L.SRC_SINE: 16, L.SRC_TRENDOU: 48}
+    return float(sum(113 + extra.get(k, 48) for k in env.spec.kinds) + 105)
+
+
 def load_pmc_traffic(workload: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    """(HBM bytes per launch, key) from the committed rocprofv3 PMC summary:
+    the workload's own entry, else the entry with the nearest steps per launch
+    of the same shape (its key says which)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(workload)
     except (OSError, ValueError):
-        return None
+        return None, None
+    if workload in d:
+        return d[workload], workload
+    stem, _, k = workload.rpartition("_fuse")
+    cands = [(abs(int(key.rpartition("_fuse")[2]) - int(k)), key) for key in d
+             if key.startswith(stem + "_fuse") and key.rpartition("_fuse")[2].isdigit()]
+    if not cands or not k.isdigit():
+        return None, None
+    key = min(cands)[1]
+    return d[key], key
+
+
+def bandwidth_probe(dev, nbytes: int = 1 << 30, reps: int = 10):
+    """Attainable HBM bandwidth on this box: the library's
+    16-B-per-lane copy kernel over two 1 GiB buffers; (read + write) GB/s."""
+    import ctypes as C
+    import torch
+    from madigan_amd import _lib as L
+    lib = L.load()
+    src = torch.empty(nbytes, dtype=torch.uint8, device=dev).fill_(1)
+    dst = torch.empty_like(src)
+    out = C.c_double()
+    L.check(lib.mgn_bandwidth_probe(C.c_void_p(dst.data_ptr()), C.c_void_p(src.data_ptr()), nbytes,
+                                    reps, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream),
+                                    C.byref(out)))
+    del src, dst
+    return out.value
 
 
 # MI355X: 256 CUs x 4 SIMDs; a wave64 VALU instruction occupies its SIMD for
@@ -270,6 +309,11 @@ def main():
                          "when profiling, so the kernel's rocprof average is the headline's)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--workload", default="C3", choices=["C1", "C2", "C3", "C4", "C5"])
+    ap.add_argument("--no-probe", dest="probe", action="store_false",
+                    help="skip the attainable-bandwidth copy probe")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1: nccl (RCCL; the statistics all-gather is the C ABI's "
+                         "mgn_stats_allgather) or gloo (several ranks may share one GPU)")
     args = ap.parse_args()
 
     import torch
@@ -278,7 +322,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 and args.dist_backend == "gloo":
+        # gloo rehearsal of the sharded path: ranks may share one GPU
+        dist.init_process_group("gloo")
+        local_rank = local_rank % max(1, torch.cuda.device_count())
+    elif world > 1:
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
     dev = torch.device(f"cuda:{local_rank}")
@@ -292,59 +340,79 @@ def main():
     env, _, _ = workload_env("C3", N, A, rank, dev)
     if args.layout:
         env.lib.mgn_set_layout(env.h, args.layout)
+    import ctypes as C
+    from madigan_amd import _lib as L
+    lib, h = env.lib, env.h
     total = args.warmup + args.steps
     actions = env.generate_actions(total, seed=0x6D6164)
     traj = env.alloc_traj(F, fields=[f for f in ("reward", "shaped", "done", "obs_price", "obs_port",
                                                  "timestamp", "tprice", "tunits", "tcost", "risk",
                                                  "margin_call")])
-    stream = torch.cuda.current_stream(dev)
+    base, per = actions.data_ptr(), N * A
 
-    def run(k0: int, k1: int, ev=None):
-        k = k0
+    # one launcher per launch length (the mgn_traj is validated once, outside
+    # the timed region); the timed loop is one ctypes call per launch
+    outs, launchers = {}, {}
+
+    def launcher(n):
+        if n not in launchers:
+            outs[n] = traj if n == F else {k: v[:n] for k, v in traj.items()}
+            launchers[n] = env.rollout_launcher(outs[n], n)
+        return launchers[n]
+
+    def plan(k0, k1):
+        seq, k = [], k0
         while k < k1:
             n = min(F, k1 - k)
-            out = traj if n == F else {kk: v[:n] for kk, v in traj.items()}
-            if ev is not None:
-                ev[0].append(torch.cuda.Event(enable_timing=True))
-                ev[0][-1].record(stream)
-            env.rollout(actions[k:k + n], out=out)
-            if ev is not None:
-                ev[1].append(torch.cuda.Event(enable_timing=True))
-                ev[1][-1].record(stream)
-                ev[2].append(n)
+            seq.append((launcher(n), base + k * per, n))
             k += n
+        return seq
 
-    run(0, args.warmup)
+    def run(seq):
+        rc = 0
+        for fn, ptr, _ in seq:
+            rc |= fn(ptr)
+        return rc
+
+    warm, timed = plan(0, args.warmup), plan(args.warmup, total)
+    # kernel durations: HIP events around each step launch on the handle's
+    # stream (mgn_set_timing; pooled events, created during the warmup)
+    L.check(lib.mgn_set_timing(h, 1), h)
+    L.check(run(warm), h)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ev = ([], [], [])
+    L.check(lib.mgn_set_timing(h, 1), h)
     t0 = time.perf_counter()
-    run(args.warmup, total, ev)
-    stats = env.episode_stats
+    rc = run(timed)
     if world > 1:
-        gathered = torch.empty((world * N, 4), dtype=torch.float64, device=dev)
-        dist.all_gather_into_tensor(gathered, stats)
+        from madigan_amd.distributed import allgather_env_stats
+        gathered = allgather_env_stats(env, n_total=world * N)
     else:
-        gathered = stats
+        gathered = env.episode_stats
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    L.check(rc, h)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        if args.dist_backend == "gloo":
+            t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-
-    full = [i for i, n in enumerate(ev[2]) if n == F]
-    launch_ms = [ev[0][i].elapsed_time(ev[1][i]) for i in full] or [
-        ev[0][i].elapsed_time(ev[1][i]) for i in range(len(ev[2]))]
-    avg_launch_s = float(np.mean(launch_ms)) / 1e3
-    steps_per_launch = F if full else ev[2][0]
-    bpes = bytes_per_env_step(A, steps_per_launch, env.D)
-    achieved_gbs = N * steps_per_launch * bpes / avg_launch_s / 1e9
+    tm = (C.c_double * 4)()
+    L.check(lib.mgn_get_timing(h, tm), h)
+    L.check(lib.mgn_set_timing(h, 0), h)
+    n_launch = int(tm[1])
+    avg_launch_s = tm[0] / max(n_launch, 1) / 1e3
+    steps_per_launch = args.steps / max(n_launch, 1)
+    units_per_launch = N * steps_per_launch
+    bpes = survey_bytes_per_env_step(env)
+    achieved_gbs = units_per_launch * bpes / avg_launch_s / 1e9
+    fused = bytes_per_env_step(A, steps_per_launch, env.D)
     value = world * N * args.steps / elapsed
     episodes = int(gathered[:, 3].sum().item())
 
@@ -352,25 +420,44 @@ def main():
     # outside the timed region, rank 0 only
     sweep = {}
     if rank == 0 and args.sweep:
+        stream = torch.cuda.current_stream(dev)
         big = env.alloc_traj(256, fields=list(traj.keys()))
         for K in (1, 16, 64, 256):
             reps = max(2, 512 // K)
             s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            out = {kk: v[:K] for kk, v in big.items()}
-            env.rollout(actions[:K], out=out)  # warm
+            fn = env.rollout_launcher({kk: v[:K] for kk, v in big.items()}, K)
+            fn(base)  # warm
             s_ev.record(stream)
             for r in range(reps):
-                env.rollout(actions[:K], out=out)
+                fn(base)
             e_ev.record(stream)
             torch.cuda.synchronize()
             us = s_ev.elapsed_time(e_ev) * 1e3 / (reps * K)
-            b = bytes_per_env_step(A, K, env.D)
             sweep[str(K)] = {"us_per_step": us, "env_steps_per_s": N / us * 1e6,
-                             "bytes_per_env_step": b, "achieved_GBs": N * b / us / 1e3}
+                             "achieved_GBs_survey_bytes": N * bpes / us / 1e3,
+                             "fused_bytes_per_env_step": bytes_per_env_step(A, K, env.D)}
 
     if rank == 0:
-        workload = f"C3_trendou_{N}x{A}_fuse{steps_per_launch}"
-        traffic = load_pmc_traffic(workload)
+        K = int(round(steps_per_launch))
+        workload = f"C3_trendou_{N}x{A}_fuse{K}"
+        traffic, traffic_key = load_pmc_traffic(workload)
+        probe = bandwidth_probe(dev) if args.probe else None
+        roof = {"bound": "hbm", "achieved": achieved_gbs, "peak": PEAK_HBM_GBS,
+                "unit": "GB/s", "frac": achieved_gbs / PEAK_HBM_GBS,
+                "traffic": traffic, "traffic_key": traffic_key,
+                "kernel": kernel_name(env, A),
+                "bytes_per_env_step": bpes,
+                "bytes_note": "SURVEY 8d algorithmic bytes per env-step (C3: 8 x (113 + 48) + 105): "
+                              "state r/w + actions + outputs per step",
+                "units_per_launch": units_per_launch, "avg_launch_us": avg_launch_s * 1e6,
+                "fused_bytes_per_env_step": fused,
+                "fused_achieved_GBs": units_per_launch * fused / avg_launch_s / 1e9,
+                "fused_note": "what the fused kernel must move (state held in registers across "
+                              "the launch's steps; PMC traffic matches this figure)",
+                "compute_issue": valu_issue(workload, avg_launch_s)}
+        if probe:
+            roof["attainable_copy_GBs"] = probe
+            roof["frac_of_attainable"] = achieved_gbs / probe
         res = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
@@ -381,14 +468,12 @@ def main():
                                    "auto-reset",
                        "n_envs_per_gpu": N, "n_assets": A, "window": 0,
                        "steps_per_launch": steps_per_launch,
-                       "assets_per_lane": int(env.lib.mgn_get_layout(env.h)),
-                       "schedule": "duo" if int(env.lib.mgn_get_schedule(env.h)) == 2 else "single",
-                       "parallelism": f"env-sharded x{world} (no per-step collective)"},
-            "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": PEAK_HBM_GBS,
-                         "unit": "GB/s", "frac": achieved_gbs / PEAK_HBM_GBS,
-                         "traffic": traffic, "kernel": kernel_name(env, A),
-                         "bytes_per_env_step": bpes, "avg_launch_us": avg_launch_s * 1e6,
-                         "compute_issue": valu_issue(workload, avg_launch_s)},
+                       "assets_per_lane": int(lib.mgn_get_layout(h)),
+                       "schedule": "duo" if int(lib.mgn_get_schedule(h)) == 2 else "single",
+                       "parallelism": f"env-sharded x{world} (no per-step collective)"
+                                      + (f", {args.dist_backend}" if world > 1 else "")},
+            "roofline": roof,
+            "kernel_us_per_step": avg_launch_s * 1e6 / steps_per_launch,
             "episodes_completed": episodes,
         }
         if sweep:
@@ -502,12 +587,11 @@ def windowed(args, world, rank, dev):
     L.check(lib.mgn_set_timing(h, 1), h)
     t0 = time.perf_counter()
     run(n_warm, n_warm + n_time)
-    stats = env.episode_stats
     if world > 1:
-        gathered = torch.empty((world * N, 4), dtype=torch.float64, device=dev)
-        dist.all_gather_into_tensor(gathered, stats)
+        from madigan_amd.distributed import allgather_env_stats
+        gathered = allgather_env_stats(env, n_total=world * N)
     else:
-        gathered = stats
+        gathered = env.episode_stats
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -515,6 +599,8 @@ def windowed(args, world, rank, dev):
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        if args.dist_backend == "gloo":
+            t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     tm = (C.c_double * 4)()
@@ -537,7 +623,7 @@ def windowed(args, world, rank, dev):
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
-                         "traffic": load_pmc_traffic(f"{wl}_gather_{N}x{A}_W{W}"),
+                         "traffic": load_pmc_traffic(f"{wl}_gather_{N}x{A}_W{W}")[0],
                          "kernel": "mgn::k_hist_gather",
                          "bytes_per_env_step": gb / (N * Kf),
                          "avg_launch_us": gather_us},

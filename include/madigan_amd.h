@@ -20,6 +20,13 @@
  *                     dqn.py:160-179); Env::step(units) } fused in one launch
  *   mgn_set_prices    DataSourceTick plug-in fed from the host
  *                     (DataSource.h:48-64, PyDataSource.h:9-24, Env.h:174-179)
+ *   mgn_set_sources   Env::setDataSource (Env.h:174-179): swap the source,
+ *                     keep the Broker / Portfolio
+ *   mgn_stats_allgather the episode-statistics all-gather of the sharded path
+ *                     (run/trainer.py:277-281 consumes the stats)
+ *   mgn_save_state /  checkpoint / resume of the env state (the reference
+ *   mgn_load_state    resumes through agent checkpoints only,
+ *                     modelling/algorithm/base.py:153-186; Env.h:31)
  *   mgn_attach_replay HDFSourceSingle as the env's DataSource (DataSource.h:89-149,
  *                     DataSource.cpp:194-408): the device-resident replay tape
  *                     staged by libmadigan_hdf.so (include/madigan_hdf.h)
@@ -45,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MGN_ABI_VERSION 5
+#define MGN_ABI_VERSION 6
 #define MGN_MAX_ASSETS 64
 #define MGN_MAX_NSTEP 64
 
@@ -253,6 +260,16 @@ int mgn_rollout(mgn_env *env, const int8_t *actions_dev, int32_t k_steps, const 
 int mgn_rollout_units(mgn_env *env, const double *units_dev, int32_t k_steps, const mgn_traj *out);
 /* prices (N,A) consumed by the next getData of MGN_SRC_EXTERNAL assets */
 int mgn_set_prices(mgn_env *env, const double *prices_dev);
+/* Env::setDataSource (Env.h:174-179; PyDataSource.h:9-15): swap the price
+ * source of every env in place.  Ledger, cash, mean entry, borrowed margin,
+ * shaper, window and statistics are kept, as the reference keeps its Broker /
+ * Portfolio.  sources (host, n_assets entries): MGN_SRC_EXTERNAL (a host
+ * DataSourceTick that feeds mgn_set_prices before each tick) or the asset's
+ * current kind with new parameters; replay handles cannot switch.
+ * prices_dev (N,A): the new source's currentPrices(), at which the Broker
+ * values the portfolio from now on (Env.h:177-178); NULL keeps the prices.
+ * Synchronises the handle's stream (the source table is uploaded). */
+int mgn_set_sources(mgn_env *env, const mgn_asset_source *sources, const double *prices_dev);
 /* attach the replay tape of a MGN_SRC_REPLAY handle and run the Env
  * constructor's first getData (Env.h:150-165) from it; stepping a replay
  * handle before this fails with MGN_ERR_CONFIG */
@@ -283,8 +300,9 @@ int mgn_rollout_window(mgn_env *env, const int8_t *actions_dev, int32_t k_steps,
  * complete once `stream` has passed the gather) */
 int mgn_set_window_stream(mgn_env *env, void *stream);
 /* kernel timing with HIP events on each kernel's own stream: on != 0 starts
- * (and clears) recording around the step kernel of mgn_rollout_hist and the
- * gather of mgn_window_hist; mgn_get_timing waits for them and returns
+ * (and clears) recording around the step kernel of mgn_rollout /
+ * mgn_rollout_hist and the gather of mgn_window_hist (events come from a
+ * per-handle pool, created once); mgn_get_timing waits for them and returns
  * {step ms total, step launches, gather ms total, gather launches} */
 int mgn_set_timing(mgn_env *env, int32_t on);
 int mgn_get_timing(mgn_env *env, double *out4);
@@ -327,6 +345,33 @@ int mgn_get_schedule(const mgn_env *env);
  * Broker rounds, bit 1 the generators, bit 2 the output stores, bit 3 the
  * logarithms of the agent reward.  Never set in product or parity runs. */
 int mgn_set_ablation(mgn_env *env, int32_t flags);
+/* The one collective of the sharded path: all-gather the (N,4)
+ * episode statistics of every rank over a caller-provided RCCL communicator
+ * (an ncclComm_t, e.g. torch's ProcessGroupNCCL._comm_ptr()), ordered on the
+ * handle's stream.  Each rank contributes rows_per_rank rows (>= N; 0 = N):
+ * its N rows of statistics, then zero rows, so ragged shards gather with one
+ * ncclAllGather; out_dev receives nranks * rows_per_rank * 4 doubles in rank
+ * order.  ncclAllGather is resolved from the RCCL the process has already
+ * loaded (else librccl.so.1), so the communicator and the call share one
+ * library instance. */
+int mgn_stats_allgather(mgn_env *env, void *nccl_comm, int32_t rows_per_rank, double *out_dev);
+/* Checkpoint / resume: the handle's whole device state (ledger,
+ * cash, generator and shaper state, window ring, n-step buffer, statistics,
+ * replay cursors, source table) plus its configuration, as one host blob of
+ * mgn_state_bytes() bytes.  mgn_save_state synchronises the stream;
+ * mgn_load_state restores the blob into a handle of the same dimensions
+ * (configuration, broker settings and RNG key included), so the restored
+ * handle continues every episode bit-exactly.  A replay tape is not part of
+ * the state: attach the same tape before loading. */
+size_t mgn_state_bytes(const mgn_env *env);
+int mgn_save_state(mgn_env *env, void *host_dst, size_t bytes);
+int mgn_load_state(mgn_env *env, const void *host_src, size_t bytes);
+/* Measurement only: the attainable HBM bandwidth of a plain
+ * device copy -- reps launches of a 16-B-per-lane grid-stride copy of bytes
+ * (a multiple of 16) from src_dev to dst_dev on stream, timed with HIP
+ * events; *gbps_out = (read + write bytes) / time in GB/s.  Synchronises. */
+int mgn_bandwidth_probe(void *dst_dev, const void *src_dev, size_t bytes, int32_t reps, void *stream,
+                        double *gbps_out);
 /* synchronise the handle's stream */
 int mgn_synchronize(mgn_env *env);
 const char *mgn_last_error(const mgn_env *env);

@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmadigan_hip.so")
 MAX_ASSETS = 64
-ABI_VERSION = 5
+ABI_VERSION = 6
 SRC_PARAMS = 64
 AUX_WIDTH = 24
 MAX_NSTEP = 64
@@ -105,6 +105,11 @@ SYMBOLS = {
     "mgn_rollout": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(Traj)]),
     "mgn_rollout_units": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(Traj)]),
     "mgn_set_prices": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mgn_set_sources": (C.c_int, [C.c_void_p, C.POINTER(AssetSource), C.c_void_p]),
+    "mgn_stats_allgather": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
+    "mgn_state_bytes": (C.c_size_t, [C.c_void_p]),
+    "mgn_save_state": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    "mgn_load_state": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     "mgn_attach_replay": (C.c_int, [C.c_void_p, C.POINTER(ReplayTape)]),
     "mgn_window_push": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mgn_window_clear": (C.c_int, [C.c_void_p, C.c_void_p]),
@@ -128,6 +133,8 @@ SYMBOLS = {
     "mgn_set_schedule": (C.c_int, [C.c_void_p, C.c_int32]),
     "mgn_get_schedule": (C.c_int, [C.c_void_p]),
     "mgn_set_ablation": (C.c_int, [C.c_void_p, C.c_int32]),
+    "mgn_bandwidth_probe": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int32, C.c_void_p,
+                                      C.POINTER(C.c_double)]),
     "mgn_synchronize": (C.c_int, [C.c_void_p]),
     "mgn_last_error": (C.c_char_p, [C.c_void_p]),
     "mgn_global_error": (C.c_char_p, []),

@@ -103,7 +103,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
 
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(compile_one, sources()))
-    cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs]
+    cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs, "-ldl"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

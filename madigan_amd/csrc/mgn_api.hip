@@ -3,7 +3,9 @@
 // One handle owns every device buffer of N envs in one arena (caller-provided
 // or hipMalloc'd), launches on one stream and never synchronises the host
 // except in mgn_create's parameter upload and mgn_synchronize.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <cmath>
 #include <cstdio>
@@ -83,8 +85,12 @@ struct mgn_env {
   hipStream_t wstream = nullptr;  // window stream (mgn_set_window_stream), null: the handle's
   // kernel timing (mgn_set_timing): start/stop event pairs on each kernel's stream
   bool timing = false;
-  std::vector<hipEvent_t> t_step, t_gather;
+  std::vector<hipEvent_t> t_step, t_gather;  // event pools, reused across mgn_set_timing calls
+  size_t t_step_n = 0, t_gather_n = 0;        // events recorded since mgn_set_timing
   bool hist_on = false;  // kparams() hands the history to the step kernel
+  // mgn_stats_allgather: the rank's padded send rows (rows_per_rank x 4)
+  double* ag_send = nullptr;
+  size_t ag_rows = 0;
 };
 
 namespace {
@@ -526,6 +532,7 @@ int mgn_destroy(mgn_env* e) {
   }
   for (hipEvent_t ev : e->t_step) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : e->t_gather) (void)hipEventDestroy(ev);
+  if (e->ag_send) (void)hipFree(e->ag_send);
   delete e;
   return MGN_OK;
 }
@@ -582,12 +589,16 @@ int mgn_step(mgn_env* e, int32_t kind, const double* units_dev, const int32_t* a
   return check_hip(e, hipGetLastError(), "mgn_step");
 }
 
+static void time_mark(mgn_env* e, std::vector<hipEvent_t>& v, size_t& n, hipStream_t st);
+
 int mgn_rollout(mgn_env* e, const int8_t* actions_dev, int32_t k_steps, const mgn_traj* out) {
   if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
   if (!actions_dev || !out) return fail(e, MGN_ERR_ARG, "null actions/out");
   if (k_steps < 1) return fail(e, MGN_ERR_LENGTH, "k_steps must be >= 1");
   if (need_tape(e) != MGN_OK) return MGN_ERR_CONFIG;
+  time_mark(e, e->t_step, e->t_step_n, e->stream);
   launch_step(e, *out, mgn::IN_DISCRETE, nullptr, nullptr, actions_dev, (int)k_steps);
+  time_mark(e, e->t_step, e->t_step_n, e->stream);
   return check_hip(e, hipGetLastError(), "mgn_rollout");
 }
 
@@ -604,6 +615,34 @@ int mgn_set_prices(mgn_env* e, const double* prices_dev) {
   if (!e || !prices_dev) return fail(e, MGN_ERR_ARG, "null handle/prices");
   return check_hip(e, hipMemcpyAsync(e->v.ext_prices, prices_dev, sizeof(double) * e->N * e->A,
                                      hipMemcpyDeviceToDevice, e->stream), "mgn_set_prices");
+}
+
+int mgn_set_sources(mgn_env* e, const mgn_asset_source* sources, const double* prices_dev) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  if (!sources) return fail(e, MGN_ERR_ARG, "null source table");
+  if (e->replay) return fail(e, MGN_ERR_CONFIG, "a replay handle cannot switch its data source");
+  std::vector<mgn_asset_source> cur(e->A);
+  int rc = check_hip(e, hipMemcpyAsync(cur.data(), e->src_dev, sizeof(mgn_asset_source) * e->A,
+                                       hipMemcpyDeviceToHost, e->stream), "mgn_set_sources (read)");
+  if (rc == MGN_OK) rc = check_hip(e, hipStreamSynchronize(e->stream), "mgn_set_sources (sync)");
+  if (rc != MGN_OK) return rc;
+  for (int i = 0; i < e->A; ++i) {
+    const int k = sources[i].kind;
+    if (k != MGN_SRC_EXTERNAL && k != cur[i].kind)
+      return fail(e, MGN_ERR_CONFIG, "asset " + std::to_string(i) +
+                                         ": a new source is MGN_SRC_EXTERNAL or the asset's current kind");
+  }
+  std::string msg;
+  const int st = validate(&e->cfg, sources, msg);
+  if (st != MGN_OK) return fail(e, st, msg);
+  std::memcpy(cur.data(), sources, sizeof(mgn_asset_source) * e->A);
+  rc = check_hip(e, hipMemcpyAsync(e->src_dev, cur.data(), sizeof(mgn_asset_source) * e->A,
+                                   hipMemcpyHostToDevice, e->stream), "mgn_set_sources (write)");
+  if (rc == MGN_OK && prices_dev)
+    rc = check_hip(e, hipMemcpyAsync(e->v.prices, prices_dev, sizeof(double) * e->N * e->A,
+                                     hipMemcpyDeviceToDevice, e->stream), "mgn_set_sources (prices)");
+  if (rc == MGN_OK) rc = check_hip(e, hipStreamSynchronize(e->stream), "mgn_set_sources (sync)");
+  return rc;
 }
 
 int mgn_window_push(mgn_env* e, const double* price_dev, const double* port_dev, const uint64_t* ts_dev) {
@@ -633,12 +672,14 @@ int mgn_window(mgn_env* e, double* price_dev, double* port_dev, uint64_t* ts_dev
   return check_hip(e, hipGetLastError(), "mgn_window");
 }
 
-static void time_mark(mgn_env* e, std::vector<hipEvent_t>& v, hipStream_t st) {
+static void time_mark(mgn_env* e, std::vector<hipEvent_t>& v, size_t& n, hipStream_t st) {
   if (!e->timing) return;
-  hipEvent_t ev;
-  if (hipEventCreate(&ev) != hipSuccess) return;
-  (void)hipEventRecord(ev, st);
-  v.push_back(ev);
+  if (n == v.size()) {
+    hipEvent_t ev;
+    if (hipEventCreate(&ev) != hipSuccess) return;
+    v.push_back(ev);
+  }
+  (void)hipEventRecord(v[n++], st);
 }
 
 static int grow(mgn_env* e, void** p, size_t bytes) {
@@ -665,10 +706,8 @@ int mgn_set_window_stream(mgn_env* e, void* stream) {
 int mgn_set_timing(mgn_env* e, int32_t on) {
   if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
   (void)hipDeviceSynchronize();
-  for (hipEvent_t ev : e->t_step) (void)hipEventDestroy(ev);
-  for (hipEvent_t ev : e->t_gather) (void)hipEventDestroy(ev);
-  e->t_step.clear();
-  e->t_gather.clear();
+  e->t_step_n = 0;
+  e->t_gather_n = 0;
   e->timing = on != 0;
   return MGN_OK;
 }
@@ -676,9 +715,10 @@ int mgn_set_timing(mgn_env* e, int32_t on) {
 int mgn_get_timing(mgn_env* e, double* out4) {
   if (!e || !out4) return fail(e, MGN_ERR_ARG, "null handle/out");
   const std::vector<hipEvent_t>* v[2] = {&e->t_step, &e->t_gather};
+  const size_t cnt[2] = {e->t_step_n, e->t_gather_n};
   for (int i = 0; i < 2; ++i) {
     double ms = 0.;
-    const size_t n = v[i]->size() / 2;
+    const size_t n = cnt[i] / 2;
     for (size_t j = 0; j < n; ++j) {
       float t = 0.f;
       (void)hipEventSynchronize((*v[i])[2 * j + 1]);
@@ -727,11 +767,11 @@ int mgn_rollout_hist(mgn_env* e, const int8_t* actions_dev, int32_t k_steps, con
   const mgn::RingDesc r = ring_desc(e);
   hipLaunchKernelGGL(mgn::k_hist_prefix, dim3((unsigned)e->N), dim3(256), 0, e->stream, r, hb.hist,
                      hb.ts, (int)rows);
-  time_mark(e, e->t_step, e->stream);
+  time_mark(e, e->t_step, e->t_step_n, e->stream);
   e->hist_on = true;
   launch_step(e, *out, mgn::IN_DISCRETE, nullptr, nullptr, actions_dev, (int)k_steps);
   e->hist_on = false;
-  time_mark(e, e->t_step, e->stream);
+  time_mark(e, e->t_step, e->t_step_n, e->stream);
   hb.k = k_steps;
   if (e->wstream) (void)hipEventRecord(hb.ready, e->stream);
   return check_hip(e, hipGetLastError(), "mgn_rollout_hist");
@@ -759,11 +799,11 @@ int mgn_window_hist(mgn_env* e, double* price_dev, double* port_dev, uint64_t* t
   const float wf = (float)(e->W * e->F), wp = (float)(e->W * (e->A + 1));
   hipStream_t st = e->wstream ? e->wstream : e->stream;
   if (e->wstream) (void)hipStreamWaitEvent(st, hb.ready, 0);
-  time_mark(e, e->t_gather, st);
+  time_mark(e, e->t_gather, e->t_gather_n, st);
   hipLaunchKernelGGL(mgn::k_hist_gather, dim3((unsigned)(e->N * kb)), dim3(256), lds, st, h,
                      price_dev, port_dev, ts_dev, ks, lds_rows, 1.0f / (float)e->F, 1.0f / (float)(e->A + 1),
                      1.0f / (float)e->W, 1.0f / wf, 1.0f / wp);
-  time_mark(e, e->t_gather, st);
+  time_mark(e, e->t_gather, e->t_gather_n, st);
   if (e->wstream) (void)hipEventRecord(hb.read, st);
   return check_hip(e, hipGetLastError(), "mgn_window_hist");
 }
@@ -782,7 +822,9 @@ int mgn_rollout_window(mgn_env* e, const int8_t* actions_dev, int32_t k_steps, c
 
 int mgn_generate_actions(mgn_env* e, int8_t* actions_dev, int32_t k_steps, uint64_t seed) {
   if (!e || !actions_dev) return fail(e, MGN_ERR_ARG, "null handle/actions");
+  if (k_steps < 1) return fail(e, MGN_ERR_LENGTH, "k_steps must be >= 1");
   const int64_t total = (int64_t)k_steps * e->N * e->A;
+  if ((total + 255) / 256 > (int64_t)0x7fffffff) return fail(e, MGN_ERR_LENGTH, "too many actions for one launch");
   hipLaunchKernelGGL(mgn::k_gen_actions, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                      e->stream, actions_dev, (int)k_steps, e->N, e->A, e->cfg.action_atoms, seed,
                      e->cfg.env_offset);
@@ -886,9 +928,9 @@ int mgn_set_schedule(mgn_env* e, int32_t schedule) {
   if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
   if (schedule < MGN_SCHED_AUTO || schedule > MGN_SCHED_DUO)
     return fail(e, MGN_ERR_CONFIG, "schedule must be MGN_SCHED_AUTO, _SINGLE or _DUO");
-  e->sched = schedule;
   if (schedule == MGN_SCHED_DUO && !duo_eligible(e))
     return fail(e, MGN_ERR_CONFIG, "the two-role kernel needs 2..8 assets, nstep 1, no replay tape");
+  e->sched = schedule;
   auto_layout(e);
   return MGN_OK;
 }
@@ -902,6 +944,126 @@ int mgn_get_layout(const mgn_env* e) { return e ? e->m : 0; }
 int mgn_set_ablation(mgn_env* e, int32_t flags) {
   if (!e) return MGN_ERR_ARG;
   e->ablate = flags;
+  return MGN_OK;
+}
+
+// RCCL entry points from the library instance the process already has loaded
+// (torch's, when the communicator is torch's); librccl.so.1 otherwise
+static void* rccl_sym(const char* name) {
+  void* f = dlsym(RTLD_DEFAULT, name);
+  if (f) return f;
+  static void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  return h ? dlsym(h, name) : nullptr;
+}
+
+int mgn_stats_allgather(mgn_env* e, void* comm, int32_t rows_per_rank, double* out_dev) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  if (!comm || !out_dev) return fail(e, MGN_ERR_ARG, "null communicator/output");
+  const size_t rows = rows_per_rank == 0 ? (size_t)e->N : (size_t)rows_per_rank;
+  if (rows_per_rank < 0 || rows < (size_t)e->N)
+    return fail(e, MGN_ERR_LENGTH, "rows_per_rank must be >= n_envs (0: n_envs)");
+  using AllGather = ncclResult_t (*)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
+  using ErrStr = const char* (*)(ncclResult_t);
+  const auto ag = reinterpret_cast<AllGather>(rccl_sym("ncclAllGather"));
+  const auto es = reinterpret_cast<ErrStr>(rccl_sym("ncclGetErrorString"));
+  if (!ag) return fail(e, MGN_ERR_DEVICE, "ncclAllGather not found (no RCCL in the process, no librccl.so.1)");
+  const double* send = e->v.episode_stats;
+  if (rows > (size_t)e->N) {
+    if (rows > e->ag_rows) {
+      if (e->ag_send) (void)hipFree(e->ag_send);
+      e->ag_send = nullptr;
+      e->ag_rows = 0;
+      const int rc = check_hip(e, hipMalloc(&e->ag_send, rows * 4 * sizeof(double)), "allgather staging");
+      if (rc != MGN_OK) return rc;
+      e->ag_rows = rows;
+    }
+    int rc = check_hip(e, hipMemcpyAsync(e->ag_send, e->v.episode_stats, (size_t)e->N * 4 * sizeof(double),
+                                         hipMemcpyDeviceToDevice, e->stream), "allgather staging copy");
+    if (rc == MGN_OK)
+      rc = check_hip(e, hipMemsetAsync(e->ag_send + (size_t)e->N * 4, 0, (rows - e->N) * 4 * sizeof(double),
+                                       e->stream), "allgather staging pad");
+    if (rc != MGN_OK) return rc;
+    send = e->ag_send;
+  }
+  const ncclResult_t r = ag(send, out_dev, rows * 4, ncclFloat64, (ncclComm_t)comm, e->stream);
+  if (r != ncclSuccess)
+    return fail(e, MGN_ERR_DEVICE, std::string("ncclAllGather: ") + (es ? es(r) : std::to_string((int)r)));
+  return MGN_OK;
+}
+
+namespace {
+struct StateHeader {
+  char magic[8];
+  int32_t abi, pad_;
+  uint64_t arena_bytes;
+  mgn_config cfg;
+};
+constexpr char kStateMagic[8] = {'M', 'G', 'N', 'S', 'T', 'A', 'T', 'E'};
+}  // namespace
+
+size_t mgn_state_bytes(const mgn_env* e) { return e ? sizeof(StateHeader) + e->arena_bytes : 0; }
+
+int mgn_save_state(mgn_env* e, void* dst, size_t bytes) {
+  if (!e || !dst) return fail(e, MGN_ERR_ARG, "null handle/destination");
+  if (bytes < mgn_state_bytes(e)) return fail(e, MGN_ERR_LENGTH, "destination smaller than mgn_state_bytes()");
+  StateHeader h{};
+  std::memcpy(h.magic, kStateMagic, 8);
+  h.abi = MGN_ABI_VERSION;
+  h.arena_bytes = e->arena_bytes;
+  h.cfg = e->cfg;
+  std::memcpy(dst, &h, sizeof h);
+  int rc = check_hip(e, hipMemcpyAsync((char*)dst + sizeof h, e->arena, e->arena_bytes, hipMemcpyDeviceToHost,
+                                       e->stream), "mgn_save_state");
+  if (rc == MGN_OK) rc = check_hip(e, hipStreamSynchronize(e->stream), "mgn_save_state (sync)");
+  return rc;
+}
+
+int mgn_load_state(mgn_env* e, const void* src, size_t bytes) {
+  if (!e || !src) return fail(e, MGN_ERR_ARG, "null handle/source");
+  StateHeader h;
+  if (bytes < sizeof h) return fail(e, MGN_ERR_LENGTH, "state blob too small");
+  std::memcpy(&h, src, sizeof h);
+  if (std::memcmp(h.magic, kStateMagic, 8) != 0) return fail(e, MGN_ERR_CONFIG, "not a madigan_amd state blob");
+  if (h.abi != MGN_ABI_VERSION) return fail(e, MGN_ERR_CONFIG, "state blob of another ABI version");
+  const mgn_config& c = h.cfg;
+  const mgn_config& m = e->cfg;
+  if (h.arena_bytes != e->arena_bytes || bytes < sizeof h + h.arena_bytes || c.n_envs != m.n_envs ||
+      c.n_assets != m.n_assets || c.window != m.window || c.reward_mode != m.reward_mode ||
+      c.nstep != m.nstep || c.n_feats != m.n_feats || c.aux != m.aux)
+    return fail(e, MGN_ERR_LENGTH, "state blob of a handle with other dimensions");
+  int rc = check_hip(e, hipMemcpyAsync(e->arena, (const char*)src + sizeof h, e->arena_bytes,
+                                       hipMemcpyHostToDevice, e->stream), "mgn_load_state");
+  if (rc == MGN_OK) rc = check_hip(e, hipStreamSynchronize(e->stream), "mgn_load_state (sync)");
+  if (rc != MGN_OK) return rc;
+  e->cfg = c;
+  auto_layout(e);
+  return MGN_OK;
+}
+
+int mgn_bandwidth_probe(void* dst_dev, const void* src_dev, size_t bytes, int32_t reps, void* stream,
+                        double* gbps_out) {
+  if (!dst_dev || !src_dev || !gbps_out) return fail(nullptr, MGN_ERR_ARG, "null probe buffers");
+  if (bytes < 16 || bytes % 16 || reps < 1) return fail(nullptr, MGN_ERR_LENGTH, "bytes: multiple of 16; reps >= 1");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t n = (int64_t)(bytes / 16);
+  const unsigned grid = 256 * 16;  // 16 workgroups per CU, XCD-round-robin
+  hipEvent_t a, b;
+  if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)
+    return fail(nullptr, MGN_ERR_DEVICE, "event create");
+  hipLaunchKernelGGL(mgn::k_copy_probe, dim3(grid), dim3(mgn::BLOCK), 0, st, (const mgn::probe_v2*)src_dev,
+                     (mgn::probe_v2*)dst_dev, n);  // warm
+  (void)hipEventRecord(a, st);
+  for (int r = 0; r < reps; ++r)
+    hipLaunchKernelGGL(mgn::k_copy_probe, dim3(grid), dim3(mgn::BLOCK), 0, st, (const mgn::probe_v2*)src_dev,
+                       (mgn::probe_v2*)dst_dev, n);
+  (void)hipEventRecord(b, st);
+  int rc = check_hip(nullptr, hipEventSynchronize(b), "mgn_bandwidth_probe");
+  float ms = 0.f;
+  if (rc == MGN_OK) rc = check_hip(nullptr, hipEventElapsedTime(&ms, a, b), "mgn_bandwidth_probe");
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  if (rc != MGN_OK) return rc;
+  *gbps_out = 2.0 * (double)bytes * reps / (ms * 1e-3) / 1e9;
   return MGN_OK;
 }
 

@@ -512,4 +512,22 @@ __global__ void k_gen_actions(int8_t* __restrict__ out, int K, int N, int A, int
   out[gid] = (int8_t)(((uint64_t)x.x * (uint32_t)atoms) >> 32);
 }
 
+// Attainable-bandwidth probe ("measure attainable bandwidth on
+// the box with a device-copy kernel"): a grid-stride 16-B-per-lane copy,
+// 4 loads in flight per lane, non-temporal stores
+typedef double probe_v2 __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(BLOCK) void k_copy_probe(const probe_v2* __restrict__ src,
+                                                      probe_v2* __restrict__ dst, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    const probe_v2 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    __builtin_nontemporal_store(a, dst + i);
+    __builtin_nontemporal_store(b, dst + i + stride);
+    __builtin_nontemporal_store(c, dst + i + 2 * stride);
+    __builtin_nontemporal_store(d, dst + i + 3 * stride);
+  }
+  for (; i < n; i += stride) __builtin_nontemporal_store(src[i], dst + i);
+}
+
 }  // namespace mgn

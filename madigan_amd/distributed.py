@@ -50,6 +50,53 @@ def allgather_episode_stats(stats, group=None):
     return torch.cat([out[r * n_max:r * n_max + sizes[r]] for r in range(world)])
 
 
+def rccl_comm(group=None, device=None) -> int:
+    """The raw RCCL communicator (ncclComm_t) of a torch "nccl" process group,
+    for mgn_stats_allgather; 0 if the group has none (gloo)."""
+    import torch
+    import torch.distributed as dist
+    g = group if group is not None else dist.group.WORLD
+    if dist.get_backend(g) != "nccl":
+        return 0
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    return int(g._get_backend(dev)._comm_ptr())
+
+
+def allgather_env_stats(env, n_total=None, group=None):
+    """All-gather a BatchedEnv's (N_local, 4) episode statistics into
+    (n_total, 4) in global env order.  Over "nccl" the collective is the C
+    ABI's mgn_stats_allgather on the handle's stream (one ncclAllGather of
+    ceil(n_total / world) rows per rank; ragged shards are zero-padded by the
+    library and trimmed here); other backends use torch's all-gather.  With
+    n_total given (the shard() partition) no size exchange is needed."""
+    import ctypes as C
+    import torch
+    import torch.distributed as dist
+    from . import _lib as L
+    stats = env.episode_stats
+    if not (dist.is_available() and dist.is_initialized()):
+        return stats
+    world = dist.get_world_size(group)
+    comm = rccl_comm(group, env.device)
+    if not comm:
+        return allgather_episode_stats(stats.cpu() if dist.get_backend(group) == "gloo" else stats,
+                                       group)
+    if n_total is None:
+        n = torch.tensor([env.N], dtype=torch.int64, device=env.device)
+        sizes = [torch.zeros_like(n) for _ in range(world)]
+        dist.all_gather(sizes, n, group=group)
+        sizes = [int(s.item()) for s in sizes]
+    else:
+        sizes = [shard(n_total, r, world)[1] for r in range(world)]
+    rows = max(sizes)
+    out = torch.empty((world * rows, 4), dtype=torch.float64, device=env.device)
+    L.check(env.lib.mgn_stats_allgather(env.h, C.c_void_p(comm), rows, C.c_void_p(out.data_ptr())),
+            env.h)
+    if all(s == rows for s in sizes):
+        return out
+    return torch.cat([out[r * rows:r * rows + sizes[r]] for r in range(world)])
+
+
 def summarize(stats):
     """Episode summary over all envs from gathered (n_total, 4) statistics:
     {last return, last length, last final equity, done count}."""

@@ -173,6 +173,7 @@ class BatchedEnv:
         self.nstep = v.nstep
         self._build_views()
         self._val = torch.empty((self.N, 10), dtype=torch.float64, device=self.device)
+        self._traj_cache = {}
         self._tape = None
         if spec.replay:
             self._attach_replay(replay_tape, int(replay_stride))
@@ -381,6 +382,20 @@ class BatchedEnv:
             setattr(t, k, None if v is None else v.data_ptr())
         return t
 
+    def _traj_for(self, out: dict, K: int):
+        """The validated mgn_traj of an output dict: validated and built once per
+        (dict, K, buffer addresses), then reused, so a loop over launches with
+        the same buffers pays one address comparison per launch."""
+        key = (id(out), K)
+        ptrs = tuple(None if v is None else v.data_ptr() for v in out.values())
+        hit = self._traj_cache.get(key)
+        if hit is not None and hit[0] is out and hit[1] == ptrs:
+            return hit[2]
+        self._check_traj(out, K)
+        t = self._traj_struct(out)
+        self._traj_cache[key] = (out, ptrs, t, C.byref(t))
+        return t
+
     def rollout(self, actions, out: Optional[dict] = None) -> dict:
         """K fused steps from discrete actions (K,N,A) int8 via action_to_transaction."""
         torch = _torch()
@@ -391,10 +406,62 @@ class BatchedEnv:
             raise ValueError(f"actions must be (K, {self.N}, {self.A}), got {tuple(actions.shape)}")
         K = int(actions.shape[0])
         out = self.alloc_traj(K) if out is None else out
-        self._check_traj(out, K)
-        t = self._traj_struct(out)
+        t = self._traj_for(out, K)
         L.check(self.lib.mgn_rollout(self.h, C.c_void_p(actions.data_ptr()), K, C.byref(t)), self.h)
         return out
+
+    def rollout_launcher(self, out: dict, k_steps: int):
+        """A launcher for repeated K-step rollouts into the same output buffers:
+        ``launch(actions_ptr)`` runs mgn_rollout on (K,N,A) int8 device actions
+        at that address, with the mgn_traj validated once here (the per-launch
+        host work is the ctypes call).  The caller keeps ``out`` alive."""
+        K = int(k_steps)
+        t = self._traj_for(out, K)
+        ref = C.byref(t)
+        fn, h = self.lib.mgn_rollout, self.h
+
+        def launch(actions_ptr: int) -> int:
+            return fn(h, actions_ptr, K, ref)
+        return launch
+
+    # ---- Env::setDataSource / checkpoint --------------------------------------------
+    def set_sources(self, spec: SourceSpec, prices=None):
+        """Env::setDataSource for every env (Env.h:174-179): swap the price
+        source in place and keep the portfolios.  spec: per asset
+        MGN_SRC_EXTERNAL (host prices through set_prices before each tick) or
+        the current kind with new parameters; prices (N,A): the new source's
+        currentPrices (None keeps the device prices)."""
+        torch = _torch()
+        if spec.n_assets != self.A:
+            raise ValueError(f"the new source has {spec.n_assets} assets, the env {self.A}")
+        srcs = (L.AssetSource * self.A)()
+        for i, (k, p) in enumerate(zip(spec.kinds, spec.params)):
+            srcs[i].kind = k
+            for j, v in enumerate(p):
+                srcs[i].p[j] = v
+        ptr = None
+        if prices is not None:
+            stage = torch.empty((self.N, self.A), dtype=torch.float64, device=self.device)
+            ptr = C.c_void_p(self._dev(prices, torch.float64, (self.N, self.A), stage).data_ptr())
+        L.check(self.lib.mgn_set_sources(self.h, srcs, ptr), self.h)
+        self.spec = spec
+
+    def state_dict(self) -> dict:
+        """The handle's whole state (mgn_save_state) as a host uint8 array plus
+        the library ABI: every episode resumes bit-exactly after load_state_dict."""
+        n = int(self.lib.mgn_state_bytes(self.h))
+        blob = np.empty(n, dtype=np.uint8)
+        L.check(self.lib.mgn_save_state(self.h, blob.ctypes.data_as(C.c_void_p), n), self.h)
+        return {"state": blob, "abi": L.ABI_VERSION}
+
+    def load_state_dict(self, sd: dict) -> None:
+        blob = np.ascontiguousarray(sd["state"], dtype=np.uint8)
+        if int(sd.get("abi", L.ABI_VERSION)) != L.ABI_VERSION:
+            raise RuntimeError("state_dict of another ABI version")
+        L.check(self.lib.mgn_load_state(self.h, blob.ctypes.data_as(C.c_void_p), blob.nbytes), self.h)
+        c = L.Config()
+        C.memmove(C.byref(c), blob.ctypes.data + 24, C.sizeof(c))
+        self.cfg = c
 
     def rollout_units(self, units, out: Optional[dict] = None) -> dict:
         """K fused Env::step(units) from units (K,N,A) fp64."""
@@ -404,8 +471,7 @@ class BatchedEnv:
             raise ValueError(f"units must be (K, {self.N}, {self.A}), got {tuple(u.shape)}")
         K = int(u.shape[0])
         out = self.alloc_traj(K) if out is None else out
-        self._check_traj(out, K)
-        t = self._traj_struct(out)
+        t = self._traj_for(out, K)
         L.check(self.lib.mgn_rollout_units(self.h, C.c_void_p(u.data_ptr()), K, C.byref(t)), self.h)
         return out
 
@@ -591,7 +657,14 @@ class PortfolioView:
 
 
 class Env:
-    """Drop-in for madigan.environments.cpp.Env (one env on the GPU)."""
+    """Drop-in for madigan.environments.cpp.Env (one env on the GPU).
+
+    Host reads go through one snapshot per state change: the first step or
+    accessor after a launch runs k_valuation and copies the handle's arena
+    and the valuation row to pinned host memory with one stream synchronise;
+    every accessor until the next mutating call reads that snapshot (the
+    reference agent reads equity, availableMargin, currentPrices, ledger, ...
+    around every step, offpolicy_q.py:140-164, dqn.py:165-176)."""
 
     def __init__(self, dataSourceType: str, initCash: float = 1_000_000.0, config_dict=None, *,
                  device=None, seed: int = 0):
@@ -609,21 +682,59 @@ class Env:
         # Env::requiredMargin_ / maintenanceMargin_ default to 0 (Env.h:131-132)
         self._broker = dict(required_margin=0.0, maintenance_margin=0.0, slippage_rel=0.0,
                             slippage_abs=0.0, transaction_cost_rel=0.0, transaction_cost_abs=0.0)
-        self._make(spec)
-
-    def _make(self, spec):
         self._spec = spec
         self._b = BatchedEnv(spec, 1, device=self._device, seed=self._seed,
                              init_cash=self._init_cash, **self._broker)
+        torch = _torch()
+        self._h_arena = torch.empty(self._b.arena.numel(), dtype=torch.uint8, pin_memory=True)
+        self._h_val = torch.empty((1, 10), dtype=torch.float64, pin_memory=True)
+        self._snap = None
+
+    # ---- host snapshot of the device state ------------------------------------------
+    def _dirty(self):
+        self._snap = None
+
+    def _snapshot(self) -> dict:
+        if self._snap is not None:
+            return self._snap
+        b = self._b
+        L.check(b.lib.mgn_valuation(b.h, C.c_void_p(b._val.data_ptr())), b.h)
+        with _torch().cuda.stream(b.stream):
+            self._h_arena.copy_(b.arena, non_blocking=True)
+            self._h_val.copy_(b._val, non_blocking=True)
+        b.stream.synchronize()
+        blob = self._h_arena.numpy()
+        base = b.arena.data_ptr()
+
+        def arr(ptr, dtype, shape):
+            off = ptr - base
+            n = int(np.prod(shape)) * np.dtype(dtype).itemsize
+            return blob[off:off + n].view(dtype).reshape(shape)
+        v, A, F = b._v, b.A, b.F
+        o = v.out
+        self._snap = dict(
+            val=dict(zip(VALUATION_FIELDS, self._h_val.numpy()[0])),
+            prices=arr(v.prices, np.float64, (A,)), ledger=arr(v.ledger, np.float64, (A,)),
+            mean_entry=arr(v.mean_entry, np.float64, (A,)),
+            timestamp=int(arr(v.timestamp, np.uint64, (1,))[0]),
+            reward=float(arr(o.reward, np.float64, (1,))[0]), done=bool(arr(o.done, np.uint8, (1,))[0]),
+            obs_price=arr(o.obs_price, np.float64, (F,)), obs_port=arr(o.obs_port, np.float64, (A + 1,)),
+            obs_ts=int(arr(o.timestamp, np.uint64, (1,))[0]),
+            tprice=arr(o.tprice, np.float64, (A,)), tunits=arr(o.tunits, np.float64, (A,)),
+            tcost=arr(o.tcost, np.float64, (A,)), risk=arr(o.risk, np.uint8, (A,)),
+            margin_call=bool(arr(o.margin_call, np.uint8, (1,))[0]))
+        return self._snap
 
     # ---- setters (Env.h:94-111) ------------------------------------------------
     def setRequiredMargin(self, requiredMargin):
         self._broker["required_margin"] = float(requiredMargin)
         self._b.set_broker(required_margin=requiredMargin)
+        self._dirty()
 
     def setMaintenanceMargin(self, maintenanceMargin):
         self._broker["maintenance_margin"] = float(maintenanceMargin)
         self._b.set_broker(maintenance_margin=maintenanceMargin)
+        self._dirty()
 
     def setSlippage(self, relativeSlippage=0.0, absSlippage=0.0):
         self._broker.update(slippage_rel=float(relativeSlippage), slippage_abs=float(absSlippage))
@@ -635,17 +746,22 @@ class Env:
         self._b.set_broker(transaction_cost_rel=relativeCost, transaction_cost_abs=absCost)
 
     def setDataSource(self, dataSource):
-        """Env::setDataSource (Env.h:174-179): a host DataSourceTick feeds every asset."""
+        """Env::setDataSource (Env.h:174-179): the host DataSourceTick becomes the
+        source of every asset; the Broker / Portfolio (ledger, cash, mean entry,
+        borrowed margin) are kept and value the portfolio at the new source's
+        currentPrices() from now on.  Its getData() runs before every step's
+        tick (PyDataSource trampoline, PyDataSource.h:9-15)."""
+        if self._spec.replay:
+            raise RuntimeError("setDataSource: a replay Env cannot switch its data source")
         prices = np.asarray(dataSource.currentPrices(), dtype=np.float64).reshape(-1)
-        spec = SourceSpec(kinds=[L.SRC_EXTERNAL] * len(prices), params=[[]] * len(prices),
-                          assets=[a.code if hasattr(a, "code") else str(a)
-                                  for a in getattr(dataSource, "assets", [])] or
-                          [f"asset_{i}" for i in range(len(prices))])
+        if prices.shape[0] != self.nAssets:
+            raise ValueError(f"the data source has {prices.shape[0]} assets, the Env {self.nAssets}")
+        spec = SourceSpec(kinds=[L.SRC_EXTERNAL] * self.nAssets, params=[[]] * self.nAssets,
+                          assets=list(self._spec.assets))
+        self._b.set_sources(spec, prices.reshape(1, -1))
         self._source = dataSource
-        torch = _torch()
-        self._make(spec)
-        # the constructor's first tick read zeros; load the source's prices as current
-        self._b.prices.copy_(torch.from_numpy(prices).view(1, -1))
+        self._spec = spec
+        self._dirty()
 
     # ---- stepping -----------------------------------------------------------------
     def _feed_external(self):
@@ -654,21 +770,24 @@ class Env:
             self._b.set_prices(p)
 
     def _state(self, o):
-        return State(o["obs_price"][0].copy(), o["obs_port"][0].copy(), int(o["timestamp"][0]))
+        return State(o["obs_price"].copy(), o["obs_port"].copy(), o["obs_ts"])
 
     def reset(self):
         if self._source is not None:
             self._source.reset()
             self._feed_external()
         self._b.reset()
-        return State(self.currentData.copy(), self.ledgerNormedFull, self.timestamp)
+        self._dirty()
+        s = self._snapshot()
+        return State(self.currentData.copy(), self.ledgerNormedFull, s["timestamp"])
 
     def step(self, *args):
         if len(args) == 0:
             self._feed_external()
             self._b.step()
-            o = self._b.host_outputs()
-            return self._state(o), float(o["reward"][0]), bool(o["done"][0]), EnvInfo(
+            self._dirty()
+            o = self._snapshot()
+            return self._state(o), o["reward"], o["done"], EnvInfo(
                 BrokerResponse(0.0, 0.0, 0.0, RiskInfo.green, False), self.dataEnd())
         if len(args) == 2:
             idx, units = args
@@ -682,32 +801,32 @@ class Env:
                 raise IndexError(f"asset index {idx} out of range")
             self._feed_external()
             self._b.step(units=np.array([float(units)]), asset_idx=np.array([idx], np.int32))
-            o = self._b.host_outputs()
-            resp = BrokerResponse(float(o["tprice"][0, idx]), float(o["tunits"][0, idx]),
-                                  float(o["tcost"][0, idx]), RiskInfo(int(o["risk"][0, idx])),
-                                  bool(o["margin_call"][0]))
-            return self._state(o), float(o["reward"][0]), bool(o["done"][0]), EnvInfo(resp, self.dataEnd())
+            self._dirty()
+            o = self._snapshot()
+            resp = BrokerResponse(float(o["tprice"][idx]), float(o["tunits"][idx]),
+                                  float(o["tcost"][idx]), RiskInfo(int(o["risk"][idx])),
+                                  o["margin_call"])
+            return self._state(o), o["reward"], o["done"], EnvInfo(resp, self.dataEnd())
         if len(args) == 1:
             units = np.asarray(args[0], dtype=np.float64).reshape(-1)
             if units.shape[0] != self.nAssets:
                 raise ValueError(f"units must have {self.nAssets} entries, got {units.shape[0]}")
             self._feed_external()
             self._b.step(units=units.reshape(1, -1))
-            o = self._b.host_outputs()
-            resp = BrokerResponse(o["tprice"][0].copy(), o["tunits"][0].copy(), o["tcost"][0].copy(),
-                                  [RiskInfo(int(r)) for r in o["risk"][0]], bool(o["margin_call"][0]))
-            return self._state(o), float(o["reward"][0]), bool(o["done"][0]), EnvInfo(resp, self.dataEnd())
+            self._dirty()
+            o = self._snapshot()
+            resp = BrokerResponse(o["tprice"].copy(), o["tunits"].copy(), o["tcost"].copy(),
+                                  [RiskInfo(int(r)) for r in o["risk"]], o["margin_call"])
+            return self._state(o), o["reward"], o["done"], EnvInfo(resp, self.dataEnd())
         raise TypeError("step() takes (), (units), (assetIdx, units) or (assetCode, units)")
 
     # ---- accessors (env.cpp:872-969) --------------------------------------------------
     def _vals(self):
-        v = self._b.valuation()
-        host = self._b._val.cpu().numpy()[0]
-        return dict(zip(v.keys(), host))
+        return self._snapshot()["val"]
 
     @property
     def currentPrices(self):
-        return self._b.prices[0].cpu().numpy()
+        return self._snapshot()["prices"].copy()
 
     def _replay_row(self):
         b = self._b
@@ -723,15 +842,15 @@ class Env:
 
     @property
     def ledger(self):
-        return self._b.ledger[0].cpu().numpy()
+        return self._snapshot()["ledger"].copy()
 
     @property
     def meanEntryPrices(self):
-        return self._b.mean_entry[0].cpu().numpy()
+        return self._snapshot()["mean_entry"].copy()
 
     @property
     def timestamp(self):
-        return int(self._b.timestamp[0].item())
+        return self._snapshot()["timestamp"]
 
     currentTime = timestamp
 
@@ -741,7 +860,7 @@ class Env:
 
     @property
     def cash(self):
-        return float(self._b.cash[0].item())
+        return float(self._vals()["cash"])
 
     @property
     def pnl(self):

@@ -1165,6 +1165,16 @@ void orc_set_prices(orc_batch *b, const double *prices) {
   memcpy(b->ext, prices, sizeof(double) * (size_t)b->N * b->A);
 }
 
+/* Env::setDataSource (Env.h:174-179): the new source replaces the old one;
+ * the Broker / Portfolio stay, and the Broker's price map now points at the
+ * new source's currentPrices() (Broker.cpp:68-76), loaded here as P. */
+void orc_set_sources(orc_batch *b, const orc_asset_src *srcs, const double *prices) {
+  memcpy(b->src, srcs, sizeof(orc_asset_src) * (size_t)b->A);
+  if (prices)
+    for (int e = 0; e < b->N; ++e)
+      memcpy(b->envs[e].P, prices + (size_t)e * b->A, sizeof(double) * (size_t)b->A);
+}
+
 /* agent per-asset reward: offpolicy_q.py:152-164 */
 static void agent_reward(const orc_env *s, int A, const double *prevVal, double prevEq,
                          const double *tp, const double *tu, const double *tc, double *r) {

@@ -162,6 +162,7 @@ void orc_rollout_mt(orc_batch *b, const int8_t *actions, int k_steps, const orc_
 void orc_action_to_units(orc_batch *b, const int8_t *actions, double *units);
 /* external prices for the next getData (N,A), ORC_SRC_EXTERNAL assets */
 void orc_set_prices(orc_batch *b, const double *prices);
+void orc_set_sources(orc_batch *b, const orc_asset_src *srcs, const double *prices);
 /* HDFSourceSingle for every env of an ORC_SRC_REPLAY batch, over the file's
  * arrays held in memory: price (T,A), feats (T,F), ts (T), time bounds
  * [first, second) as findBounds left them, cacheSize.  Env g's source is first

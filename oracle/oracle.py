@@ -88,6 +88,7 @@ def lib(fast: bool = False):
         L.orc_rollout_mt.argtypes = [P, P, C.c_int, C.POINTER(Out), C.c_int]
         L.orc_action_to_units.argtypes = [P, P, P]
         L.orc_set_prices.argtypes = [P, P]
+        L.orc_set_sources.argtypes = [P, P, P]
         L.orc_set_replay.argtypes = [P, P, P, P] + [C.c_int64] * 5
         L.orc_set_replay.restype = C.c_int64
         L.orc_get_field.argtypes = [P, C.c_int, P]
@@ -249,6 +250,13 @@ class OracleBatch:
     def set_prices(self, prices):
         p = np.ascontiguousarray(prices, dtype=np.float64).reshape(self.N, self.A)
         self.L.orc_set_prices(self.h, _ptr(p))
+
+    def set_sources(self, sources, prices=None):
+        """Env::setDataSource: new (kind, params) per asset, portfolios kept;
+        prices (N,A) become the current prices (None keeps them)."""
+        self._srcs = make_srcs(sources)
+        p = None if prices is None else np.ascontiguousarray(prices, dtype=np.float64).reshape(self.N, self.A)
+        self.L.orc_set_sources(self.h, self._srcs, _ptr(p))
 
     # -- state -------------------------------------------------------------
     def field(self, f):

@@ -309,6 +309,8 @@ def main():
                          "when profiling, so the kernel's rocprof average is the headline's)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--workload", default="C3", choices=["C1", "C2", "C3", "C4", "C5"])
+    ap.add_argument("--dump-stats", default=None,
+                    help="rank 0 saves the gathered (n_total, 4) episode statistics (.npy)")
     ap.add_argument("--no-probe", dest="probe", action="store_false",
                     help="skip the attainable-bandwidth copy probe")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -437,6 +439,8 @@ def main():
                              "achieved_GBs_survey_bytes": N * bpes / us / 1e3,
                              "fused_bytes_per_env_step": bytes_per_env_step(A, K, env.D)}
 
+    if rank == 0 and args.dump_stats:
+        np.save(args.dump_stats, gathered.cpu().numpy())
     if rank == 0:
         K = int(round(steps_per_launch))
         workload = f"C3_trendou_{N}x{A}_fuse{K}"

@@ -40,10 +40,19 @@ constexpr int DUO_BLOCK = 512;
 #ifdef MGN_STAMPS
 // diagnostic build only: per role, cycles of [work 1, wait A, work 2, wait B]
 // summed over one wave per role and block, then the iteration count
-__device__ unsigned long long g_duo_stamps[16];
+__device__ unsigned long long g_duo_stamps[24];
+// per-block sub-phase accumulators, one writer (the block's first ledger lane)
+__shared__ unsigned long long s_duo_sub[8];
+// wall clock (s_memrealtime, 100 MHz) per block (first 2048 blocks), plain
+// stores by one lane: [0] generator entry, [1] ledger entry, [2] ledger loop
+// start, [3] ledger loop end, [4] generator loop end, [5] generator exit,
+// [6] / [7] ledger after iteration 0 / 2
+__device__ unsigned long long g_duo_wall[2048 * 8];
 #define MGN_T(v) v = __builtin_amdgcn_s_memtime()
+#define MGN_WALL(i) if ((threadIdx.x & 255) == 0 && blockIdx.x < 2048) g_duo_wall[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime()
 #else
 #define MGN_T(v)
+#define MGN_WALL(i)
 #endif
 constexpr int DUO_HALF = DUO_BLOCK / 2;
 
@@ -53,9 +62,13 @@ enum { REC_STEP = 1, REC_TICK = 2, REC_DONE = 4, REC_MCALL = 8 };
 template <int S>
 struct DuoRec {
   static constexpr int EPB = DUO_HALF / S;
-  double rL[DUO_HALF], rPrev[DUO_HALF], rTp[DUO_HALF], rTu[DUO_HALF], rTc[DUO_HALF];
+  // per lane: ledger, responses, agent reward, per-asset shaped reward
+  double rL[DUO_HALF], rTp[DUO_HALF], rTu[DUO_HALF], rTc[DUO_HALF];
+  double rAr[DUO_HALF], rShv[DUO_HALF];
   int32_t rRk[DUO_HALF];
-  double rPrevEq[EPB], rCurEq[EPB], rCash[EPB], rLp[EPB], rB[EPB], rRew[EPB];
+  // per env: equity (post-tick, also of a refill tick), cash, borrowed
+  // margin, log reward, the shaper's input and output (D == 1)
+  double rCurEq[EPB], rCash[EPB], rB[EPB], rRew[EPB], rRin[EPB], rShaped[EPB];
   int32_t rK[EPB], rFlags[EPB];
 };
 
@@ -73,7 +86,12 @@ struct DuoShared {
 // Output pointers live in VGPR pairs (in_vgpr: the compiler cannot move them
 // back into SGPRs) and their null tests in one uniform bit mask: with every
 // pointer of KParams and mgn_traj in SGPRs the kernel spilled SGPRs to VGPR
-// lanes and reloaded them with v_readlane inside the step loop.
+// lanes and reloaded them with v_readlane inside the step loop.  The VGPR
+// pointers are typed address_space(1) (global): a pointer whose provenance
+// the compiler cannot see is otherwise generic, its accesses become FLAT
+// instructions, and FLAT counts on lgkmcnt as well as vmcnt -- every LDS
+// wait and every barrier of the step loop then waited for the previous
+// stores (and the next action's load) to complete in memory.
 enum : uint32_t { O_REW = 1u, O_AREW = 2u, O_SHP = 4u, O_DONE = 8u, O_OPR = 16u, O_OPT = 32u,
                   O_TS = 64u, O_TP = 128u, O_TU = 256u, O_TC = 512u, O_RISK = 1024u,
                   O_MC = 2048u, O_NSH = 4096u, O_DEND = 8192u };
@@ -84,12 +102,25 @@ __device__ __forceinline__ uint32_t traj_mask(const mgn_traj& o) {
          (o.tcost ? O_TC : 0u) | (o.risk ? O_RISK : 0u) | (o.margin_call ? O_MC : 0u) |
          (o.n_shaped ? O_NSH : 0u) | (o.data_end ? O_DEND : 0u);
 }
+#define MGN_G __attribute__((address_space(1)))
 template <typename T>
-__device__ __forceinline__ T* vptr(T* q) {
-  return reinterpret_cast<T*>(in_vgpr(reinterpret_cast<uintptr_t>(q)));
+__device__ __forceinline__ MGN_G T* vptr(T* q) {
+  return (MGN_G T*)in_vgpr(reinterpret_cast<uintptr_t>(q));
 }
-__device__ __forceinline__ mgn_traj traj_vgpr(const mgn_traj& o) {
-  mgn_traj v;
+template <typename T>
+__device__ __forceinline__ const MGN_G T* vptr(const T* q) {
+  return (const MGN_G T*)in_vgpr(reinterpret_cast<uintptr_t>(q));
+}
+struct GTraj {
+  MGN_G double *reward, *agent_reward, *shaped;
+  MGN_G uint8_t* done;
+  MGN_G double *obs_price, *obs_port;
+  MGN_G uint64_t* timestamp;
+  MGN_G double *tprice, *tunits, *tcost;
+  MGN_G uint8_t *risk, *margin_call, *n_shaped, *data_end;
+};
+__device__ __forceinline__ GTraj traj_vgpr(const mgn_traj& o) {
+  GTraj v;
   v.reward = vptr(o.reward);
   v.agent_reward = vptr(o.agent_reward);
   v.shaped = vptr(o.shaped);
@@ -106,132 +137,176 @@ __device__ __forceinline__ mgn_traj traj_vgpr(const mgn_traj& o) {
   v.data_end = vptr(o.data_end);
   return v;
 }
+// the generator side's per-env state outputs, global VGPR pointers
+struct GState {
+  MGN_G double *epstats, *ring, *hist;
+  MGN_G uint64_t *ring_ts, *hist_ts;
+};
 
-// The generator lane's half of an Env step: everything downstream of the
-// record (Env.h:211-229, Portfolio.cpp:150-155, offpolicy_q.py:152-164,
-// nstep_buffer.py n = 1, preprocessor.py:172-175)
+// The step finish is split between the roles.  The ledger lanes evaluate it
+// (ledger_finish: Env.h:211-229 reward, Portfolio.cpp:150-155
+// ledgerNormedFull, offpolicy_q.py:152-164 agent reward, nstep_buffer.py
+// n = 1 shaping) right after the step's post-tick sums and publish it in the
+// step record; the generator lanes store the record's outputs one iteration
+// later (duo_store) and keep the episode statistics and the window ring
+// (preprocessor.py:172-175).  Each value is the same expression
+// of the same operands as in k_step, so every output stays bit-identical.
 struct GenOut {
-  double shA, shB, ep_ret, ep_len, cos_qn;
-  DdrPre ddr;  // DDR's reward-independent operands, from the current A, B
+  double ep_ret, ep_len, n_done;
   int32_t head, len;
   int32_t hcnt, klast;  // launch history: next row, the step its rows belong to
 };
+// the ledger side's shaper state (nstep_buffer.py:38-60) and PPC constants
+struct LedOut {
+  double shA, shB, cos_qn;
+};
 
-// P, ts: the State's price and timestamp (the tick the record belongs to)
+// the finish of step k on the ledger side (its post-tick quantities in
+// registers); writes the record's output fields
 template <int S>
-__device__ __forceinline__ void duo_finish(const DuoRec<S>& sh, const Lane<1>& s, const KParams& p,
-                                           const mgn_traj& out, uint32_t om, int in_kind, int env,
-                                           int el, int l, int ls, double P, uint64_t ts,
-                                           bool need_ar, GenOut& g) {
+__device__ __forceinline__ void ledger_finish(DuoRec<S>& rc, const Lane<1>& s, const KParams& p,
+                                              const double* s_tgt, int el, int l, int ls,
+                                              double cash, double qb, double prevEq, double curEq,
+                                              double reward, double prevVal, double tp, double tu,
+                                              double tc, bool need_ar, LedOut& g) {
   constexpr int M = 1;
+  const bool valid = s.valid[0];
+  const int D = p.D;
+  const double Lc = s.L[0], P = s.P[0];
+  double ar[M];
+  ar[0] = 0.;
+  if (valid && need_ar) {
+    double v = (((Lc * P) - prevVal) - (tu * tp + tc)) / prevEq;
+    v += 1;
+    v = (v < .35) ? .35 : v;
+    ar[0] = log_ratio(v);
+  }
+  double cos_term = 0.;
+  if (p.shaper == MGN_SHAPER_PPC) {
+    const double port0 = (cash - qb) / curEq;
+    const double portA = (Lc * P) / curEq;
+    double pp[M], pq[M];
+    const double qv = valid ? s_tgt[1 + s.asset[0]] : 0.;
+    const double pv = valid ? portA : 0.;
+    pp[0] = pv * pv;
+    pq[0] = pv * qv;
+    const double np_ = sqrt(port0 * port0 + canon<M, S>(pp));
+    const double dot = port0 * s_tgt[0] + canon<M, S>(pq);
+    cos_term = p.cos_temp * (dot / (np_ * g.cos_qn));
+  }
+  double shaped_s = 0., rin_s = 0., shaped_v = 0.;
+  if (D == 1) {
+    rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
+    if (p.shaper == MGN_SHAPER_DDR) {  // shape() for DDR (nstep_buffer.py:128-162)
+      const double r = rin_s;
+      shaped_s = clip1((0.0 + 1.0 * ddr_one_pre(r, g.shA, g.shB, ddr_pre(g.shA, g.shB))) / 1);
+      double m = r < 0. ? r : 0.;
+      if (r != r) m = r;
+      g.shA += p.eta * (r - g.shA);
+      g.shB += p.eta * (m * m - g.shB);
+    } else {
+      shaped_s = shape(p.shaper, rin_s, g.shA, g.shB, p.eta, cos_term, p.sexp);
+    }
+  } else {
+    shaped_v = valid ? shape(p.shaper, ar[0], g.shA, g.shB, p.eta, cos_term, p.sexp) : 0.;
+  }
+  rc.rAr[l] = ar[0];
+  rc.rShv[l] = shaped_v;
+  if (ls == 0) {
+    rc.rRin[el] = rin_s;
+    rc.rShaped[el] = shaped_s;
+  }
+}
+
+// the generator side's half: the record's stores, episode statistics and
+// window row.  P, ts: the State's price and timestamp (the tick the record
+// belongs to)
+template <int S>
+__device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s, const KParams& p,
+                                          const GTraj& out, const GState& gs, uint32_t om, int env,
+                                          int el, int l, int ls, double P, uint64_t ts, GenOut& g) {
   const int flags = sh.rFlags[el];
   if (flags == 0) return;
   const int A = p.A;
   const int D = p.D;
-  const double cash = sh.rCash[el];
-  const double Lc = sh.rL[l];
   const bool valid = s.valid[0];
+  // ledgerNormedFull (Portfolio.cpp:150-155) of the record's State: these
+  // two divisions are off the ledger's step chain here
+  const double eq = sh.rCurEq[el];
+  const double portA = (sh.rL[l] * P) / eq;
+  const double port0 = (sh.rCash[el] - sh.rB[el]) / eq;
   if (flags & REC_STEP) {
     const int k = sh.rK[el];
     const size_t oN = (size_t)k * p.N, oNA = (size_t)k * p.N * A;
-    const double prevEq = sh.rPrevEq[el];
     const double curEq = sh.rCurEq[el];
-    const double qb = sh.rB[el];
-    const double tp = sh.rTp[l], tu = sh.rTu[l], tc = sh.rTc[l];
     const bool done = (flags & REC_DONE) != 0;
-    const double reward = sh.rRew[el];  // the ledger side's log(max(curEq / prevEq, clamp))
-    double ar[M];
-    ar[0] = 0.;
-    if (valid && need_ar) {
-      double v = (((Lc * P) - sh.rPrev[l]) - (tu * tp + tc)) / prevEq;
-      v += 1;
-      v = (v < .35) ? .35 : v;
-      ar[0] = log_ratio(v);
-    }
-    double cos_term = 0.;
-    if (p.shaper == MGN_SHAPER_PPC) {
-      const double port0 = (cash - qb) / curEq;
-      const double portA = (Lc * P) / curEq;
-      double pp[M], pq[M];
-      const double qv = valid ? p.target[1 + s.asset[0]] : 0.;
-      const double pv = valid ? portA : 0.;
-      pp[0] = pv * pv;
-      pq[0] = pv * qv;
-      const double np_ = sqrt(port0 * port0 + canon<M, S>(pp));
-      const double dot = port0 * p.target[0] + canon<M, S>(pq);
-      cos_term = p.cos_temp * (dot / (np_ * g.cos_qn));
-    }
-    double shaped_s = 0., rin_s = 0., shaped_v = 0.;
-    if (D == 1) {
-      rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
-      if (p.shaper == MGN_SHAPER_DDR) {  // shape() for DDR (nstep_buffer.py:128-162) on g.ddr
-        const double r = rin_s;
-        shaped_s = clip1((0.0 + 1.0 * ddr_one_pre(r, g.shA, g.shB, g.ddr)) / 1);
-        double m = r < 0. ? r : 0.;
-        if (r != r) m = r;
-        g.shA += p.eta * (r - g.shA);
-        g.shB += p.eta * (m * m - g.shB);
-      } else {
-        shaped_s = shape(p.shaper, rin_s, g.shA, g.shB, p.eta, cos_term, p.sexp);
-      }
-    } else {
-      shaped_v = valid ? shape(p.shaper, ar[0], g.shA, g.shB, p.eta, cos_term, p.sexp) : 0.;
-    }
-    if (valid && D != 1) {
+    const double reward = sh.rRew[el];
+    // BrokerResponse, State.portfolio = ledgerNormedFull, State.price, done, marginCall
+    if (valid) {
       const size_t i = oNA + (size_t)env * A + s.asset[0];
-      if (om & O_AREW) out.agent_reward[i] = ar[0];
-      if (om & O_SHP) out.shaped[i] = shaped_v;
+      if (om & O_TP) out.tprice[i] = sh.rTp[l];
+      if (om & O_TU) out.tunits[i] = sh.rTu[l];
+      if (om & O_TC) out.tcost[i] = sh.rTc[l];
+      if (om & O_RISK) out.risk[i] = (uint8_t)sh.rRk[l];
+      if (om & O_OPT) out.obs_port[(size_t)k * p.N * (A + 1) + (size_t)env * (A + 1) + 1 + s.asset[0]] = portA;
+      if (om & O_OPR) out.obs_price[(oN + env) * (size_t)p.F + s.asset[0]] = P;
+      if (D != 1) {
+        if (om & O_AREW) out.agent_reward[i] = sh.rAr[l];
+        if (om & O_SHP) out.shaped[i] = sh.rShv[l];
+      }
     }
     if (ls == 0) {
+      if (om & O_OPT) out.obs_port[(size_t)k * p.N * (A + 1) + (size_t)env * (A + 1)] = port0;
+      if (om & O_DONE) out.done[oN + env] = done ? 1 : 0;
+      if (om & O_MC) out.margin_call[oN + env] = (flags & REC_MCALL) ? 1 : 0;
       if (om & O_DEND) out.data_end[oN + env] = 0;
       if (om & O_REW) out.reward[oN + env] = reward;
       if (om & O_TS) out.timestamp[oN + env] = ts;
       if (om & O_NSH) out.n_shaped[oN + env] = 1;
       if (D == 1) {
-        if (om & O_AREW) out.agent_reward[oN + env] = rin_s;
-        if (om & O_SHP) out.shaped[oN + env] = shaped_s;
+        if (om & O_AREW) out.agent_reward[oN + env] = sh.rRin[el];
+        if (om & O_SHP) out.shaped[oN + env] = sh.rShaped[el];
       }
     }
     g.ep_ret += reward;
     g.ep_len += 1;
     if (done) {
       if (ls == 0) {
-        double* st = p.epstats + (size_t)env * 4;
+        MGN_G double* st = gs.epstats + (size_t)env * 4;
         st[0] = g.ep_ret;
         st[1] = g.ep_len;
         st[2] = curEq;
-        st[3] = st[3] + 1;
+        g.n_done = g.n_done + 1;
+        st[3] = g.n_done;
       }
       g.ep_ret = 0;
       g.ep_len = 0;
     }
   }
   if (p.W > 0) {
-    // StackerDiscrete.stream_state of the State (preprocessor.py:172-175),
-    // the values ring_push computes from the same sums
-    const double eq = (cash + sh.rLp[el]) - sh.rB[el];
+    // StackerDiscrete.stream_state of the State (preprocessor.py:172-175):
+    // (L * P) / equity and (cash - borrowed) / equity, the values ring_push
+    // computes from the same sums
     g.head = (g.head + 1) % p.W;
     if (g.len < p.W) g.len += 1;
     const int R = p.F + p.A + 1;
-    double* row = p.ring + ((size_t)env * p.W + g.head) * R;
-    double* hrow = p.hist ? p.hist + ((size_t)env * p.hrows + g.hcnt) * R : nullptr;
+    MGN_G double* row = gs.ring + ((size_t)env * p.W + g.head) * R;
+    MGN_G double* hrow = p.hist ? gs.hist + ((size_t)env * p.hrows + g.hcnt) * R : nullptr;
     if (valid) {
       const double pv = p.ring_log ? log_norm(P) : P;
-      const double lv = (Lc * P) / eq;
       row[s.asset[0]] = pv;
-      row[p.F + 1 + s.asset[0]] = lv;
+      row[p.F + 1 + s.asset[0]] = portA;
       if (hrow) {
         hrow[s.asset[0]] = pv;
-        hrow[p.F + 1 + s.asset[0]] = lv;
+        hrow[p.F + 1 + s.asset[0]] = portA;
       }
     }
     if (ls == 0) {
-      const double cv = (cash - sh.rB[el]) / eq;
-      row[p.F] = cv;
-      p.ring_ts[(size_t)env * p.W + g.head] = ts;
+      row[p.F] = port0;
+      gs.ring_ts[(size_t)env * p.W + g.head] = ts;
       if (hrow) {
-        hrow[p.F] = cv;
-        p.hist_ts[(size_t)env * p.hrows + g.hcnt] = ts;
+        hrow[p.F] = port0;
+        gs.hist_ts[(size_t)env * p.hrows + g.hcnt] = ts;
       }
     }
     if (hrow) {
@@ -273,7 +348,13 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
                                             double (&tu)[1], double (&tc)[1], int (&rk)[1], int ls,
                                             Sums& after, int& any_mc) {
   double cu2[1], me2[1], bm3[1], tpr[1], tco[1];
+#ifdef MGN_STAMPS
+  const unsigned long long t_a = __builtin_amdgcn_s_memtime();
+#endif
   order_prep<1, S>(s, p, er, uc, ls, cu2, me2, bm3, tpr, tco);
+#ifdef MGN_STAMPS
+  const unsigned long long t_b = __builtin_amdgcn_s_memtime();
+#endif
   const OrderRec& own = er.r[ls];
   const int act = uc[0] != 0. ? 1 : 0;
   const uint32_t act_bits = (uint32_t)seg_or<S>(act << ls);
@@ -325,6 +406,9 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
     go_bits = (go_bits & below) | (go_now & (1u << i0)) | (act_bits & ~(below | (1u << i0)));
   }
   cash = cend;
+#ifdef MGN_STAMPS
+  const unsigned long long t_c = __builtin_amdgcn_s_memtime();
+#endif
   any_mc = seg_or<S>(act & mc) != 0;
   rk[0] = act ? (mc ? MGN_MARGIN_CALL : (insuff ? MGN_INSUFF_MARGIN : MGN_GREEN)) : rk[0];
   const bool go_own[1] = {go != 0};
@@ -345,15 +429,29 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   apply_orders<1>(s, go_own, cu2, me2, bm3, tpr, tco, uc, tp, tu, tc);
+#ifdef MGN_STAMPS
+  const unsigned long long t_d = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == DUO_HALF) {
+    s_duo_sub[0] += t_b - t_a;
+    s_duo_sub[1] += t_c - t_b;
+    s_duo_sub[2] += t_d - t_c;
+  }
+#endif
 }
 
 // ABL: the diagnostic ablation build (mgn_set_ablation != 0); the product
-// instantiation carries no ablation branches
-template <int S, bool RQ1, bool ABL>
-__global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out, int in_kind,
+// instantiation carries no ablation branches.  DISC: discrete actions
+// (mgn_rollout) compiled in alone; otherwise in_kind selects Env::step() /
+// step(units) / step(assetIdx, units) at run time.  (With every input kind in
+// one body the paths merge before the Broker, and the wait the units load
+// needs there also stalled the discrete path on its action prefetch.)
+template <int S, bool RQ1, bool ABL, bool DISC>
+__global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out, int in_kind_rt,
                                                         const double* __restrict__ units_in,
                                                         const int32_t* __restrict__ aidx_in,
                                                         const int8_t* __restrict__ act_in, int K) {
+  const int in_kind = DISC ? IN_DISCRETE : in_kind_rt;
+  MGN_WALL(threadIdx.x < DUO_HALF ? 0 : 1);
   constexpr int M = 1;
   constexpr int EPB = DUO_HALF / S;  // envs per block
   constexpr int APADK = S;
@@ -390,27 +488,21 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
     sh.more[1] = 0;
     sh.more[2] = 0;
   }
+#ifdef MGN_STAMPS
+  if (threadIdx.x < 8) s_duo_sub[threadIdx.x] = 0;
+#endif
   __syncthreads();
 
   if (gen_role) {
     // ---------------- generator waves
-    p.eta = in_vgpr(p.eta);
-    p.cos_temp = in_vgpr(p.cos_temp);
     Lane<M> s;
     load_lane<M>(s, p, envc, ls);
     if (!live) s.valid[0] = false;
     uint64_t ts = p.ts[envc];
-    const int D = p.D;
     GenOut g;
-    if (D == 1) {
-      g.shA = p.sA[envc];
-      g.shB = p.sB[envc];
-    } else {
-      g.shA = s.valid[0] ? p.sA[(size_t)envc * A + s.asset[0]] : 0.;
-      g.shB = s.valid[0] ? p.sB[(size_t)envc * A + s.asset[0]] : 0.;
-    }
     g.ep_ret = p.ep[(size_t)envc * 2];
     g.ep_len = p.ep[(size_t)envc * 2 + 1];
+    g.n_done = p.epstats[(size_t)envc * 4 + 3];
     g.head = 0;
     g.len = 0;
     g.hcnt = p.W;
@@ -419,33 +511,31 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       g.head = p.rhead[envc];
       g.len = p.rlen[envc];
     }
-    g.cos_qn = 0.;
-    if (p.shaper == MGN_SHAPER_PPC) {
-      double qq[M];
-      const double q = s.valid[0] ? p.target[1 + s.asset[0]] : 0.;
-      qq[0] = q * q;
-      g.cos_qn = sqrt(p.target[0] * p.target[0] + canon<M, S>(qq));
-    }
-    const bool need_ar = (p.reward_mode != MGN_REWARD_ENV_LOG) || (out.agent_reward != nullptr);
     const uint32_t om = traj_mask(out);
-    const mgn_traj ov = traj_vgpr(out);
+    const GTraj ov = traj_vgpr(out);
+    GState gs;
+    gs.epstats = vptr(p.epstats);
+    gs.ring = vptr(p.ring);
+    gs.ring_ts = vptr(p.ring_ts);
+    gs.hist = vptr(p.hist);
+    gs.hist_ts = vptr(p.hist_ts);
     // the Philox key schedule (seed + r * W, r < 10) is loop-invariant: from a
     // VGPR seed it stays in VGPRs instead of 20 spilled SGPRs
     p.seed = in_vgpr(p.seed);
     p.env_offset = in_vgpr(p.env_offset);
-    p.epstats = vptr(p.epstats);
-    p.ring = vptr(p.ring);
-    p.ring_ts = vptr(p.ring_ts);
+    // drain the prologue's loads here: otherwise the wait-count pass cannot
+    // tell them from the loop's stores and waits for every store (vmcnt(0))
+    // where a prologue value is first used inside the loop
+    drain_vmem();
+    // the ledger side is on the critical path of both phases: its VALU issue
+    // goes first on the shared SIMD (priority, then age)
+    __builtin_amdgcn_s_setprio(0);
     int j = 0;
 #ifdef MGN_STAMPS
     unsigned long long T0 = 0, T1 = 0, T2 = 0, T3 = 0, T4 = 0, acc[4] = {0, 0, 0, 0};
 #endif
     for (;; ++j) {
       MGN_T(T0);
-      // issue priority to the role on the critical path of the phase: the
-      // ledger's orders in phase 1, the generator's step finish in phase 2
-      // (VALU issue between the two waves of a SIMD goes by priority, then age)
-      __builtin_amdgcn_s_setprio(0);
       // phase 1: tick j
       const double P_prev = s.P[0];
       const uint64_t ts_prev = ts;
@@ -455,16 +545,13 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
         ts = ts + 1;
         sh.price[l] = s.P[0];
       }
-      if (D == 1 && p.shaper == MGN_SHAPER_DDR) g.ddr = ddr_pre(g.shA, g.shB);
       if (threadIdx.x == 0) sh.more[(j + 1) % 3] = 0;
       MGN_T(T1);
       __syncthreads();  // A: prices of tick j published
       MGN_T(T2);
-      __builtin_amdgcn_s_setprio(2);
-      // phase 2: finish step j-1 (its State: the price and time before tick j)
+      // phase 2: store step j-1 (its State: the price and time before tick j)
       if (live && j > 0 && !(ABL && (p.ablate & 4)))
-        duo_finish<S>(sh.rec[(j - 1) & 1], s, p, ov, om, in_kind, env, el, l, ls, P_prev, ts_prev,
-                      need_ar, g);
+        duo_store<S>(sh.rec[(j - 1) & 1], s, p, ov, gs, om, env, el, l, ls, P_prev, ts_prev, g);
       MGN_T(T3);
       __syncthreads();  // B: record j published
       MGN_T(T4);
@@ -479,9 +566,10 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       atomicAdd(&g_duo_stamps[8], (unsigned long long)j);
     }
 #endif
+    MGN_WALL(4);
     if (!live) return;
-    if (D == 1 && p.shaper == MGN_SHAPER_DDR) g.ddr = ddr_pre(g.shA, g.shB);
-    duo_finish<S>(sh.rec[j & 1], s, p, ov, om, in_kind, env, el, l, ls, s.P[0], ts, need_ar, g);
+    duo_store<S>(sh.rec[j & 1], s, p, ov, gs, om, env, el, l, ls, s.P[0], ts, g);
+    MGN_WALL(5);
     if (s.valid[0]) {
       const size_t i = (size_t)env * A + s.asset[0];
       p.P[i] = s.P[0];
@@ -499,35 +587,52 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
         p.rhead[env] = g.head;
         p.rlen[env] = g.len;
       }
-      if (D == 1) {
-        p.sA[env] = g.shA;
-        p.sB[env] = g.shB;
-      }
-    }
-    if (D != 1 && s.valid[0]) {
-      p.sA[(size_t)env * A + s.asset[0]] = g.shA;
-      p.sB[(size_t)env * A + s.asset[0]] = g.shB;
     }
     return;
   }
 
   // ---------------- ledger waves
-  const uint32_t om = traj_mask(out);
-  const mgn_traj ov = traj_vgpr(out);
-  act_in = vptr(act_in);
-  units_in = vptr(units_in);
-  aidx_in = vptr(aidx_in);
+  const MGN_G int8_t* gact = vptr(act_in);
+  const MGN_G double* gunits = vptr(units_in);
+  const MGN_G int32_t* gaidx = vptr(aidx_in);
   p.init_cash = in_vgpr(p.init_cash);
   p.mainM = in_vgpr(p.mainM);
   p.unit_size = in_vgpr(p.unit_size);
+  p.eta = in_vgpr(p.eta);
+  p.cos_temp = in_vgpr(p.cos_temp);
   Lane<M> s;
   load_lane<M>(s, p, envc, ls);
   if (!live) s.valid[0] = false;
   double cash = p.cash[envc];
+  const int D = p.D;
+  LedOut g;
+  if (D == 1) {
+    g.shA = p.sA[envc];
+    g.shB = p.sB[envc];
+  } else {
+    g.shA = s.valid[0] ? p.sA[(size_t)envc * A + s.asset[0]] : 0.;
+    g.shB = s.valid[0] ? p.sB[(size_t)envc * A + s.asset[0]] : 0.;
+  }
+  g.cos_qn = 0.;
+  if (p.shaper == MGN_SHAPER_PPC) {
+    double qq[M];
+    const double q = s.valid[0] ? s_tgt[1 + s.asset[0]] : 0.;
+    qq[0] = q * q;
+    g.cos_qn = sqrt(s_tgt[0] * s_tgt[0] + canon<M, S>(qq));
+  }
+  const bool need_ar = (p.reward_mode != MGN_REWARD_ENV_LOG) || (out.agent_reward != nullptr);
   Sums s0 = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
-  int8_t act_next[M] = {0};
-  if (in_kind == IN_DISCRETE && s.valid[0]) act_next[0] = act_in[(size_t)env * A + s.asset[0]];
+  // the discrete action of lane (env, asset) at step k lives at act + k * N * A;
+  // one load per iteration, unconditional (clamped address), one step ahead:
+  // no merge copy of a pending load, so the wait lands at the next iteration's use
+  const MGN_G int8_t* act_lane = gact + (size_t)envc * A + (s.valid[0] ? s.asset[0] : 0);
+  const size_t act_step = (size_t)p.N * A;
+  int act_cur = 0;  // the action of step k, loaded one iteration ahead
+  if (in_kind == IN_DISCRETE) act_cur = act_lane[0];
+  drain_vmem();
 
+  __builtin_amdgcn_s_setprio(2);  // the critical path of both phases
+  MGN_WALL(2);
   int k = 0;
   int pending = 0;
 #ifdef MGN_STAMPS
@@ -540,9 +645,15 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
 #ifdef MGN_STAMPS
     jn = j;
 #endif
-    __builtin_amdgcn_s_setprio(2);
     const bool stepping = live && (pending == 0) && (k < K);
     const bool ticking = live && (stepping || (pending > 0));
+    // this iteration's action, and the load of the next iteration's (step k + 1
+    // if this one steps, else step k again)
+    const int act_now = act_cur;
+    if (in_kind == IN_DISCRETE) {
+      const int kn = k + (stepping ? 1 : 0);
+      act_cur = act_lane[(size_t)(kn < K ? kn : K - 1) * act_step];
+    }
     const size_t oN = (size_t)k * p.N, oNA = (size_t)k * p.N * A;
     double uc[M], tp[M], tu[M], tc[M];
     int rk[M];
@@ -561,19 +672,17 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
         const double bp = (cash + s0.sh) + (s0.lp - s0.ml);
         const double avM = RQ1 ? bp : bp / p.reqM;
         const int half = p.atoms / 2;
-        const int a = act_next[0];
-        if (k + 1 < K && s.valid[0])
-          act_next[0] = act_in[oNA + (size_t)p.N * A + (size_t)env * A + s.asset[0]];
+        const int a = act_now;
         if (s.valid[0]) {
           const double u = p.unit_size * avM / s.P[0];
           uc[0] = (double)(a - half) * u;
           if (a == 0) uc[0] = (s.L[0] != 0) ? -s.L[0] : 0.;
         }
       } else if (in_kind == IN_UNITS) {
-        uc[0] = s.valid[0] ? units_in[oNA + (size_t)env * A + s.asset[0]] : 0.;
+        uc[0] = s.valid[0] ? gunits[oNA + (size_t)env * A + s.asset[0]] : 0.;
       } else if (in_kind == IN_SINGLE) {
-        const int ai = aidx_in[env];
-        const double u = units_in[oN + env];
+        const int ai = gaidx[env];
+        const double u = gunits[oN + env];
         uc[0] = (s.valid[0] && s.asset[0] == ai) ? u : 0.;
       }
       prevVal = s.L[0] * s.P[0];
@@ -591,7 +700,6 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
     MGN_T(T1);
     __syncthreads();  // A: the prices of tick j are in LDS
     MGN_T(T2);
-    __builtin_amdgcn_s_setprio(0);
     bool reset_now = false;
     int flags = 0;
     DuoRec<S>& rc = sh.rec[j & 1];
@@ -605,44 +713,39 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
         q.lp = canon<M, S>(tlp);
       }
       const double curEq = (cash + q.lp) - q.b;
-      // Env.h:211-212 (0.01 clamp for step(i, u), Env.h:238); on this side, whose
-      // phase 2 has slack, for the generator side's step finish
+      // Env.h:211-212 (0.01 clamp for step(i, u), Env.h:238)
       const double ratio = curEq / prevEq;
       const double clampv = (in_kind == IN_SINGLE) ? 0.01 : 0.3;
       const double reward = log_ratio((ratio < clampv) ? clampv : ratio);
       const bool done = any_mc || margin_call(q, cash, p.mainM) || (curEq < 0.1 * p.init_cash);
+#ifdef MGN_STAMPS
+      const unsigned long long t_p2a = __builtin_amdgcn_s_memtime();
+#endif
       rc.rL[l] = s.L[0];
-      rc.rPrev[l] = prevVal;
       rc.rTp[l] = tp[0];
       rc.rTu[l] = tu[0];
       rc.rTc[l] = tc[0];
       rc.rRk[l] = rk[0];
       flags = REC_STEP | (done ? REC_DONE : 0) | (mcall ? REC_MCALL : 0);
-      // the step's ledger-side outputs: BrokerResponse, State.portfolio =
-      // ledgerNormedFull (Portfolio.cpp:150-155), State.price, done, marginCall
-      if (s.valid[0]) {
-        const size_t i = oNA + (size_t)env * A + s.asset[0];
-        if (om & O_TP) ov.tprice[i] = tp[0];
-        if (om & O_TU) ov.tunits[i] = tu[0];
-        if (om & O_TC) ov.tcost[i] = tc[0];
-        if (om & O_RISK) ov.risk[i] = (uint8_t)rk[0];
-        if (om & O_OPT)
-          ov.obs_port[(size_t)k * p.N * (A + 1) + (size_t)env * (A + 1) + 1 + s.asset[0]] =
-              (s.L[0] * s.P[0]) / curEq;
-        if (om & O_OPR) ov.obs_price[(oN + env) * (size_t)p.F + s.asset[0]] = s.P[0];
+      // the step finish (ledgerNormedFull, agent reward, shaper) into the
+      // record; the generator side stores the step's outputs from it one
+      // iteration later, so the ledger waves issue no stores and their only
+      // vector-memory wait is on the action load
+      if (!(ABL && (p.ablate & 4)))
+        ledger_finish<S>(rc, s, p, s_tgt, el, l, ls, cash, q.b, prevEq, curEq, reward, prevVal, tp[0],
+                         tu[0], tc[0], need_ar, g);
+#ifdef MGN_STAMPS
+      const unsigned long long t_p2b = __builtin_amdgcn_s_memtime();
+      if (threadIdx.x == DUO_HALF) {
+        s_duo_sub[3] += t_p2a - T2;
+        s_duo_sub[4] += t_p2b - t_p2a;
       }
+#endif
       if (ls == 0) {
-        if (om & O_OPT) ov.obs_port[(size_t)k * p.N * (A + 1) + (size_t)env * (A + 1)] = (cash - q.b) / curEq;
-        if (om & O_DONE) ov.done[oN + env] = done ? 1 : 0;
-        if (om & O_MC) ov.margin_call[oN + env] = (uint8_t)mcall;
-      }
-      if (ls == 0) {
-        rc.rPrevEq[el] = prevEq;
         rc.rCurEq[el] = curEq;
-        rc.rRew[el] = reward;
         rc.rCash[el] = cash;
-        rc.rLp[el] = q.lp;
         rc.rB[el] = q.b;
+        rc.rRew[el] = reward;
         rc.rK[el] = k;
       }
       s0 = q;
@@ -662,11 +765,11 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       pending -= 1;
       const Sums q = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
       if (pending == 0) s0 = q;
-      rc.rL[l] = s.L[0];
       flags = REC_TICK;
-      if (ls == 0) {
+      rc.rL[l] = s.L[0];
+      if (ls == 0) {  // the window row's equity (ring_push's sums)
+        rc.rCurEq[el] = (cash + q.lp) - q.b;
         rc.rCash[el] = cash;
-        rc.rLp[el] = q.lp;
         rc.rB[el] = q.b;
       }
     }
@@ -682,9 +785,12 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
     MGN_T(T4);
 #ifdef MGN_STAMPS
     acc[0] += T1 - T0; acc[1] += T2 - T1; acc[2] += T3 - T2; acc[3] += T4 - T3;
+    if (j == 0) MGN_WALL(6);
+    if (j == 2) MGN_WALL(7);
 #endif
     if (!sh.more[j % 3]) break;
   }
+  MGN_WALL(3);
 #ifdef MGN_STAMPS
   if (threadIdx.x == DUO_HALF) {
     for (int i = 0; i < 4; ++i) atomicAdd(&g_duo_stamps[4 + i], acc[i]);
@@ -692,6 +798,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
     atomicAdd(&g_duo_stamps[10], 1ull);
     atomicAdd(&g_duo_stamps[11], accb[0]);
     atomicAdd(&g_duo_stamps[12], accb[1]);
+    for (int i = 0; i < 5; ++i) atomicAdd(&g_duo_stamps[13 + i], s_duo_sub[i]);
   }
 #endif
 
@@ -702,7 +809,17 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
     p.mep[i] = s.mep[0];
     p.Bm[i] = s.Bm[0];
   }
-  if (ls == 0) p.cash[env] = cash;
+  if (ls == 0) {
+    p.cash[env] = cash;
+    if (D == 1) {
+      p.sA[env] = g.shA;
+      p.sB[env] = g.shB;
+    }
+  }
+  if (D != 1 && s.valid[0]) {
+    p.sA[(size_t)env * A + s.asset[0]] = g.shA;
+    p.sB[(size_t)env * A + s.asset[0]] = g.shB;
+  }
 }
 
 }  // namespace mgn

@@ -25,6 +25,11 @@ namespace mgn {
 
 constexpr int BLOCK = 256;
 
+// wait for every outstanding vector-memory load / store of this wave, as a
+// real S_WAITCNT (gfx9 simm16: vmcnt 0, expcnt 7, lgkmcnt 15) that the
+// wait-count insertion pass sees: loads issued before it are complete after it
+__device__ __forceinline__ void drain_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 struct KParams {
   int N, A, W, D;
   int F;       // State.price width (features): A for the generators
@@ -479,6 +484,7 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
                             kind == MGN_SRC_SINEDYNTREND, p.seed, genv, (uint32_t)a, tick);
     } else {
       s.P[m] = p.ext[(size_t)env * p.A + a];
+      drain_vmem();  // in this branch: the kinds' merge point then needs no wait
     }
   }
 }
@@ -671,6 +677,7 @@ __device__ __forceinline__ T in_vgpr(T x) {
   asm volatile("" : "+v"(x));
   return x;
 }
+
 
 // x / required_margin; x / 1.0 == x exactly in IEEE, so the common
 // required_margin == 1 case skips the division with identical bits.
@@ -1042,7 +1049,7 @@ __device__ __forceinline__ double dsr_one(double r, double A, double B) {
   // ((B - A^2)^2)^(3/4) = |B - A^2|^(3/2), evaluated as a*sqrt(a): within 2 ulp of
   // libm pow (outputs are compared at rtol 1e-12; they never feed back into state)
   const double a = fabs(t);
-  return (B * dA - (A * dB) / 2) / (a * sqrt(a) + 1.1920928955078125e-07);
+  return out_div(B * dA - (A * dB) / 2, a * sqrt(a) + 1.1920928955078125e-07);
 }
 __device__ __forceinline__ double ddr_one(double r, double A, double B) {
   // r > 0: (r - A/2) / (sqrt(B) + eps); else (B(r - A/2) - A r^2/2) / (B^(3/2) + eps),
@@ -1052,7 +1059,7 @@ __device__ __forceinline__ double ddr_one(double r, double A, double B) {
   const bool pos = r > 0.;
   const double num = pos ? h : (B * h - (A * (r * r)) / 2);
   const double den = (pos ? sB : B * sB) + 1.1920928955078125e-07;
-  return num / den;
+  return out_div(num, den);
 }
 // ddr_one with its reward-independent operands (A/2 and the two
 // denominators) evaluated ahead of the reward: the same operations on the
@@ -1068,7 +1075,7 @@ __device__ __forceinline__ double ddr_one_pre(double r, double A, double B, cons
   const double h = r - q.hA;
   const bool pos = r > 0.;
   const double num = pos ? h : (B * h - (A * (r * r)) / 2);
-  return num / (pos ? q.dpos : q.dneg);
+  return out_div(num, pos ? q.dpos : q.dneg);
 }
 __device__ __forceinline__ double clip1(double v) { return v < -1. ? -1. : (v > 1. ? 1. : v); }
 

@@ -3,9 +3,12 @@
 MGN_DEFINE_APAD(8)
 #ifdef MGN_STAMPS
 extern "C" int mgn_diag_stamps(unsigned long long* h) {
-  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(mgn::g_duo_stamps), 16 * sizeof(unsigned long long)) != hipSuccess)
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(mgn::g_duo_stamps), 24 * sizeof(unsigned long long)) != hipSuccess)
     return 1;
-  unsigned long long z[16] = {};
+  unsigned long long z[24] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(mgn::g_duo_stamps), z, sizeof(z)) != hipSuccess;
+}
+extern "C" int mgn_diag_wall(unsigned long long* h) {
+  return hipMemcpyFromSymbol(h, HIP_SYMBOL(mgn::g_duo_wall), 2048 * 8 * sizeof(unsigned long long)) != hipSuccess;
 }
 #endif

@@ -34,12 +34,16 @@ void launch_duo(const StepArgs& a) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(DUO_BLOCK), 0, a.stream, a.p, a.out, a.in_kind,
                        a.units, a.aidx, a.act, a.K);
   };
-  if (a.p.ablate) {
-    if (a.p.reqm_one) go(k_step_duo<S, true, true>);
-    else go(k_step_duo<S, false, true>);
+  const bool disc = a.in_kind == IN_DISCRETE;
+  if (a.p.ablate) {  // diagnostic timing builds: discrete actions only
+    if (a.p.reqm_one) go(k_step_duo<S, true, true, true>);
+    else go(k_step_duo<S, false, true, true>);
+  } else if (disc) {
+    if (a.p.reqm_one) go(k_step_duo<S, true, false, true>);
+    else go(k_step_duo<S, false, false, true>);
   } else {
-    if (a.p.reqm_one) go(k_step_duo<S, true, false>);
-    else go(k_step_duo<S, false, false>);
+    if (a.p.reqm_one) go(k_step_duo<S, true, false, false>);
+    else go(k_step_duo<S, false, false, false>);
   }
 }
 

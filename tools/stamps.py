@@ -29,8 +29,11 @@ def main():
     for _ in range(3):
         env.rollout(acts)
     torch.cuda.synchronize()
-    buf = (C.c_ulonglong * 16)()
+    buf = (C.c_ulonglong * 24)()
     fn(buf)
+    wall = getattr(lib, "mgn_diag_wall")
+    wall.argtypes = [C.POINTER(C.c_ulonglong)]
+    wb = (C.c_ulonglong * (2048 * 8))()
     reps = 10
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -48,7 +51,23 @@ def main():
         res[role] = {k: round(v[base + i] / max(it, 1), 1)
                      for i, k in enumerate(("work1", "waitA", "work2", "waitB"))}
     res["ledger"]["action"] = round(v[11] / max(it_l, 1), 1)
-    res["ledger"]["broker"] = round(v[12] / max(it_l, 1), 1)
+    res["ledger"]["broker_parts"] = {k: round(v[13 + i] / max(it_l, 1), 1)
+                                     for i, k in enumerate(("order_prep", "spec_loop", "post"))}
+    res["ledger"]["phase2_parts"] = {k: round(v[16 + i] / max(it_l, 1), 1)
+                                     for i, k in enumerate(("sums_done", "finish"))}
+    # one more launch for the wall-clock phases (us from the first block entry)
+    env.rollout(acts)
+    torch.cuda.synchronize()
+    wall(wb)
+    import numpy as np
+    nb = min(2048, (N + 31) // 32)
+    w = np.frombuffer(wb, dtype=np.uint64).reshape(2048, 8)[:nb].astype(np.int64)
+    t0 = w[:, :2].min()
+    names = ("gen_entry", "led_entry", "led_loop_start", "led_loop_end", "gen_loop_end", "gen_exit",
+             "led_iter0_end", "led_iter2_end")
+    res["wall_us"] = {k: [round(float(w[:, i].min() - t0) / 100, 2),
+                          round(float(np.median(w[:, i]) - t0) / 100, 2),
+                          round(float(w[:, i].max() - t0) / 100, 2)] for i, k in enumerate(names)}
     print(json.dumps(res))
 
 

@@ -395,8 +395,9 @@ def main():
         gathered = env.episode_stats
     torch.cuda.synchronize()
     if world > 1:
+        # barrier + synchronize; at one rank the synchronize above is both
         dist.barrier()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     L.check(rc, h)
     if world > 1:
@@ -598,8 +599,9 @@ def windowed(args, world, rank, dev):
         gathered = env.episode_stats
     torch.cuda.synchronize()
     if world > 1:
+        # barrier + synchronize; at one rank the synchronize above is both
         dist.barrier()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)

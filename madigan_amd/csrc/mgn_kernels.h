@@ -1049,7 +1049,7 @@ __device__ __forceinline__ double dsr_one(double r, double A, double B) {
   // ((B - A^2)^2)^(3/4) = |B - A^2|^(3/2), evaluated as a*sqrt(a): within 2 ulp of
   // libm pow (outputs are compared at rtol 1e-12; they never feed back into state)
   const double a = fabs(t);
-  return out_div(B * dA - (A * dB) / 2, a * sqrt(a) + 1.1920928955078125e-07);
+  return (B * dA - (A * dB) / 2) / (a * sqrt(a) + 1.1920928955078125e-07);
 }
 __device__ __forceinline__ double ddr_one(double r, double A, double B) {
   // r > 0: (r - A/2) / (sqrt(B) + eps); else (B(r - A/2) - A r^2/2) / (B^(3/2) + eps),
@@ -1059,7 +1059,7 @@ __device__ __forceinline__ double ddr_one(double r, double A, double B) {
   const bool pos = r > 0.;
   const double num = pos ? h : (B * h - (A * (r * r)) / 2);
   const double den = (pos ? sB : B * sB) + 1.1920928955078125e-07;
-  return out_div(num, den);
+  return num / den;
 }
 // ddr_one with its reward-independent operands (A/2 and the two
 // denominators) evaluated ahead of the reward: the same operations on the
@@ -1075,7 +1075,7 @@ __device__ __forceinline__ double ddr_one_pre(double r, double A, double B, cons
   const double h = r - q.hA;
   const bool pos = r > 0.;
   const double num = pos ? h : (B * h - (A * (r * r)) / 2);
-  return out_div(num, pos ? q.dpos : q.dneg);
+  return num / (pos ? q.dpos : q.dneg);
 }
 __device__ __forceinline__ double clip1(double v) { return v < -1. ? -1. : (v > 1. ? 1. : v); }
 

@@ -9,6 +9,6 @@ extern "C" int mgn_diag_stamps(unsigned long long* h) {
   return hipMemcpyToSymbol(HIP_SYMBOL(mgn::g_duo_stamps), z, sizeof(z)) != hipSuccess;
 }
 extern "C" int mgn_diag_wall(unsigned long long* h) {
-  return hipMemcpyFromSymbol(h, HIP_SYMBOL(mgn::g_duo_wall), 2048 * 8 * sizeof(unsigned long long)) != hipSuccess;
+  return hipMemcpyFromSymbol(h, HIP_SYMBOL(mgn::g_duo_wall), 2048 * 16 * sizeof(unsigned long long)) != hipSuccess;
 }
 #endif

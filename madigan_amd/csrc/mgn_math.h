@@ -203,25 +203,12 @@ __device__ __forceinline__ Draw draw0(uint64_t seed, uint64_t env, uint32_t asse
 // rare last-bit cases (36 of 3e5 random ratios against glibc).  |s| < 1/63,
 // so the dropped s^11/11 term is < 2^-66 relative.  Elsewhere the library log.
 // Compared with the oracle (glibc log) at rtol 1e-12.
-// n / d for outputs that never feed back into state (rewards, shaped
-// rewards; compared with the oracle at rtol 1e-12): the hardware reciprocal,
-// one Newton step on it and one correction of the quotient -- within an ulp
-// of the correctly rounded quotient, in 6 instructions and a shorter chain
-// than the IEEE division sequence (div_scale / rcp / 4 fma / div_fmas /
-// div_fixup).  d must be a normal positive or negative number.
-__device__ __forceinline__ double out_div(double n, double d) {
-  double r = __builtin_amdgcn_rcp(d);
-  r = __fma_rn(__fma_rn(-d, r, 1.0), r, r);
-  const double q = n * r;
-  return __fma_rn(__fma_rn(-q, d, n), r, q);
-}
-
 __device__ __forceinline__ double log_ratio(double x) {
   const double d = x - 1.0;
   if (fabs(d) <= 0.03125) {
     const double u = x + 1.0;
     const double e = x - (u - 1.0);  // x + 1 == u + e exactly
-    const double sh = out_div(d, u);  // the residual below is exact for any sh near d / u
+    const double sh = d / u;
     const double r = __fma_rn(-sh, u, d);  // d - sh * u exactly
     const double sl = (r - sh * e) * 0.5;  // 1/u ~ 1/2 to 2 %: s_lo needs few bits
     const double s2 = sh * sh;

@@ -33,7 +33,7 @@ def main():
     fn(buf)
     wall = getattr(lib, "mgn_diag_wall")
     wall.argtypes = [C.POINTER(C.c_ulonglong)]
-    wb = (C.c_ulonglong * (2048 * 8))()
+    wb = (C.c_ulonglong * (2048 * 16))()
     reps = 10
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -61,7 +61,10 @@ def main():
     wall(wb)
     import numpy as np
     nb = min(2048, (N + 31) // 32)
-    w = np.frombuffer(wb, dtype=np.uint64).reshape(2048, 8)[:nb].astype(np.int64)
+    raw = np.frombuffer(wb, dtype=np.uint64).reshape(2048, 16)[:nb].copy()
+    if os.environ.get("STAMPS_RAW"):
+        np.save(os.environ["STAMPS_RAW"], raw)
+    w = raw[:, :8].astype(np.int64)
     t0 = w[:, :2].min()
     names = ("gen_entry", "led_entry", "led_loop_start", "led_loop_end", "gen_loop_end", "gen_exit",
              "led_iter0_end", "led_iter2_end")

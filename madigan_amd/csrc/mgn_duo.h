@@ -47,12 +47,27 @@ __shared__ unsigned long long s_duo_sub[8];
 // stores by one lane: [0] generator entry, [1] ledger entry, [2] ledger loop
 // start, [3] ledger loop end, [4] generator loop end, [5] generator exit,
 // [6] / [7] ledger after iteration 0 / 2
-__device__ unsigned long long g_duo_wall[2048 * 16];
+__device__ unsigned long long g_duo_wall[2048 * 32];
 #define MGN_T(v) v = __builtin_amdgcn_s_memtime()
-#define MGN_WALL(i) if ((threadIdx.x & 255) == 0 && blockIdx.x < 2048) g_duo_wall[blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime()
+#define MGN_WALL(i) if ((threadIdx.x & 255) == 0 && blockIdx.x < 2048) g_duo_wall[blockIdx.x * 32 + (i)] = __builtin_amdgcn_s_memrealtime()
+#elif defined(MGN_WALLX)
+// lighter diagnostic build: the wall stamps, the hardware ids and per block
+// the slowest iteration's phases ([12] generator store phase, [13] its
+// iteration, [14] ledger phase 1, [15] its iteration), no cycle accumulators
+__device__ unsigned long long g_duo_stamps[24];
+__device__ unsigned long long g_duo_wall[2048 * 32];
+#define MGN_T(v)
+#define MGN_WALL(i) if ((threadIdx.x & 255) == 0 && blockIdx.x < 2048) g_duo_wall[blockIdx.x * 32 + (i)] = __builtin_amdgcn_s_memrealtime()
 #else
 #define MGN_T(v)
 #define MGN_WALL(i)
+#endif
+#ifdef MGN_WALLX
+#define MGN_RT(v) v = __builtin_amdgcn_s_memrealtime()
+#define MGN_WALLV(i, val_) if ((threadIdx.x & 255) == 0 && blockIdx.x < 2048) g_duo_wall[blockIdx.x * 32 + (i)] = (val_)
+#else
+#define MGN_RT(v)
+#define MGN_WALLV(i, val_)
 #endif
 constexpr int DUO_HALF = DUO_BLOCK / 2;
 
@@ -136,6 +151,15 @@ __device__ __forceinline__ GTraj traj_vgpr(const mgn_traj& o) {
   v.n_shaped = vptr(o.n_shaped);
   v.data_end = vptr(o.data_end);
   return v;
+}
+// output stores (written once per launch, read after it)
+template <typename T>
+__device__ __forceinline__ void ost(MGN_G T* q, T v) {
+#ifdef MGN_X_NT
+  __builtin_nontemporal_store(v, q);
+#else
+  *q = v;
+#endif
 }
 // the generator side's per-env state outputs, global VGPR pointers
 struct GState {
@@ -244,28 +268,28 @@ __device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s,
     // BrokerResponse, State.portfolio = ledgerNormedFull, State.price, done, marginCall
     if (valid) {
       const size_t i = oNA + (size_t)env * A + s.asset[0];
-      if (om & O_TP) out.tprice[i] = sh.rTp[l];
-      if (om & O_TU) out.tunits[i] = sh.rTu[l];
-      if (om & O_TC) out.tcost[i] = sh.rTc[l];
-      if (om & O_RISK) out.risk[i] = (uint8_t)sh.rRk[l];
-      if (om & O_OPT) out.obs_port[(size_t)k * p.N * (A + 1) + (size_t)env * (A + 1) + 1 + s.asset[0]] = portA;
-      if (om & O_OPR) out.obs_price[(oN + env) * (size_t)p.F + s.asset[0]] = P;
+      if (om & O_TP) ost(out.tprice + (i), sh.rTp[l]);
+      if (om & O_TU) ost(out.tunits + (i), sh.rTu[l]);
+      if (om & O_TC) ost(out.tcost + (i), sh.rTc[l]);
+      if (om & O_RISK) ost(out.risk + (i), (uint8_t)sh.rRk[l]);
+      if (om & O_OPT) ost(out.obs_port + ((size_t)k * p.N * (A + 1) + (size_t)env * (A + 1) + 1 + s.asset[0]), portA);
+      if (om & O_OPR) ost(out.obs_price + ((oN + env) * (size_t)p.F + s.asset[0]), P);
       if (D != 1) {
-        if (om & O_AREW) out.agent_reward[i] = sh.rAr[l];
-        if (om & O_SHP) out.shaped[i] = sh.rShv[l];
+        if (om & O_AREW) ost(out.agent_reward + (i), sh.rAr[l]);
+        if (om & O_SHP) ost(out.shaped + (i), sh.rShv[l]);
       }
     }
     if (ls == 0) {
-      if (om & O_OPT) out.obs_port[(size_t)k * p.N * (A + 1) + (size_t)env * (A + 1)] = port0;
-      if (om & O_DONE) out.done[oN + env] = done ? 1 : 0;
-      if (om & O_MC) out.margin_call[oN + env] = (flags & REC_MCALL) ? 1 : 0;
-      if (om & O_DEND) out.data_end[oN + env] = 0;
-      if (om & O_REW) out.reward[oN + env] = reward;
-      if (om & O_TS) out.timestamp[oN + env] = ts;
-      if (om & O_NSH) out.n_shaped[oN + env] = 1;
+      if (om & O_OPT) ost(out.obs_port + ((size_t)k * p.N * (A + 1) + (size_t)env * (A + 1)), port0);
+      if (om & O_DONE) ost(out.done + (oN + env), (uint8_t)(done ? 1 : 0));
+      if (om & O_MC) ost(out.margin_call + (oN + env), (uint8_t)((flags & REC_MCALL) ? 1 : 0));
+      if (om & O_DEND) ost(out.data_end + (oN + env), (uint8_t)(0));
+      if (om & O_REW) ost(out.reward + (oN + env), reward);
+      if (om & O_TS) ost(out.timestamp + (oN + env), (uint64_t)(ts));
+      if (om & O_NSH) ost(out.n_shaped + (oN + env), (uint8_t)(1));
       if (D == 1) {
-        if (om & O_AREW) out.agent_reward[oN + env] = sh.rRin[el];
-        if (om & O_SHP) out.shaped[oN + env] = sh.rShaped[el];
+        if (om & O_AREW) ost(out.agent_reward + (oN + env), sh.rRin[el]);
+        if (om & O_SHP) ost(out.shaped + (oN + env), sh.rShaped[el]);
       }
     }
     g.ep_ret += reward;
@@ -439,6 +463,25 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
 #endif
 }
 
+// The kernel arguments (KParams + mgn_traj, ~640 bytes) are read through the
+// scalar cache in chunks the register allocator interleaves with their uses,
+// each chunk a dependent miss on a cold cache at launch (~1.7 us of the
+// prologue measured).  One scalar load per 64-byte line, all in flight
+// together, warms every line for the cost of one miss.
+template <int BYTES>
+__device__ __forceinline__ void warm_kernargs() {
+  static_assert(BYTES <= 12 * 64, "one operand per line below");
+  const __attribute__((address_space(4))) uint32_t* ka =
+      (const __attribute__((address_space(4))) uint32_t*)__builtin_amdgcn_kernarg_segment_ptr();
+  constexpr int L = (BYTES + 63) / 64;
+  uint32_t x[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) x[i] = ka[(i < L ? i : L - 1) * 16];
+  // one consumer of every line: the loads issue together, one wait
+  asm volatile("" ::"s"(x[0]), "s"(x[1]), "s"(x[2]), "s"(x[3]), "s"(x[4]), "s"(x[5]), "s"(x[6]),
+               "s"(x[7]), "s"(x[8]), "s"(x[9]), "s"(x[10]), "s"(x[11]));
+}
+
 // ABL: the diagnostic ablation build (mgn_set_ablation != 0); the product
 // instantiation carries no ablation branches.  DISC: discrete actions
 // (mgn_rollout) compiled in alone; otherwise in_kind selects Env::step() /
@@ -450,12 +493,13 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
                                                         const double* __restrict__ units_in,
                                                         const int32_t* __restrict__ aidx_in,
                                                         const int8_t* __restrict__ act_in, int K) {
+  warm_kernargs<(int)(sizeof(KParams) + sizeof(mgn_traj) + 48)>();
   const int in_kind = DISC ? IN_DISCRETE : in_kind_rt;
   MGN_WALL(threadIdx.x < DUO_HALF ? 0 : 1);
-#ifdef MGN_STAMPS
+#if defined(MGN_STAMPS) || defined(MGN_WALLX)
   if (threadIdx.x == 0 && blockIdx.x < 2048) {  // HW_ID (CU / SE) and XCC_ID of the block
-    g_duo_wall[blockIdx.x * 16 + 8] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-    g_duo_wall[blockIdx.x * 16 + 9] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    g_duo_wall[blockIdx.x * 32 + 8] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    g_duo_wall[blockIdx.x * 32 + 9] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
   }
 #endif
   constexpr int M = 1;
@@ -465,6 +509,70 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
   __shared__ EnvRecs<S> recs[EPB];
   __shared__ mgn_asset_source s_src[APADK];  // p.A <= APADK assets
   __shared__ double s_tgt[MGN_MAX_ASSETS + 1];
+  const bool gen_role = threadIdx.x < DUO_HALF;
+  const int l = threadIdx.x % DUO_HALF;
+  const int el = l / S;
+  const int ls = l % S;
+  const int env = blockIdx.x * EPB + el;
+  const bool live = env < p.N;
+  const int envc = live ? env : 0;  // clamped index for the dead tail (never stored)
+  const int A = p.A;
+  // Prologue: each role's state loads are issued first, then the parameter
+  // staging loads, so the launch pays one memory round trip before the loop
+  // (the staging's wait covers both) instead of two.
+  Lane<M> s;
+  s.asset[0] = ls;
+  s.valid[0] = live && ls < A;
+  s.rcur = 0;
+  s.row = 0;
+  s.pf_ok = false;
+  s.fcol = -1;
+  const size_t li = (size_t)envc * A + (s.valid[0] ? ls : 0);
+  s.P[0] = s.valid[0] ? p.P[li] : 0.;
+  s.L[0] = s.mep[0] = s.Bm[0] = s.sx[0] = s.oum[0] = s.dy[0] = 0.;
+  s.tlen[0] = 0;
+  s.tfl[0] = 0;
+  // generator role: the source state, timestamp, episode accumulators, window
+  uint64_t ts = 0;
+  double ep_ret = 0., ep_len = 0., n_done = 0.;
+  int32_t rhead = 0, rlen = 0;
+  // ledger role: the ledger, cash, shaper state, the first action
+  double cash = 0., shA = 0., shB = 0.;
+  int act_cur = 0;
+  const MGN_G int8_t* act_lane = vptr(act_in) + li;
+  if (gen_role) {
+    if (s.valid[0]) {
+      s.sx[0] = p.sx[li];
+      s.oum[0] = p.oum[li];
+      s.dy[0] = p.dy[li];
+      s.tlen[0] = p.tlen[li];
+      s.tfl[0] = p.tfl[li];
+    }
+    ts = p.ts[envc];
+    ep_ret = p.ep[(size_t)envc * 2];
+    ep_len = p.ep[(size_t)envc * 2 + 1];
+    n_done = p.epstats[(size_t)envc * 4 + 3];
+    if (p.W > 0) {
+      rhead = p.rhead[envc];
+      rlen = p.rlen[envc];
+    }
+  } else {
+    if (s.valid[0]) {
+      s.L[0] = p.L[li];
+      s.mep[0] = p.mep[li];
+      s.Bm[0] = p.Bm[li];
+    }
+    cash = p.cash[envc];
+    if (p.D == 1) {
+      shA = p.sA[envc];
+      shB = p.sB[envc];
+    } else if (s.valid[0]) {
+      shA = p.sA[li];
+      shB = p.sB[li];
+    }
+    if (in_kind == IN_DISCRETE && K > 0) act_cur = act_lane[0];
+  }
+  MGN_WALL(gen_role ? 16 : 17);
   {
     const double* g = reinterpret_cast<const double*>(p.src);
     double* d = reinterpret_cast<double*>(s_src);
@@ -475,14 +583,6 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
     p.src = s_src;
     if (p.target) p.target = s_tgt;
   }
-  const bool gen_role = threadIdx.x < DUO_HALF;
-  const int l = threadIdx.x % DUO_HALF;
-  const int el = l / S;
-  const int ls = l % S;
-  const int env = blockIdx.x * EPB + el;
-  const bool live = env < p.N;
-  const int envc = live ? env : 0;  // clamped index for the dead tail (never stored)
-  const int A = p.A;
   if (!gen_role && ls == 0) {
     sh.tick[el] = (live && K > 0) ? 1 : 0;
     sh.reset[el] = 0;
@@ -498,25 +598,19 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
   if (threadIdx.x < 8) s_duo_sub[threadIdx.x] = 0;
 #endif
   __syncthreads();
+  MGN_WALL(gen_role ? 18 : 19);
+  s.kind[0] = s.valid[0] ? s_src[ls].kind : -1;
 
   if (gen_role) {
     // ---------------- generator waves
-    Lane<M> s;
-    load_lane<M>(s, p, envc, ls);
-    if (!live) s.valid[0] = false;
-    uint64_t ts = p.ts[envc];
     GenOut g;
-    g.ep_ret = p.ep[(size_t)envc * 2];
-    g.ep_len = p.ep[(size_t)envc * 2 + 1];
-    g.n_done = p.epstats[(size_t)envc * 4 + 3];
-    g.head = 0;
-    g.len = 0;
+    g.ep_ret = ep_ret;
+    g.ep_len = ep_len;
+    g.n_done = n_done;
+    g.head = rhead;
+    g.len = rlen;
     g.hcnt = p.W;
     g.klast = 0;
-    if (p.W > 0) {
-      g.head = p.rhead[envc];
-      g.len = p.rlen[envc];
-    }
     const uint32_t om = traj_mask(out);
     const GTraj ov = traj_vgpr(out);
     GState gs;
@@ -533,6 +627,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
     // tell them from the loop's stores and waits for every store (vmcnt(0))
     // where a prologue value is first used inside the loop
     drain_vmem();
+    MGN_WALL(20);
     int j = 0;
 #ifdef MGN_STAMPS
     unsigned long long T0 = 0, T1 = 0, T2 = 0, T3 = 0, T4 = 0, acc[4] = {0, 0, 0, 0};
@@ -541,6 +636,9 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
     // pass stores the last record through the loop's own (already fetched)
     // store code, with no tick and no barrier
     bool fin = false;
+#ifdef MGN_WALLX
+    unsigned long long R1 = 0, R2 = 0, rmax = 0, rj = 0;
+#endif
     for (;; ++j) {
       MGN_T(T0);
       // phase 1: the ledger's broker is the critical path, its VALU issue goes
@@ -563,10 +661,18 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
         __syncthreads();  // A: prices of tick j published
         MGN_T(T2);
       }
+      MGN_RT(R1);
       __builtin_amdgcn_s_setprio(2);
       // phase 2: store step j-1 (its State: the price and time before tick j)
       if (live && j > 0 && !(ABL && (p.ablate & 4)))
         duo_store<S>(sh.rec[(j - 1) & 1], s, p, ov, gs, om, env, el, l, ls, P_prev, ts_prev, g);
+      MGN_RT(R2);
+#ifdef MGN_WALLX
+      if (R2 - R1 > rmax) {
+        rmax = R2 - R1;
+        rj = j;
+      }
+#endif
       if (fin) break;
       MGN_T(T3);
       __syncthreads();  // B: record j published
@@ -581,6 +687,8 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       }
     }
     MGN_WALL(5);
+    MGN_WALLV(12, rmax);
+    MGN_WALLV(13, rj);
 #ifdef MGN_STAMPS
     if (threadIdx.x == 0) {
       for (int i = 0; i < 4; ++i) atomicAdd(&g_duo_stamps[i], acc[i]);
@@ -611,7 +719,6 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
   }
 
   // ---------------- ledger waves
-  const MGN_G int8_t* gact = vptr(act_in);
   const MGN_G double* gunits = vptr(units_in);
   const MGN_G int32_t* gaidx = vptr(aidx_in);
   p.init_cash = in_vgpr(p.init_cash);
@@ -619,19 +726,10 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
   p.unit_size = in_vgpr(p.unit_size);
   p.eta = in_vgpr(p.eta);
   p.cos_temp = in_vgpr(p.cos_temp);
-  Lane<M> s;
-  load_lane<M>(s, p, envc, ls);
-  if (!live) s.valid[0] = false;
-  double cash = p.cash[envc];
   const int D = p.D;
   LedOut g;
-  if (D == 1) {
-    g.shA = p.sA[envc];
-    g.shB = p.sB[envc];
-  } else {
-    g.shA = s.valid[0] ? p.sA[(size_t)envc * A + s.asset[0]] : 0.;
-    g.shB = s.valid[0] ? p.sB[(size_t)envc * A + s.asset[0]] : 0.;
-  }
+  g.shA = shA;
+  g.shB = shB;
   g.cos_qn = 0.;
   if (p.shaper == MGN_SHAPER_PPC) {
     double qq[M];
@@ -641,14 +739,13 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
   }
   const bool need_ar = (p.reward_mode != MGN_REWARD_ENV_LOG) || (out.agent_reward != nullptr);
   Sums s0 = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
-  // the discrete action of lane (env, asset) at step k lives at act + k * N * A;
-  // one load per iteration, unconditional (clamped address), one step ahead:
-  // no merge copy of a pending load, so the wait lands at the next iteration's use
-  const MGN_G int8_t* act_lane = gact + (size_t)envc * A + (s.valid[0] ? s.asset[0] : 0);
+  // the discrete action of lane (env, asset) at step k lives at act + k * N * A
+  // (act_lane: this lane's step-0 action, loaded in the prologue); one load per
+  // iteration, unconditional (clamped address), one step ahead: no merge copy
+  // of a pending load, so the wait lands at the next iteration's use
   const size_t act_step = (size_t)p.N * A;
-  int act_cur = 0;  // the action of step k, loaded one iteration ahead
-  if (in_kind == IN_DISCRETE) act_cur = act_lane[0];
   drain_vmem();
+  MGN_WALL(21);
 
   __builtin_amdgcn_s_setprio(2);  // the critical path of both phases
   MGN_WALL(2);
@@ -659,8 +756,12 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
   unsigned long long Ta = 0, Tb = 0, accb[2] = {0, 0};
   int jn = 0;
 #endif
+#ifdef MGN_WALLX
+  unsigned long long R0 = 0, R1 = 0, rmax = 0, rj = 0;
+#endif
   for (int j = 0;; ++j) {
     MGN_T(T0);
+    MGN_RT(R0);
 #ifdef MGN_STAMPS
     jn = j;
 #endif
@@ -717,6 +818,13 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
 #endif
     }
     MGN_T(T1);
+    MGN_RT(R1);
+#ifdef MGN_WALLX
+    if (R1 - R0 > rmax) {
+      rmax = R1 - R0;
+      rj = j;
+    }
+#endif
     __syncthreads();  // A: the prices of tick j are in LDS
     MGN_T(T2);
     bool reset_now = false;
@@ -810,6 +918,8 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
     if (!sh.more[j % 3]) break;
   }
   MGN_WALL(3);
+  MGN_WALLV(14, rmax);
+  MGN_WALLV(15, rj);
 #ifdef MGN_STAMPS
   if (threadIdx.x == DUO_HALF) {
     for (int i = 0; i < 4; ++i) atomicAdd(&g_duo_stamps[4 + i], acc[i]);

@@ -26,19 +26,23 @@ def main():
     fn = getattr(lib, "mgn_diag_stamps")
     fn.argtypes = [C.POINTER(C.c_ulonglong)]
     acts = env.generate_actions(fuse, seed=5)
+    # the bench's output set unless STAMPS_FIELDS names one (comma separated)
+    fields = os.environ.get("STAMPS_FIELDS", "reward,shaped,done,obs_price,obs_port,timestamp,tprice,"
+                                             "tunits,tcost,risk,margin_call").split(",")
+    out = env.alloc_traj(fuse, fields=[f for f in fields if f])
     for _ in range(3):
-        env.rollout(acts)
+        env.rollout(acts, out)
     torch.cuda.synchronize()
     buf = (C.c_ulonglong * 24)()
     fn(buf)
     wall = getattr(lib, "mgn_diag_wall")
     wall.argtypes = [C.POINTER(C.c_ulonglong)]
-    wb = (C.c_ulonglong * (2048 * 16))()
+    wb = (C.c_ulonglong * (2048 * 32))()
     reps = 10
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        env.rollout(acts)
+        env.rollout(acts, out)
     e1.record()
     torch.cuda.synchronize()
     fn(buf)
@@ -56,12 +60,12 @@ def main():
     res["ledger"]["phase2_parts"] = {k: round(v[16 + i] / max(it_l, 1), 1)
                                      for i, k in enumerate(("sums_done", "finish"))}
     # one more launch for the wall-clock phases (us from the first block entry)
-    env.rollout(acts)
+    env.rollout(acts, out)
     torch.cuda.synchronize()
     wall(wb)
     import numpy as np
     nb = min(2048, (N + 31) // 32)
-    raw = np.frombuffer(wb, dtype=np.uint64).reshape(2048, 16)[:nb].copy()
+    raw = np.frombuffer(wb, dtype=np.uint64).reshape(2048, 32)[:nb].copy()
     if os.environ.get("STAMPS_RAW"):
         np.save(os.environ["STAMPS_RAW"], raw)
     w = raw[:, :8].astype(np.int64)

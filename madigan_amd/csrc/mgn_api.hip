@@ -314,10 +314,11 @@ void launch_val(const mgn_env* e, double* out);
 // Lane layout: as few lanes per env as keeps >= 2 waves per SIMD resident
 // (256 CUs x 4 SIMDs x 2), so large batches run thread-per-env-like (less
 // cross-lane work per env) and small batches spread each env over more lanes.
-// the two-role kernel: one lane per asset per role, padded width 2..8, one-step
-// rewards, generator sources (k_step handles replay tapes and n-step buffers)
+// the two-role kernel: one lane per asset per role, padded width 2..16, one-step
+// rewards, generator sources or a replay tape (k_step handles n-step buffers
+// and the multi-component sources)
 bool duo_eligible(const mgn_env* e) {
-  return e->apad >= 2 && e->apad <= 8 && e->cfg.nstep == 1 && !e->replay && !e->cfg.aux;
+  return e->apad >= 2 && e->apad <= 16 && e->cfg.nstep == 1 && !e->cfg.aux;
 }
 // automatic: where the single-role kernel would run one lane per asset (small
 // batches: one wave per SIMD), give every asset a second lane in a partner wave
@@ -351,7 +352,7 @@ void launch_step(const mgn_env* e, const mgn_traj& out, int in_kind, const doubl
                  const int32_t* aidx, const int8_t* act, int K) {
   mgn::StepArgs a{kparams(e), out, in_kind, units, aidx, act, K, e->stream};
   if (e->duo) {
-    const int idx = e->apad <= 2 ? 1 : e->apad <= 4 ? 2 : 3;
+    const int idx = e->apad <= 2 ? 1 : e->apad <= 4 ? 2 : e->apad <= 8 ? 3 : 4;
     kDuo[idx](a);
     return;
   }

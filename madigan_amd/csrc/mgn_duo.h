@@ -242,13 +242,42 @@ __device__ __forceinline__ void ledger_finish(DuoRec<S>& rc, const Lane<1>& s, c
   }
 }
 
+// replay (RP): the State's tape row, this lane's feature value and the row's
+// dataEnd flag (HDFSourceSingle, DataSource.cpp:391-398)
+struct RpCur {
+  double curF;
+  int64_t row;
+  uint32_t dend;
+};
+
+// State.price of the record's State into dst (put_feats): the tape's feature
+// row for replay (one column per lane when F <= S, else read back per column),
+// else the generator price of the lane's asset; lg: StackerDiscrete's log
+template <int S, bool RP>
+__device__ __forceinline__ void duo_feats(const Lane<1>& s, const KParams& p, int ls, double P,
+                                          const RpCur& rp, MGN_G double* dst, bool lg) {
+  if constexpr (RP) {
+    if (s.fcol >= 0) {
+      if (s.fcol < p.F) ost(dst + s.fcol, lg ? log_norm(rp.curF) : rp.curF);
+    } else {
+      for (int f = ls; f < p.F; f += S) {
+        const double v = p.rp_feat[(size_t)rp.row * p.F + f];
+        ost(dst + f, lg ? log_norm(v) : v);
+      }
+    }
+  } else if (s.valid[0]) {
+    ost(dst + s.asset[0], lg ? log_norm(P) : P);
+  }
+}
+
 // the generator side's half: the record's stores, episode statistics and
-// window row.  P, ts: the State's price and timestamp (the tick the record
-// belongs to)
-template <int S>
+// window row.  P, ts, rp: the State's price, timestamp and tape row (the tick
+// the record belongs to)
+template <int S, bool RP>
 __device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s, const KParams& p,
                                           const GTraj& out, const GState& gs, uint32_t om, int env,
-                                          int el, int l, int ls, double P, uint64_t ts, GenOut& g) {
+                                          int el, int l, int ls, double P, uint64_t ts, const RpCur& rp,
+                                          GenOut& g) {
   const int flags = sh.rFlags[el];
   if (flags == 0) return;
   const int A = p.A;
@@ -273,17 +302,17 @@ __device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s,
       if (om & O_TC) ost(out.tcost + (i), sh.rTc[l]);
       if (om & O_RISK) ost(out.risk + (i), (uint8_t)sh.rRk[l]);
       if (om & O_OPT) ost(out.obs_port + ((size_t)k * p.N * (A + 1) + (size_t)env * (A + 1) + 1 + s.asset[0]), portA);
-      if (om & O_OPR) ost(out.obs_price + ((oN + env) * (size_t)p.F + s.asset[0]), P);
       if (D != 1) {
         if (om & O_AREW) ost(out.agent_reward + (i), sh.rAr[l]);
         if (om & O_SHP) ost(out.shaped + (i), sh.rShv[l]);
       }
     }
+    if (om & O_OPR) duo_feats<S, RP>(s, p, ls, P, rp, out.obs_price + (oN + env) * (size_t)p.F, false);
     if (ls == 0) {
       if (om & O_OPT) ost(out.obs_port + ((size_t)k * p.N * (A + 1) + (size_t)env * (A + 1)), port0);
       if (om & O_DONE) ost(out.done + (oN + env), (uint8_t)(done ? 1 : 0));
       if (om & O_MC) ost(out.margin_call + (oN + env), (uint8_t)((flags & REC_MCALL) ? 1 : 0));
-      if (om & O_DEND) ost(out.data_end + (oN + env), (uint8_t)(0));
+      if (om & O_DEND) ost(out.data_end + (oN + env), (uint8_t)(RP ? rp.dend : 0u));
       if (om & O_REW) ost(out.reward + (oN + env), reward);
       if (om & O_TS) ost(out.timestamp + (oN + env), (uint64_t)(ts));
       if (om & O_NSH) ost(out.n_shaped + (oN + env), (uint8_t)(1));
@@ -316,14 +345,11 @@ __device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s,
     const int R = p.F + p.A + 1;
     MGN_G double* row = gs.ring + ((size_t)env * p.W + g.head) * R;
     MGN_G double* hrow = p.hist ? gs.hist + ((size_t)env * p.hrows + g.hcnt) * R : nullptr;
+    duo_feats<S, RP>(s, p, ls, P, rp, row, p.ring_log != 0);
+    if (hrow) duo_feats<S, RP>(s, p, ls, P, rp, hrow, p.ring_log != 0);
     if (valid) {
-      const double pv = p.ring_log ? log_norm(P) : P;
-      row[s.asset[0]] = pv;
       row[p.F + 1 + s.asset[0]] = portA;
-      if (hrow) {
-        hrow[s.asset[0]] = pv;
-        hrow[p.F + 1 + s.asset[0]] = portA;
-      }
+      if (hrow) hrow[p.F + 1 + s.asset[0]] = portA;
     }
     if (ls == 0) {
       row[p.F] = port0;
@@ -366,6 +392,36 @@ __device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s,
 // uses, so the ledger, responses and sums are bit-identical to XRounds; an
 // unrefused batch (the common case) costs one pass instead of S dependent
 // rounds.
+// The four canonical sums (L*P, mep*L, short L*mep, borrowed margin) of one
+// pass, as a streaming pairwise tree: leaves are read from LDS in order and
+// each subtree is summed before the next is read, so log2(S) partials per sum
+// are live instead of S leaves (S = 16 kept all 64 leaf doubles in VGPRs and
+// spilled).  The grouping is tree<S>'s, so the sums are bit-identical.  Leaf j
+// is post-order (executed order before this lane's) where bit j of `post`.
+// RP: the subtree is on the root's rightmost path; its left children are
+// recorded in sib[level] so the last leaf can be replaced afterwards.
+struct Q4 {
+  double a, b, c, d;
+};
+__device__ __forceinline__ Q4 q4add(const Q4& x, const Q4& y) {
+  return Q4{x.a + y.a, x.b + y.b, x.c + y.c, x.d + y.d};
+}
+template <int N>
+constexpr int ilog2() { return N <= 1 ? 0 : 1 + ilog2<N / 2>(); }
+template <int S, int LO, int N, bool RP>
+__device__ __forceinline__ Q4 tree4(const EnvRecs<S>& er, uint32_t post, Q4 (&sib)[6]) {
+  if constexpr (N == 1) {
+    const d2* rv = reinterpret_cast<const d2*>(&er.r[LO]) + (((post >> LO) & 1u) ? 2 : 0);
+    const d2 a = rv[0], b = rv[1];
+    return Q4{a.x, a.y, b.x, b.y};
+  } else {
+    const Q4 l = tree4<S, LO, N / 2, false>(er, post, sib);
+    const Q4 r = tree4<S, LO + N / 2, N / 2, RP>(er, post, sib);
+    if constexpr (RP) sib[ilog2<N>() - 1] = l;
+    return q4add(l, r);
+  }
+}
+
 template <int S, bool RQ1>
 __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRecs<S>& er,
                                             double& cash, const double (&uc)[1], double (&tp)[1],
@@ -386,7 +442,12 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
   const double cash0 = cash;
   int go = 0, mc = 0, insuff = 0;
   double cend = cash0;
-  double lv[4][S];  // this lane's leaves of the last (consistent) pass
+  // S <= 8: the leaves of the last (consistent) pass in registers (measured
+  // ~1 % faster at S = 8 than the streaming tree); S = 16: the streaming tree,
+  // its rightmost-path left children kept
+  constexpr bool STREAM = S >= 16;
+  Q4 sib[6];
+  double lv[4][STREAM ? 1 : S];
   for (int it = 0; it <= S; ++it) {
     // cash before this lane's order, and after the last order, under the guess
     double c = cash0, c_own = cash0;
@@ -401,17 +462,29 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
     cend = c;
     // canonical sums before this lane's order: leaves of executed earlier
     // orders after the order, the others before
+    double r0, r1, r2, r3;
+    if constexpr (STREAM) {
+      const Q4 rt = tree4<S, 0, S, true>(er, go_bits & ((1u << ls) - 1u), sib);
+      r0 = rt.a;
+      r1 = rt.b;
+      r2 = rt.c;
+      r3 = rt.d;
+    } else {
 #pragma unroll
-    for (int j = 0; j < S; ++j) {
-      const bool post = (j < ls) && ((go_bits >> j) & 1);
-      const d2* rv = reinterpret_cast<const d2*>(&er.r[j]) + (post ? 2 : 0);
-      const d2 a = rv[0], b = rv[1];
-      lv[0][j] = a.x;
-      lv[1][j] = a.y;
-      lv[2][j] = b.x;
-      lv[3][j] = b.y;
+      for (int j = 0; j < S; ++j) {
+        const bool post = (j < ls) && ((go_bits >> j) & 1);
+        const d2* rv = reinterpret_cast<const d2*>(&er.r[j]) + (post ? 2 : 0);
+        const d2 a = rv[0], b = rv[1];
+        lv[0][j] = a.x;
+        lv[1][j] = a.y;
+        lv[2][j] = b.x;
+        lv[3][j] = b.y;
+      }
+      r0 = tree<S>(lv[0]);
+      r1 = tree<S>(lv[1]);
+      r2 = tree<S>(lv[2]);
+      r3 = tree<S>(lv[3]);
     }
-    const double r0 = tree<S>(lv[0]), r1 = tree<S>(lv[1]), r2 = tree<S>(lv[2]), r3 = tree<S>(lv[3]);
     // Portfolio::checkRisk(i, u), Portfolio.cpp:254-279 (as XRounds)
     const double pnl = r0 - r1;
     const double balance = c_own + r2;
@@ -437,19 +510,30 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
   rk[0] = act ? (mc ? MGN_MARGIN_CALL : (insuff ? MGN_INSUFF_MARGIN : MGN_GREEN)) : rk[0];
   const bool go_own[1] = {go != 0};
   // the post-transaction sums: the last lane's leaves are final but its own;
-  // settle that one and broadcast its trees to the segment
-  if (ls == S - 1 && go) {
-    const d2* rv = reinterpret_cast<const d2*>(&er.r[S - 1]) + 2;
-    const d2 a = rv[0], b = rv[1];
-    lv[0][S - 1] = a.x;
-    lv[1][S - 1] = a.y;
-    lv[2][S - 1] = b.x;
-    lv[3][S - 1] = b.y;
+  // settle that one (its leaf at the bottom of the rightmost path, the left
+  // children recorded) and broadcast its trees to the segment
+  Q4 x;
+  if constexpr (STREAM) {
+    const d2* rv = reinterpret_cast<const d2*>(&er.r[S - 1]) + ((ls == S - 1 && go) ? 2 : 0);
+    const d2 la = rv[0], lb = rv[1];
+    x = Q4{la.x, la.y, lb.x, lb.y};
+#pragma unroll
+    for (int k = 0; k < ilog2<S>(); ++k) x = q4add(sib[k], x);
+  } else {
+    if (ls == S - 1 && go) {
+      const d2* rv = reinterpret_cast<const d2*>(&er.r[S - 1]) + 2;
+      const d2 a = rv[0], b = rv[1];
+      lv[0][S - 1] = a.x;
+      lv[1][S - 1] = a.y;
+      lv[2][S - 1] = b.x;
+      lv[3][S - 1] = b.y;
+    }
+    x = Q4{tree<S>(lv[0]), tree<S>(lv[1]), tree<S>(lv[2]), tree<S>(lv[3])};
   }
-  after.lp = seg_bcast<S, S - 1>(tree<S>(lv[0]));
-  after.ml = seg_bcast<S, S - 1>(tree<S>(lv[1]));
-  after.sh = seg_bcast<S, S - 1>(tree<S>(lv[2]));
-  after.b = seg_bcast<S, S - 1>(tree<S>(lv[3]));
+  after.lp = seg_bcast<S, S - 1>(x.a);
+  after.ml = seg_bcast<S, S - 1>(x.b);
+  after.sh = seg_bcast<S, S - 1>(x.c);
+  after.b = seg_bcast<S, S - 1>(x.d);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   apply_orders<1>(s, go_own, cu2, me2, bm3, tpr, tco, uc, tp, tu, tc);
@@ -482,13 +566,50 @@ __device__ __forceinline__ void warm_kernargs() {
                "s"(x[7]), "s"(x[8]), "s"(x[9]), "s"(x[10]), "s"(x[11]));
 }
 
+// HDFSourceSingle::getData on the tape (gen_tick's replay branch): the row
+// iterCache / loadData would serve, then advance (wrap = the reference's
+// rewind to boundsIdx_.first, DataSource.cpp:368-371, :397-399).  The next
+// row's price, feature, timestamp and dataEnd flag are loaded here for the
+// next tick, so a tick's tape reads leave the step's dependency chain.
+struct RpNext {
+  double P, F;
+  uint64_t ts;
+  uint32_t dend;
+};
+__device__ __forceinline__ void duo_replay_tick(Lane<1>& s, const KParams& p, uint64_t& ts,
+                                                RpCur& cur, RpNext& nx) {
+  const int64_t row = s.rcur;
+  const bool fown = s.fcol >= 0 && s.fcol < p.F;
+  if (s.pf_ok) {
+    if (s.valid[0]) s.P[0] = nx.P;
+    if (fown) cur.curF = nx.F;
+    ts = nx.ts;
+    cur.dend = nx.dend;
+  } else {
+    if (s.valid[0]) s.P[0] = p.rp_price[(size_t)row * p.A + s.asset[0]];
+    if (fown) cur.curF = p.rp_feat[(size_t)row * p.F + s.fcol];
+    ts = p.rp_ts[row];
+    cur.dend = p.rp_end[row];
+  }
+  cur.row = row;
+  s.row = row;
+  s.rcur = (row + 1 == p.rp_rows) ? 0 : row + 1;
+  if (s.valid[0]) nx.P = p.rp_price[(size_t)s.rcur * p.A + s.asset[0]];
+  if (fown) nx.F = p.rp_feat[(size_t)s.rcur * p.F + s.fcol];
+  nx.ts = p.rp_ts[s.rcur];
+  nx.dend = p.rp_end[s.rcur];
+  s.pf_ok = true;
+}
+
 // ABL: the diagnostic ablation build (mgn_set_ablation != 0); the product
 // instantiation carries no ablation branches.  DISC: discrete actions
 // (mgn_rollout) compiled in alone; otherwise in_kind selects Env::step() /
 // step(units) / step(assetIdx, units) at run time.  (With every input kind in
 // one body the paths merge before the Broker, and the wait the units load
-// needs there also stalled the discrete path on its action prefetch.)
-template <int S, bool RQ1, bool ABL, bool DISC>
+// needs there also stalled the discrete path on its action prefetch.)  RP:
+// every asset from the replay tape (mgn_attach_replay): the generator lanes
+// read the tape, one row ahead, instead of ticking a generator.
+template <int S, bool RQ1, bool ABL, bool DISC, bool RP>
 __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out, int in_kind_rt,
                                                         const double* __restrict__ units_in,
                                                         const int32_t* __restrict__ aidx_in,
@@ -541,6 +662,10 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
   int act_cur = 0;
   const MGN_G int8_t* act_lane = vptr(act_in) + li;
   if (gen_role) {
+    if constexpr (RP) {
+      s.rcur = p.rcur[envc];
+      if (p.F <= S) s.fcol = ls;  // one feature column per lane: prefetched
+    }
     if (s.valid[0]) {
       s.sx[0] = p.sx[li];
       s.oum[0] = p.oum[li];
@@ -636,6 +761,8 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
     // pass stores the last record through the loop's own (already fetched)
     // store code, with no tick and no barrier
     bool fin = false;
+    RpCur rp{0., 0, 0u};  // replay: the current State's tape row
+    RpNext rnx{0., 0., 0, 0u};
 #ifdef MGN_WALLX
     unsigned long long R1 = 0, R2 = 0, rmax = 0, rj = 0;
 #endif
@@ -649,11 +776,17 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       // phase 1: tick j
       const double P_prev = s.P[0];
       const uint64_t ts_prev = ts;
+      const RpCur rp_prev = rp;
       if (!fin) {
         if (live && sh.tick[el]) {
-          if (sh.reset[el]) src_reset<M, false>(s, p, env, ts);  // Env::reset -> dataSource->reset (Env.h:183)
-          if (!(ABL && (p.ablate & 2))) gen_tick<M, false, false>(s, p, env, ts);
-          ts = ts + 1;
+          if constexpr (RP) {
+            // the replay source carries on through a reset (DataSource.cpp:200-206)
+            duo_replay_tick(s, p, ts, rp, rnx);
+          } else {
+            if (sh.reset[el]) src_reset<M, false>(s, p, env, ts);  // Env::reset -> dataSource->reset (Env.h:183)
+            if (!(ABL && (p.ablate & 2))) gen_tick<M, false, false>(s, p, env, ts);
+            ts = ts + 1;
+          }
           sh.price[l] = s.P[0];
         }
         if (threadIdx.x == 0) sh.more[(j + 1) % 3] = 0;
@@ -665,7 +798,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       __builtin_amdgcn_s_setprio(2);
       // phase 2: store step j-1 (its State: the price and time before tick j)
       if (live && j > 0 && !(ABL && (p.ablate & 4)))
-        duo_store<S>(sh.rec[(j - 1) & 1], s, p, ov, gs, om, env, el, l, ls, P_prev, ts_prev, g);
+        duo_store<S, RP>(sh.rec[(j - 1) & 1], s, p, ov, gs, om, env, el, l, ls, P_prev, ts_prev, rp_prev, g);
       MGN_RT(R2);
 #ifdef MGN_WALLX
       if (R2 - R1 > rmax) {
@@ -707,6 +840,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
     }
     if (ls == 0) {
       p.ts[env] = ts;
+      if (RP) p.rcur[env] = s.rcur;
       p.ep[(size_t)env * 2] = g.ep_ret;
       p.ep[(size_t)env * 2 + 1] = g.ep_len;
       if (p.W > 0) {

@@ -35,15 +35,23 @@ void launch_duo(const StepArgs& a) {
                        a.units, a.aidx, a.act, a.K);
   };
   const bool disc = a.in_kind == IN_DISCRETE;
-  if (a.p.ablate) {  // diagnostic timing builds: discrete actions only
-    if (a.p.reqm_one) go(k_step_duo<S, true, true, true>);
-    else go(k_step_duo<S, false, true, true>);
+  if (a.p.replay) {  // replay tapes (no ablation build)
+    if (disc) {
+      if (a.p.reqm_one) go(k_step_duo<S, true, false, true, true>);
+      else go(k_step_duo<S, false, false, true, true>);
+    } else {
+      if (a.p.reqm_one) go(k_step_duo<S, true, false, false, true>);
+      else go(k_step_duo<S, false, false, false, true>);
+    }
+  } else if (a.p.ablate) {  // diagnostic timing builds: discrete actions only
+    if (a.p.reqm_one) go(k_step_duo<S, true, true, true, false>);
+    else go(k_step_duo<S, false, true, true, false>);
   } else if (disc) {
-    if (a.p.reqm_one) go(k_step_duo<S, true, false, true>);
-    else go(k_step_duo<S, false, false, true>);
+    if (a.p.reqm_one) go(k_step_duo<S, true, false, true, false>);
+    else go(k_step_duo<S, false, false, true, false>);
   } else {
-    if (a.p.reqm_one) go(k_step_duo<S, true, false, false>);
-    else go(k_step_duo<S, false, false, false>);
+    if (a.p.reqm_one) go(k_step_duo<S, true, false, false, false>);
+    else go(k_step_duo<S, false, false, false, false>);
   }
 }
 
@@ -85,7 +93,7 @@ void dispatch_m(int m, const Arg& a) {
 #define MGN_DEFINE_APAD(A)                                                                   \
   namespace mgn {                                                                            \
   void launch_duo_a##A(const StepArgs& a) {                                                  \
-    if constexpr (A >= 2 && A <= 8) launch_duo<A>(a);                                        \
+    if constexpr (A >= 2 && A <= 16) launch_duo<A>(a);                                       \
   }                                                                                          \
   void launch_step_a##A(int m, const StepArgs& a) { dispatch_m<StepL, A>(m, a); }            \
   void launch_init_a##A(int m, const InitArgs& a) { dispatch_m<InitL, A>(m, a); }            \

@@ -289,6 +289,8 @@ def test_nstep_rollout(gpu, shaper, mode, n):
 
 @pytest.mark.parametrize("A,kw", [
     (8, dict(reward_shaper="DDR")),
+    (16, dict(reward_shaper="DDR")),
+    (13, dict(reward_shaper="DSR", reward_mode="agent_per_asset", window=6)),
     (3, dict(reward_shaper="DSR", reward_mode="agent_per_asset")),
     (4, dict(reward_shaper="PPC", cosine_temp=0.05, window=8, norm_type="log")),
     (2, dict(reward_shaper="sortino_shaperA", sortino_exp=2, reward_mode="agent_sum", window=5)),

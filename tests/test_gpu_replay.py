@@ -35,11 +35,15 @@ def hdf_config(path, cache, start=None, end=None):
     return {"data_source_type": "HDFSourceSingle", "data_source_config": d}
 
 
-@pytest.mark.parametrize("A,F,cache,stride,window,norm", [
-    (3, 5, 37, 7, 8, "lookback"), (1, 2, 300, 0, 0, None), (8, 8, 64, 11, 16, "log"),
-    (16, 3, 25, 5, 4, "standard_normal")])
-def test_replay_rollout_bitwise(gpu, tmp_path, A, F, cache, stride, window, norm):
+@pytest.mark.parametrize("A,F,cache,stride,window,norm,sched", [
+    (3, 5, 37, 7, 8, "lookback", "auto"), (1, 2, 300, 0, 0, None, "auto"),
+    (8, 8, 64, 11, 16, "log", "auto"), (8, 8, 64, 11, 16, "log", "single"),
+    (16, 3, 25, 5, 4, "standard_normal", "auto"), (16, 16, 25, 5, 0, None, "auto")])
+def test_replay_rollout_bitwise(gpu, tmp_path, A, F, cache, stride, window, norm, sched):
+    """Both step schedules: "auto" runs the two-role kernel for A >= 2 (tape
+    rows prefetched by the generator lanes), "single" forces k_step."""
     from madigan_amd import BatchedEnv
+    from madigan_amd import _lib as L
     from madigan_amd.config import spec_from_config
     path, price, feats, ts = replay_file(tmp_path, A=A, F=F, seed=A)
     # a bounded time range that is not a multiple of the cache
@@ -53,6 +57,10 @@ def test_replay_rollout_bitwise(gpu, tmp_path, A, F, cache, stride, window, norm
               transaction_cost_rel=0.002, reward_shaper="DDR", adaptation_rate=0.001,
               unit_size=0.5, auto_reset=True, window=window, norm_type=norm, seed=5)
     g = BatchedEnv(spec, N, device=gpu, replay_stride=stride, **kw)
+    if sched == "single":
+        L.check(g.lib.mgn_set_schedule(g.h, L.SCHED_SINGLE), g.h)
+    else:
+        assert g.lib.mgn_get_schedule(g.h) == (L.SCHED_DUO if A >= 2 else L.SCHED_SINGLE)
     first, second, _, _ = O.hdf_bounds(ts, start, end)
     okw = dict(kw, n_envs=N, n_feats=F, auto_reset=1)
     orc = O.OracleBatch(okw, [(O.SRC_REPLAY, [])] * A)

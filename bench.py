@@ -626,6 +626,7 @@ def windowed(args, world, rank, dev):
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": desc, "n_envs_per_gpu": N, "n_assets": A, "n_feats": env.F,
                        "window": W, "steps_per_launch": Kf,
+                       "schedule": "duo" if int(lib.mgn_get_schedule(h)) == 2 else "single",
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,

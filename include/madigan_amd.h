@@ -367,9 +367,11 @@ size_t mgn_state_bytes(const mgn_env *env);
 int mgn_save_state(mgn_env *env, void *host_dst, size_t bytes);
 int mgn_load_state(mgn_env *env, const void *host_src, size_t bytes);
 /* Measurement only: the attainable HBM bandwidth of a plain
- * device copy -- reps launches of a 16-B-per-lane grid-stride copy of bytes
- * (a multiple of 16) from src_dev to dst_dev on stream, timed with HIP
- * events; *gbps_out = (read + write bytes) / time in GB/s.  Synchronises. */
+ * device copy of bytes (a multiple of 16) from src_dev to dst_dev on stream,
+ * 16 B per lane: the best of six copy shapes (one 16- or 32-KiB chunk per
+ * workgroup or a grid-stride loop; plain or nontemporal stores), each timed over reps
+ * launches with HIP events; *gbps_out = (read + write bytes) / time in GB/s.
+ * Synchronises. */
 int mgn_bandwidth_probe(void *dst_dev, const void *src_dev, size_t bytes, int32_t reps, void *stream,
                         double *gbps_out);
 /* synchronise the handle's stream */

@@ -516,18 +516,41 @@ __global__ void k_gen_actions(int8_t* __restrict__ out, int K, int N, int A, int
 // the box with a device-copy kernel"): a grid-stride 16-B-per-lane copy,
 // 4 loads in flight per lane, non-temporal stores
 typedef double probe_v2 __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ void probe_st(probe_v2* q, probe_v2 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, q);
+  else *q = v;
+}
+// ONESHOT: one U x 4-KiB chunk per workgroup (U x 16 B per lane, each
+// coalesced), grid = bytes / chunk; else a grid-stride loop over 16 waves per
+// CU with 4 loads in flight.  NT: nontemporal stores.
+template <bool NT, bool ONESHOT, int U = 4>
 __global__ __launch_bounds__(BLOCK) void k_copy_probe(const probe_v2* __restrict__ src,
                                                       probe_v2* __restrict__ dst, int64_t n) {
-  const int64_t stride = (int64_t)gridDim.x * BLOCK;
-  int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-  for (; i + 3 * stride < n; i += 4 * stride) {
-    const probe_v2 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-    __builtin_nontemporal_store(a, dst + i);
-    __builtin_nontemporal_store(b, dst + i + stride);
-    __builtin_nontemporal_store(c, dst + i + 2 * stride);
-    __builtin_nontemporal_store(d, dst + i + 3 * stride);
+  if constexpr (ONESHOT) {
+    const int64_t base = (int64_t)blockIdx.x * (U * BLOCK) + threadIdx.x;
+    if (base + (U - 1) * BLOCK < n) {
+      probe_v2 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = src[base + u * BLOCK];
+#pragma unroll
+      for (int u = 0; u < U; ++u) probe_st<NT>(dst + base + u * BLOCK, v[u]);
+    } else {
+      for (int u = 0; u < U; ++u)
+        if (base + u * BLOCK < n) probe_st<NT>(dst + base + u * BLOCK, src[base + u * BLOCK]);
+    }
+  } else {
+    const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+      const probe_v2 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+      probe_st<NT>(dst + i, a);
+      probe_st<NT>(dst + i + stride, b);
+      probe_st<NT>(dst + i + 2 * stride, c);
+      probe_st<NT>(dst + i + 3 * stride, d);
+    }
+    for (; i < n; i += stride) probe_st<NT>(dst + i, src[i]);
   }
-  for (; i < n; i += stride) __builtin_nontemporal_store(src[i], dst + i);
 }
 
 }  // namespace mgn

@@ -84,6 +84,7 @@ struct DuoRec {
   // per env: equity (post-tick, also of a refill tick), cash, borrowed
   // margin, log reward, the shaper's input and output (D == 1)
   double rCurEq[EPB], rCash[EPB], rB[EPB], rRew[EPB], rRin[EPB], rShaped[EPB];
+  double rCos[EPB];  // PPC's cos term (n-step: added to the column at add time)
   int32_t rK[EPB], rFlags[EPB];
 };
 
@@ -187,7 +188,7 @@ struct LedOut {
 
 // the finish of step k on the ledger side (its post-tick quantities in
 // registers); writes the record's output fields
-template <int S>
+template <int S, bool NST>
 __device__ __forceinline__ void ledger_finish(DuoRec<S>& rc, const Lane<1>& s, const KParams& p,
                                               const double* s_tgt, int el, int l, int ls,
                                               double cash, double qb, double prevEq, double curEq,
@@ -219,7 +220,10 @@ __device__ __forceinline__ void ledger_finish(DuoRec<S>& rc, const Lane<1>& s, c
     cos_term = p.cos_temp * (dot / (np_ * g.cos_qn));
   }
   double shaped_s = 0., rin_s = 0., shaped_v = 0.;
-  if (D == 1) {
+  if constexpr (NST) {
+    // n > 1: the generator side adds the column value to the NStepBuffer
+    if (D == 1) rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
+  } else if (D == 1) {
     rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
     if (p.shaper == MGN_SHAPER_DDR) {  // shape() for DDR (nstep_buffer.py:128-162)
       const double r = rin_s;
@@ -239,6 +243,7 @@ __device__ __forceinline__ void ledger_finish(DuoRec<S>& rc, const Lane<1>& s, c
   if (ls == 0) {
     rc.rRin[el] = rin_s;
     rc.rShaped[el] = shaped_s;
+    rc.rCos[el] = cos_term;
   }
 }
 
@@ -270,14 +275,24 @@ __device__ __forceinline__ void duo_feats(const Lane<1>& s, const KParams& p, in
   }
 }
 
+// n > 1 (NST): the NStepBuffer of one env on the generator side -- fill count
+// and oldest index (tracked by every lane of the env), the shaper state of
+// the lane's column (D == 1: the env's, held by lane 0), and the env's (n, D)
+// ring in LDS (nstep_buffer.py:315-356 as replay_buffer.py:68-80 drives it)
+struct NstState {
+  int32_t len, head;
+  double A, B;
+  double* ring;
+};
+
 // the generator side's half: the record's stores, episode statistics and
 // window row.  P, ts, rp: the State's price, timestamp and tape row (the tick
 // the record belongs to)
-template <int S, bool RP>
+template <int S, bool RP, bool NST>
 __device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s, const KParams& p,
                                           const GTraj& out, const GState& gs, uint32_t om, int env,
                                           int el, int l, int ls, double P, uint64_t ts, const RpCur& rp,
-                                          GenOut& g) {
+                                          GenOut& g, NstState& ns) {
   const int flags = sh.rFlags[el];
   if (flags == 0) return;
   const int A = p.A;
@@ -304,7 +319,7 @@ __device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s,
       if (om & O_OPT) ost(out.obs_port + ((size_t)k * p.N * (A + 1) + (size_t)env * (A + 1) + 1 + s.asset[0]), portA);
       if (D != 1) {
         if (om & O_AREW) ost(out.agent_reward + (i), sh.rAr[l]);
-        if (om & O_SHP) ost(out.shaped + (i), sh.rShv[l]);
+        if (!NST && (om & O_SHP)) ost(out.shaped + (i), sh.rShv[l]);
       }
     }
     if (om & O_OPR) duo_feats<S, RP>(s, p, ls, P, rp, out.obs_price + (oN + env) * (size_t)p.F, false);
@@ -315,11 +330,34 @@ __device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s,
       if (om & O_DEND) ost(out.data_end + (oN + env), (uint8_t)(RP ? rp.dend : 0u));
       if (om & O_REW) ost(out.reward + (oN + env), reward);
       if (om & O_TS) ost(out.timestamp + (oN + env), (uint64_t)(ts));
-      if (om & O_NSH) ost(out.n_shaped + (oN + env), (uint8_t)(1));
+      if (!NST && (om & O_NSH)) ost(out.n_shaped + (oN + env), (uint8_t)(1));
       if (D == 1) {
         if (om & O_AREW) ost(out.agent_reward + (oN + env), sh.rRin[el]);
-        if (om & O_SHP) ost(out.shaped + (oN + env), sh.rShaped[el]);
+        if (!NST && (om & O_SHP)) ost(out.shaped + (oN + env), sh.rShaped[el]);
       }
+    }
+    if constexpr (NST) {
+      // NStepBuffer add + pops (as k_step): append the column value; pop once
+      // if full, every entry on done; the popped aggregates are row k's
+      const int n = p.nstep;
+      const int L1 = ns.len + 1;
+      const int pops = done ? L1 : (L1 >= n ? 1 : 0);
+      const bool ppc = p.shaper == MGN_SHAPER_PPC;
+      const double cosv = sh.rCos[el];
+      MGN_G double* row = (om & O_SHP) ? out.shaped + (oN + env) * (size_t)n * D : nullptr;
+      if (D == 1) {
+        if (ls == 0) {
+          const double rin = sh.rRin[el];
+          nstep_column(p, ns.ring, row, 0, 1, ppc ? rin + cosv : rin, done, ns.len, ns.head, ns.A, ns.B);
+        }
+      } else if (valid) {
+        const double a = sh.rAr[l];
+        nstep_column(p, ns.ring, row, s.asset[0], D, ppc ? a + cosv : a, done, ns.len, ns.head, ns.A,
+                     ns.B);
+      }
+      if (ls == 0 && (om & O_NSH)) ost(out.n_shaped + (oN + env), (uint8_t)pops);
+      ns.head = (ns.head + pops) % n;
+      ns.len = L1 - pops;
     }
     g.ep_ret += reward;
     g.ep_len += 1;
@@ -608,8 +646,10 @@ __device__ __forceinline__ void duo_replay_tick(Lane<1>& s, const KParams& p, ui
 // one body the paths merge before the Broker, and the wait the units load
 // needs there also stalled the discrete path on its action prefetch.)  RP:
 // every asset from the replay tape (mgn_attach_replay): the generator lanes
-// read the tape, one row ahead, instead of ticking a generator.
-template <int S, bool RQ1, bool ABL, bool DISC, bool RP>
+// read the tape, one row ahead, instead of ticking a generator.  NST: n-step
+// aggregation (nstep > 1) on the generator side, each env's (n, D) ring in
+// dynamic LDS (launch_duo sizes it: envs per block x n x D doubles).
+template <int S, bool RQ1, bool ABL, bool DISC, bool RP, bool NST>
 __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out, int in_kind_rt,
                                                         const double* __restrict__ units_in,
                                                         const int32_t* __restrict__ aidx_in,
@@ -630,6 +670,8 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
   __shared__ EnvRecs<S> recs[EPB];
   __shared__ mgn_asset_source s_src[APADK];  // p.A <= APADK assets
   __shared__ double s_tgt[MGN_MAX_ASSETS + 1];
+  __shared__ double s_disc[NST ? MGN_MAX_NSTEP : 1];
+  extern __shared__ __attribute__((aligned(16))) double s_nring[];  // NST: (EPB, n, D)
   const bool gen_role = threadIdx.x < DUO_HALF;
   const int l = threadIdx.x % DUO_HALF;
   const int el = l / S;
@@ -661,6 +703,8 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
   double cash = 0., shA = 0., shB = 0.;
   int act_cur = 0;
   const MGN_G int8_t* act_lane = vptr(act_in) + li;
+  // NST (generator role): the env's NStepBuffer
+  NstState nst{0, 0, 0., 0., NST ? s_nring + (size_t)el * p.nstep * p.D : nullptr};
   if (gen_role) {
     if constexpr (RP) {
       s.rcur = p.rcur[envc];
@@ -672,6 +716,20 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       s.dy[0] = p.dy[li];
       s.tlen[0] = p.tlen[li];
       s.tfl[0] = p.tfl[li];
+    }
+    if constexpr (NST) {
+      nst.len = p.nlen[envc];
+      nst.head = p.nhead[envc];
+      if (p.D == 1) {
+        nst.A = p.sA[envc];
+        nst.B = p.sB[envc];
+      } else if (s.valid[0]) {
+        nst.A = p.sA[li];
+        nst.B = p.sB[li];
+      }
+      // the env's ring into LDS (every lane of the env copies a share)
+      const int nD = p.nstep * p.D;
+      for (int i = ls; i < nD; i += S) nst.ring[i] = p.nring[(size_t)envc * nD + i];
     }
     ts = p.ts[envc];
     ep_ret = p.ep[(size_t)envc * 2];
@@ -705,8 +763,11 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
     for (int i = threadIdx.x; i < n; i += DUO_BLOCK) d[i] = g[i];
     if (p.target)
       for (int i = threadIdx.x; i <= p.A; i += DUO_BLOCK) s_tgt[i] = p.target[i];
+    if constexpr (NST)
+      for (int i = threadIdx.x; i < p.nstep; i += DUO_BLOCK) s_disc[i] = p.disc[i];
     p.src = s_src;
     if (p.target) p.target = s_tgt;
+    if constexpr (NST) p.disc = s_disc;
   }
   if (!gen_role && ls == 0) {
     sh.tick[el] = (live && K > 0) ? 1 : 0;
@@ -798,7 +859,8 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       __builtin_amdgcn_s_setprio(2);
       // phase 2: store step j-1 (its State: the price and time before tick j)
       if (live && j > 0 && !(ABL && (p.ablate & 4)))
-        duo_store<S, RP>(sh.rec[(j - 1) & 1], s, p, ov, gs, om, env, el, l, ls, P_prev, ts_prev, rp_prev, g);
+        duo_store<S, RP, NST>(sh.rec[(j - 1) & 1], s, p, ov, gs, om, env, el, l, ls, P_prev, ts_prev,
+                              rp_prev, g, nst);
       MGN_RT(R2);
 #ifdef MGN_WALLX
       if (R2 - R1 > rmax) {
@@ -837,6 +899,23 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       p.dy[i] = s.dy[0];
       p.tlen[i] = s.tlen[0];
       p.tfl[i] = s.tfl[0];
+    }
+    if constexpr (NST) {
+      const int nD = p.nstep * p.D;
+      for (int i = ls; i < nD; i += S) p.nring[(size_t)env * nD + i] = nst.ring[i];
+      if (ls == 0) {
+        p.nlen[env] = nst.len;
+        p.nhead[env] = nst.head;
+      }
+      if (p.D == 1) {
+        if (ls == 0) {
+          p.sA[env] = nst.A;
+          p.sB[env] = nst.B;
+        }
+      } else if (s.valid[0]) {
+        p.sA[(size_t)env * A + s.asset[0]] = nst.A;
+        p.sB[(size_t)env * A + s.asset[0]] = nst.B;
+      }
     }
     if (ls == 0) {
       p.ts[env] = ts;
@@ -993,7 +1072,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       // iteration later, so the ledger waves issue no stores and their only
       // vector-memory wait is on the action load
       if (!(ABL && (p.ablate & 4)))
-        ledger_finish<S>(rc, s, p, s_tgt, el, l, ls, cash, q.b, prevEq, curEq, reward, prevVal, tp[0],
+        ledger_finish<S, NST>(rc, s, p, s_tgt, el, l, ls, cash, q.b, prevEq, curEq, reward, prevVal, tp[0],
                          tu[0], tc[0], need_ar, g);
 #ifdef MGN_STAMPS
       const unsigned long long t_p2b = __builtin_amdgcn_s_memtime();
@@ -1074,12 +1153,12 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
   }
   if (ls == 0) {
     p.cash[env] = cash;
-    if (D == 1) {
+    if (!NST && D == 1) {  // n > 1: the generator side owns the shaper state
       p.sA[env] = g.shA;
       p.sB[env] = g.shB;
     }
   }
-  if (D != 1 && s.valid[0]) {
+  if (!NST && D != 1 && s.valid[0]) {
     p.sA[(size_t)env * A + s.asset[0]] = g.shA;
     p.sB[(size_t)env * A + s.asset[0]] = g.shB;
   }

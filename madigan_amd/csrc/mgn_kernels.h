@@ -1166,11 +1166,12 @@ __device__ __forceinline__ double shape(int shaper, double r, double& A, double&
 // (:62-91, :128-162); PPC / none: sum_k gamma^k v_k, v = r (+ temp*cos for
 // PPC, stored at add time) (:182-204, :23-27).  Ring (n, D) per env, oldest
 // at `head`; out: the env's (n, D) row of this step, zero after the pops.
-__device__ __forceinline__ void nstep_column(const KParams& p, double* out, int env, int d, int D,
+// ring: the env's (n, D) ring (global for k_step, LDS for k_step_duo)
+template <typename RingP, typename OutP>
+__device__ __forceinline__ void nstep_column(const KParams& p, RingP ring, OutP out, int d, int D,
                                           double v, bool done, int len, int head, double& A,
                                           double& B) {
   const int n = p.nstep;
-  double* ring = p.nring + (size_t)env * n * D;
   ring[(size_t)((head + len) % n) * D + d] = v;
   len += 1;
   const bool sr = p.shaper == MGN_SHAPER_DSR || p.shaper == MGN_SHAPER_DDR;
@@ -1497,14 +1498,14 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
         double* row = (out.shaped && !(p.ablate & 4)) ? out.shaped + (oN + env) * (size_t)n * D : nullptr;
         if (D == 1) {
           if (ls == 0)
-            nstep_column(p, row, env, 0, 1, ppc ? rin_s + cos_term : rin_s, done, nlen, nhead,
-                         shA[0], shB[0]);
+            nstep_column(p, p.nring + (size_t)env * n, row, 0, 1, ppc ? rin_s + cos_term : rin_s, done,
+                         nlen, nhead, shA[0], shB[0]);
         } else {
 #pragma unroll
           for (int m = 0; m < M; ++m)
             if (s.valid[m])
-              nstep_column(p, row, env, s.asset[m], D, ppc ? ar[m] + cos_term : ar[m], done, nlen,
-                           nhead, shA[m], shB[m]);
+              nstep_column(p, p.nring + (size_t)env * n * D, row, s.asset[m], D,
+                           ppc ? ar[m] + cos_term : ar[m], done, nlen, nhead, shA[m], shB[m]);
         }
         if (ls == 0 && out.n_shaped && !(p.ablate & 4)) out.n_shaped[oN + env] = (uint8_t)pops;
         nhead = (nhead + pops) % n;

@@ -30,28 +30,40 @@ template <int S>
 void launch_duo(const StepArgs& a) {
   constexpr int epb = DUO_HALF / S;
   const int grid = (a.p.N + epb - 1) / epb;
+  const bool nst = a.p.nstep > 1;
+  // NST: the envs' n-step rings in dynamic LDS (duo_nst_lds_bytes)
+  const size_t lds = nst ? (size_t)epb * a.p.nstep * a.p.D * sizeof(double) : 0;
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(DUO_BLOCK), 0, a.stream, a.p, a.out, a.in_kind,
+    if (lds) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(DUO_BLOCK), lds, a.stream, a.p, a.out, a.in_kind,
                        a.units, a.aidx, a.act, a.K);
   };
   const bool disc = a.in_kind == IN_DISCRETE;
-  if (a.p.replay) {  // replay tapes (no ablation build)
+  if (nst) {  // n-step buffers (generator sources; no ablation build)
     if (disc) {
-      if (a.p.reqm_one) go(k_step_duo<S, true, false, true, true>);
-      else go(k_step_duo<S, false, false, true, true>);
+      if (a.p.reqm_one) go(k_step_duo<S, true, false, true, false, true>);
+      else go(k_step_duo<S, false, false, true, false, true>);
     } else {
-      if (a.p.reqm_one) go(k_step_duo<S, true, false, false, true>);
-      else go(k_step_duo<S, false, false, false, true>);
+      if (a.p.reqm_one) go(k_step_duo<S, true, false, false, false, true>);
+      else go(k_step_duo<S, false, false, false, false, true>);
+    }
+  } else if (a.p.replay) {  // replay tapes (no ablation build)
+    if (disc) {
+      if (a.p.reqm_one) go(k_step_duo<S, true, false, true, true, false>);
+      else go(k_step_duo<S, false, false, true, true, false>);
+    } else {
+      if (a.p.reqm_one) go(k_step_duo<S, true, false, false, true, false>);
+      else go(k_step_duo<S, false, false, false, true, false>);
     }
   } else if (a.p.ablate) {  // diagnostic timing builds: discrete actions only
-    if (a.p.reqm_one) go(k_step_duo<S, true, true, true, false>);
-    else go(k_step_duo<S, false, true, true, false>);
+    if (a.p.reqm_one) go(k_step_duo<S, true, true, true, false, false>);
+    else go(k_step_duo<S, false, true, true, false, false>);
   } else if (disc) {
-    if (a.p.reqm_one) go(k_step_duo<S, true, false, true, false>);
-    else go(k_step_duo<S, false, false, true, false>);
+    if (a.p.reqm_one) go(k_step_duo<S, true, false, true, false, false>);
+    else go(k_step_duo<S, false, false, true, false, false>);
   } else {
-    if (a.p.reqm_one) go(k_step_duo<S, true, false, false, false>);
-    else go(k_step_duo<S, false, false, false, false>);
+    if (a.p.reqm_one) go(k_step_duo<S, true, false, false, false, false>);
+    else go(k_step_duo<S, false, false, false, false, false>);
   }
 }
 

@@ -291,6 +291,10 @@ def test_nstep_rollout(gpu, shaper, mode, n):
     (8, dict(reward_shaper="DDR")),
     (16, dict(reward_shaper="DDR")),
     (13, dict(reward_shaper="DSR", reward_mode="agent_per_asset", window=6)),
+    (8, dict(reward_shaper="DDR", nstep_return=20, discount=0.99)),
+    (3, dict(reward_shaper="DSR", reward_mode="agent_per_asset", nstep_return=4, discount=0.9)),
+    (4, dict(reward_shaper="PPC", cosine_temp=0.05, nstep_return=3, window=4)),
+    (2, dict(reward_shaper="sharpe_shaper", nstep_return=5, reward_mode="agent_sum")),
     (3, dict(reward_shaper="DSR", reward_mode="agent_per_asset")),
     (4, dict(reward_shaper="PPC", cosine_temp=0.05, window=8, norm_type="log")),
     (2, dict(reward_shaper="sortino_shaperA", sortino_exp=2, reward_mode="agent_sum", window=5)),

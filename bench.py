@@ -216,15 +216,16 @@ def c5_replay_file(A: int, T: int, path: str) -> None:
               price_key="price", feature_key="features", timestamp_key="timestamps")
 
 
-def workload_env(name, N, A, rank, dev):
-    """(BatchedEnv, description, window) for a --workload."""
+def workload_env(name, N, A, rank, dev, **extra):
+    """(BatchedEnv, description, window) for a --workload (extra: C3 overrides,
+    e.g. nstep_return for the n-step diagnostic lines)."""
     from madigan_amd import BatchedEnv
     from madigan_amd.config import ou_spec, spec_from_config, trendou_spec
     seed = 0x6D6164 + int(name[1])
     off = rank * N
     if name == "C3":
         spec = trendou_spec(*[[p] * A for p in TRENDOU_P])
-        return (BatchedEnv(spec, N, device=dev, seed=seed, env_offset=off, **c3_kwargs()),
+        return (BatchedEnv(spec, N, device=dev, seed=seed, env_offset=off, **{**c3_kwargs(), **extra}),
                 "C3: TrendOU x8 assets per env, slippage 1e-4 + 2% cost broker, DDR eta=.001 n=1, "
                 "discrete actions via action_to_transaction, auto-reset", 0)
     base = dict(required_margin=1.0, maintenance_margin=0.25, transaction_cost_rel=0.02,
@@ -285,7 +286,10 @@ def kernel_name(env, A: int) -> str:
     apad = 1 << max(0, (A - 1).bit_length())
     rq1 = "true" if env.cfg.required_margin == 1.0 else "false"
     if int(env.lib.mgn_get_schedule(env.h)) == L.SCHED_DUO:
-        return f"mgn::k_step_duo<{apad}, {rq1}, false>"
+        # <S, RQ1, ABL, DISC, RP, NST>: the bench launches discrete actions
+        rp = "true" if env.spec.replay else "false"
+        nst = "true" if env.nstep > 1 else "false"
+        return f"mgn::k_step_duo<{apad}, {rq1}, false, true, {rp}, {nst}>"
     nst = "true" if env.nstep > 1 else "false"
     return f"mgn::k_step<{m}, {apad // m}, {rq1}, {nst}>"
 
@@ -303,6 +307,10 @@ def main():
     ap.add_argument("--n-envs", type=int, default=8192, help="envs per GPU")
     ap.add_argument("--assets", type=int, default=8)
     ap.add_argument("--layout", type=int, default=0, help="assets per lane (0 = auto)")
+    ap.add_argument("--schedule", default="auto", choices=["auto", "single", "duo"],
+                    help="C3 diagnostics: pin the step kernel (results are bit-identical)")
+    ap.add_argument("--nstep", type=int, default=1,
+                    help="C3 diagnostics: n-step aggregation (nstep_return), not the headline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sweep", action="store_true",
                     help="also time 1/16/64/256 steps per launch (separate launches; keep it off "
@@ -339,9 +347,14 @@ def main():
     if args.workload != "C3":
         return windowed(args, world, rank, dev)
     N, A, F = args.n_envs, args.assets, args.fuse
-    env, _, _ = workload_env("C3", N, A, rank, dev)
+    extra = dict(nstep_return=args.nstep, discount=0.99) if args.nstep > 1 else {}
+    env, _, _ = workload_env("C3", N, A, rank, dev, **extra)
     if args.layout:
         env.lib.mgn_set_layout(env.h, args.layout)
+    if args.schedule != "auto":
+        from madigan_amd import _lib as L
+        L.check(env.lib.mgn_set_schedule(env.h, L.SCHED_DUO if args.schedule == "duo" else L.SCHED_SINGLE),
+                env.h)
     import ctypes as C
     from madigan_amd import _lib as L
     lib, h = env.lib, env.h

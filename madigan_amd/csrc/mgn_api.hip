@@ -323,7 +323,7 @@ bool duo_eligible(const mgn_env* e) {
   if (e->apad < 2 || e->apad > 16 || e->cfg.aux) return false;
   if (e->cfg.nstep > 1) {
     const size_t epb = (size_t)(256 / e->apad);  // DUO_BLOCK / 2 lanes per role (mgn_duo.h)
-    if (e->replay || epb * e->cfg.nstep * e->D * sizeof(double) > kDuoNstLds) return false;
+    if (e->replay || epb * e->cfg.nstep * (e->D + 1) * sizeof(double) > kDuoNstLds) return false;
   }
   return true;
 }

@@ -282,7 +282,8 @@ __device__ __forceinline__ void duo_feats(const Lane<1>& s, const KParams& p, in
 struct NstState {
   int32_t len, head;
   double A, B;
-  double* ring;
+  double* ring;     // (n, D)
+  double* scratch;  // (n): one pop's summands (D == 1)
 };
 
 // the generator side's half: the record's stores, episode statistics and
@@ -345,7 +346,46 @@ __device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s,
       const bool ppc = p.shaper == MGN_SHAPER_PPC;
       const double cosv = sh.rCos[el];
       MGN_G double* row = (om & O_SHP) ? out.shaped + (oN + env) * (size_t)n * D : nullptr;
-      if (D == 1) {
+      const bool naive = p.shaper >= MGN_SHAPER_SHARPE;
+      if (D == 1 && !done && L1 >= n && !naive) {
+        // the common case, one pop of a full buffer: the env's S lanes
+        // evaluate the L1 summands (term k on lane k mod S) into LDS, lane 0
+        // sums them in k order -- nstep_column's operations, in its order
+        const double rin = sh.rRin[el];
+        const int tail = (ns.head + ns.len) % n;
+        if (ls == 0) ns.ring[tail] = ppc ? rin + cosv : rin;
+        const double A0 = seg_bcast<S, 0>(ns.A), B0 = seg_bcast<S, 0>(ns.B);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const PopPre c = pop_pre(p.shaper, A0, B0);
+        double* scr = ns.scratch;
+        for (int kk = ls; kk < L1; kk += S) {
+          const int idx = (ns.head + kk < n) ? ns.head + kk : ns.head + kk - n;
+          scr[kk] = pop_term(p.shaper, ns.ring[idx], A0, B0, c, p.disc[kk]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (ls == 0) {
+          double acc = 0.0;
+          for (int kk = 0; kk < L1; ++kk) acc += scr[kk];
+          double res = acc;
+          if (p.shaper == MGN_SHAPER_DSR || p.shaper == MGN_SHAPER_DDR) {
+            res = clip1(acc / L1);
+            const double r0 = ns.ring[ns.head];
+            ns.A += p.eta * (r0 - ns.A);
+            if (p.shaper == MGN_SHAPER_DSR) {
+              ns.B += p.eta * (r0 * r0 - ns.B);
+            } else {
+              double m = r0 < 0. ? r0 : 0.;
+              if (r0 != r0) m = r0;
+              ns.B += p.eta * (m * m - ns.B);
+            }
+          }
+          if (row) ost(row, res);
+        }
+        if (row)
+          for (int jj = 1 + ls; jj < n; jj += S) ost(row + jj, 0.);
+      } else if (D == 1) {
         if (ls == 0) {
           const double rin = sh.rRin[el];
           nstep_column(p, ns.ring, row, 0, 1, ppc ? rin + cosv : rin, done, ns.len, ns.head, ns.A, ns.B);
@@ -647,8 +687,9 @@ __device__ __forceinline__ void duo_replay_tick(Lane<1>& s, const KParams& p, ui
 // needs there also stalled the discrete path on its action prefetch.)  RP:
 // every asset from the replay tape (mgn_attach_replay): the generator lanes
 // read the tape, one row ahead, instead of ticking a generator.  NST: n-step
-// aggregation (nstep > 1) on the generator side, each env's (n, D) ring in
-// dynamic LDS (launch_duo sizes it: envs per block x n x D doubles).
+// aggregation (nstep > 1) on the generator side, each env's (n, D) ring and
+// an n-entry pop scratch in dynamic LDS (launch_duo sizes it: envs per block
+// x n x (D + 1) doubles).
 template <int S, bool RQ1, bool ABL, bool DISC, bool RP, bool NST>
 __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out, int in_kind_rt,
                                                         const double* __restrict__ units_in,
@@ -704,7 +745,8 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
   int act_cur = 0;
   const MGN_G int8_t* act_lane = vptr(act_in) + li;
   // NST (generator role): the env's NStepBuffer
-  NstState nst{0, 0, 0., 0., NST ? s_nring + (size_t)el * p.nstep * p.D : nullptr};
+  NstState nst{0, 0, 0., 0., NST ? s_nring + (size_t)el * p.nstep * p.D : nullptr,
+               NST ? s_nring + (size_t)EPB * p.nstep * p.D + (size_t)el * p.nstep : nullptr};
   if (gen_role) {
     if constexpr (RP) {
       s.rcur = p.rcur[envc];

@@ -1078,6 +1078,38 @@ __device__ __forceinline__ double ddr_one_pre(double r, double A, double B, cons
   return num / (pos ? q.dpos : q.dneg);
 }
 __device__ __forceinline__ double clip1(double v) { return v < -1. ? -1. : (v > 1. ? 1. : v); }
+// dsr_one with its reward-independent denominator evaluated once per pop (the
+// same operations on the same operands)
+__device__ __forceinline__ double dsr_den(double A, double B) {
+  const double a = fabs(B - A * A);
+  return a * sqrt(a) + 1.1920928955078125e-07;
+}
+__device__ __forceinline__ double dsr_one_den(double r, double A, double B, double den) {
+  const double dA = r - A;
+  const double dB = r * r - B;
+  return (B * dA - (A * dB) / 2) / den;
+}
+// the summand of one NStepBuffer entry at discount slot k (nstep_buffer.py:62-91,
+// :128-162; PPC / none: the stored value)
+struct PopPre {
+  DdrPre q;
+  double dden;
+};
+__device__ __forceinline__ PopPre pop_pre(int shaper, double A, double B) {
+  PopPre c;
+  c.q = DdrPre{0., 0., 0.};
+  c.dden = 0.;
+  if (shaper == MGN_SHAPER_DDR) c.q = ddr_pre(A, B);
+  else if (shaper == MGN_SHAPER_DSR) c.dden = dsr_den(A, B);
+  return c;
+}
+__device__ __forceinline__ double pop_term(int shaper, double r, double A, double B, const PopPre& c,
+                                           double disc_k) {
+  double f = r;
+  if (shaper == MGN_SHAPER_DSR) f = dsr_one_den(r, A, B, c.dden);
+  else if (shaper == MGN_SHAPER_DDR) f = ddr_one_pre(r, A, B, c.q);
+  return disc_k * f;
+}
 
 // naive shapers (nstep_buffer.py:207-312), benchmark 0.  x**e and x**(1/e) as
 // numpy evaluates them on float64 arrays: exponents 2 and 0.5 take numpy's
@@ -1189,13 +1221,9 @@ __device__ __forceinline__ void nstep_column(const KParams& p, RingP ring, OutP 
       continue;
     }
     double acc = 0.0;
-    for (int k = 0; k < len; ++k) {
-      const double r = ring[(size_t)((head + k) % n) * D + d];
-      double f = r;
-      if (p.shaper == MGN_SHAPER_DSR) f = dsr_one(r, A, B);
-      else if (p.shaper == MGN_SHAPER_DDR) f = ddr_one(r, A, B);
-      acc += p.disc[k] * f;
-    }
+    const PopPre c = pop_pre(p.shaper, A, B);
+    for (int k = 0, idx = head; k < len; ++k, idx = (idx + 1 == n) ? 0 : idx + 1)
+      acc += pop_term(p.shaper, ring[(size_t)idx * D + d], A, B, c, p.disc[k]);
     double res = acc;
     if (sr) {
       res = clip1(acc / len);

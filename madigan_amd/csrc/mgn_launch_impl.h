@@ -32,7 +32,7 @@ void launch_duo(const StepArgs& a) {
   const int grid = (a.p.N + epb - 1) / epb;
   const bool nst = a.p.nstep > 1;
   // NST: the envs' n-step rings in dynamic LDS (duo_nst_lds_bytes)
-  const size_t lds = nst ? (size_t)epb * a.p.nstep * a.p.D * sizeof(double) : 0;
+  const size_t lds = nst ? (size_t)epb * a.p.nstep * (a.p.D + 1) * sizeof(double) : 0;
   auto go = [&](auto kern) {
     if (lds) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(DUO_BLOCK), lds, a.stream, a.p, a.out, a.in_kind,

@@ -168,6 +168,17 @@ struct GState {
   MGN_G uint64_t *ring_ts, *hist_ts;
 };
 
+// One-step shaping (DSR / DDR / PPC / naive, n = 1) runs on the ledger side,
+// right after the step's reward.  MGN_X_GEN_SHAPE moves it to the generator
+// side (the shaper state feeds only the shaped reward): measured slower at
+// C3 (2.79 -> 2.95 us per step at 256-step launches; the generator's store
+// phase then sets phase 2), kept as a diagnostic build.
+#ifdef MGN_X_GEN_SHAPE
+constexpr bool kGenShape = true;
+#else
+constexpr bool kGenShape = false;
+#endif
+
 // The step finish is split between the roles.  The ledger lanes evaluate it
 // (ledger_finish: Env.h:211-229 reward, Portfolio.cpp:150-155
 // ledgerNormedFull, offpolicy_q.py:152-164 agent reward, nstep_buffer.py
@@ -220,8 +231,9 @@ __device__ __forceinline__ void ledger_finish(DuoRec<S>& rc, const Lane<1>& s, c
     cos_term = p.cos_temp * (dot / (np_ * g.cos_qn));
   }
   double shaped_s = 0., rin_s = 0., shaped_v = 0.;
-  if constexpr (NST) {
-    // n > 1: the generator side adds the column value to the NStepBuffer
+  if constexpr (NST || kGenShape) {
+    // the generator side shapes (n = 1) or adds the column value to the
+    // NStepBuffer (n > 1)
     if (D == 1) rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
   } else if (D == 1) {
     rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
@@ -320,7 +332,12 @@ __device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s,
       if (om & O_OPT) ost(out.obs_port + ((size_t)k * p.N * (A + 1) + (size_t)env * (A + 1) + 1 + s.asset[0]), portA);
       if (D != 1) {
         if (om & O_AREW) ost(out.agent_reward + (i), sh.rAr[l]);
-        if (!NST && (om & O_SHP)) ost(out.shaped + (i), sh.rShv[l]);
+        if constexpr (!NST && kGenShape) {
+          const double v = shape(p.shaper, sh.rAr[l], ns.A, ns.B, p.eta, sh.rCos[el], p.sexp);
+          if (om & O_SHP) ost(out.shaped + (i), v);
+        } else if (!NST && (om & O_SHP)) {
+          ost(out.shaped + (i), sh.rShv[l]);
+        }
       }
     }
     if (om & O_OPR) duo_feats<S, RP>(s, p, ls, P, rp, out.obs_price + (oN + env) * (size_t)p.F, false);
@@ -334,7 +351,24 @@ __device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s,
       if (!NST && (om & O_NSH)) ost(out.n_shaped + (oN + env), (uint8_t)(1));
       if (D == 1) {
         if (om & O_AREW) ost(out.agent_reward + (oN + env), sh.rRin[el]);
-        if (!NST && (om & O_SHP)) ost(out.shaped + (oN + env), sh.rShaped[el]);
+        if (!NST && !kGenShape && (om & O_SHP)) ost(out.shaped + (oN + env), sh.rShaped[el]);
+      }
+    }
+    if constexpr (!NST && kGenShape) {
+      if (D == 1) {
+        // every lane of the env evaluates the env's shaper (same operands)
+        const double r = sh.rRin[el];
+        double v;
+        if (p.shaper == MGN_SHAPER_DDR) {  // shape() for DDR (nstep_buffer.py:128-162)
+          v = clip1((0.0 + 1.0 * ddr_one_pre(r, ns.A, ns.B, ddr_pre(ns.A, ns.B))) / 1);
+          double m = r < 0. ? r : 0.;
+          if (r != r) m = r;
+          ns.A += p.eta * (r - ns.A);
+          ns.B += p.eta * (m * m - ns.B);
+        } else {
+          v = shape(p.shaper, r, ns.A, ns.B, p.eta, sh.rCos[el], p.sexp);
+        }
+        if (ls == 0 && (om & O_SHP)) ost(out.shaped + (oN + env), v);
       }
     }
     if constexpr (NST) {
@@ -759,9 +793,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       s.tlen[0] = p.tlen[li];
       s.tfl[0] = p.tfl[li];
     }
-    if constexpr (NST) {
-      nst.len = p.nlen[envc];
-      nst.head = p.nhead[envc];
+    if constexpr (NST || kGenShape) {  // the generator side owns the shaper state
       if (p.D == 1) {
         nst.A = p.sA[envc];
         nst.B = p.sB[envc];
@@ -769,6 +801,10 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
         nst.A = p.sA[li];
         nst.B = p.sB[li];
       }
+    }
+    if constexpr (NST) {
+      nst.len = p.nlen[envc];
+      nst.head = p.nhead[envc];
       // the env's ring into LDS (every lane of the env copies a share)
       const int nD = p.nstep * p.D;
       for (int i = ls; i < nD; i += S) nst.ring[i] = p.nring[(size_t)envc * nD + i];
@@ -949,6 +985,8 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
         p.nlen[env] = nst.len;
         p.nhead[env] = nst.head;
       }
+    }
+    if constexpr (NST || kGenShape) {
       if (p.D == 1) {
         if (ls == 0) {
           p.sA[env] = nst.A;
@@ -1195,12 +1233,12 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
   }
   if (ls == 0) {
     p.cash[env] = cash;
-    if (!NST && D == 1) {  // n > 1: the generator side owns the shaper state
+    if (!(NST || kGenShape) && D == 1) {  // else the generator side owns the shaper state
       p.sA[env] = g.shA;
       p.sB[env] = g.shB;
     }
   }
-  if (!NST && D != 1 && s.valid[0]) {
+  if (!(NST || kGenShape) && D != 1 && s.valid[0]) {
     p.sA[(size_t)env * A + s.asset[0]] = g.shA;
     p.sB[(size_t)env * A + s.asset[0]] = g.shB;
   }

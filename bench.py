@@ -121,6 +121,8 @@ def bandwidth_probe(dev, nbytes: int = 1 << 30, reps: int = 10):
     return out.value
 
 
+SCHED_NAMES = {1: "single", 2: "duo", 3: "trio"}
+
 # MI355X: 256 CUs x 4 SIMDs; a wave64 VALU instruction occupies its SIMD for
 # at least 4 cycles (16 lanes per cycle; fp64 FMA at full rate, transcendental
 # and fp64 divide / sqrt steps longer); peak engine clock 2.4 GHz
@@ -285,6 +287,8 @@ def kernel_name(env, A: int) -> str:
     m = int(env.lib.mgn_get_layout(env.h))
     apad = 1 << max(0, (A - 1).bit_length())
     rq1 = "true" if env.cfg.required_margin == 1.0 else "false"
+    if int(env.lib.mgn_get_schedule(env.h)) == L.SCHED_TRIO:
+        return f"mgn::k_step_trio<{apad}, {rq1}, true>"
     if int(env.lib.mgn_get_schedule(env.h)) == L.SCHED_DUO:
         # <S, RQ1, ABL, DISC, RP, NST>: the bench launches discrete actions
         rp = "true" if env.spec.replay else "false"
@@ -307,7 +311,7 @@ def main():
     ap.add_argument("--n-envs", type=int, default=8192, help="envs per GPU")
     ap.add_argument("--assets", type=int, default=8)
     ap.add_argument("--layout", type=int, default=0, help="assets per lane (0 = auto)")
-    ap.add_argument("--schedule", default="auto", choices=["auto", "single", "duo"],
+    ap.add_argument("--schedule", default="auto", choices=["auto", "single", "duo", "trio"],
                     help="C3 diagnostics: pin the step kernel (results are bit-identical)")
     ap.add_argument("--nstep", type=int, default=1,
                     help="C3 diagnostics: n-step aggregation (nstep_return), not the headline")
@@ -353,8 +357,8 @@ def main():
         env.lib.mgn_set_layout(env.h, args.layout)
     if args.schedule != "auto":
         from madigan_amd import _lib as L
-        L.check(env.lib.mgn_set_schedule(env.h, L.SCHED_DUO if args.schedule == "duo" else L.SCHED_SINGLE),
-                env.h)
+        L.check(env.lib.mgn_set_schedule(env.h, {"single": L.SCHED_SINGLE, "duo": L.SCHED_DUO,
+                                                  "trio": L.SCHED_TRIO}[args.schedule]), env.h)
     import ctypes as C
     from madigan_amd import _lib as L
     lib, h = env.lib, env.h
@@ -487,7 +491,7 @@ def main():
                        "n_envs_per_gpu": N, "n_assets": A, "window": 0,
                        "steps_per_launch": steps_per_launch,
                        "assets_per_lane": int(lib.mgn_get_layout(h)),
-                       "schedule": "duo" if int(lib.mgn_get_schedule(h)) == 2 else "single",
+                       "schedule": SCHED_NAMES[int(lib.mgn_get_schedule(h))],
                        "parallelism": f"env-sharded x{world} (no per-step collective)"
                                       + (f", {args.dist_backend}" if world > 1 else "")},
             "roofline": roof,
@@ -639,7 +643,7 @@ def windowed(args, world, rank, dev):
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": desc, "n_envs_per_gpu": N, "n_assets": A, "n_feats": env.F,
                        "window": W, "steps_per_launch": Kf,
-                       "schedule": "duo" if int(lib.mgn_get_schedule(h)) == 2 else "single",
+                       "schedule": SCHED_NAMES[int(lib.mgn_get_schedule(h))],
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,

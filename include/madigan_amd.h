@@ -335,10 +335,13 @@ int mgn_set_layout(mgn_env *env, int32_t assets_per_lane);
 int mgn_get_layout(const mgn_env *env);
 /* Step schedule: MGN_SCHED_SINGLE = k_step (every lane runs the whole Env
  * step for its assets); MGN_SCHED_DUO = k_step_duo (each asset also has a lane
- * in a generator wave that shares the SIMD; 2..8 assets, nstep 1, no replay);
- * MGN_SCHED_AUTO (default) = DUO where eligible and the layout is one asset per
- * lane.  Results are bit-identical; only speed changes. */
-enum { MGN_SCHED_AUTO = 0, MGN_SCHED_SINGLE = 1, MGN_SCHED_DUO = 2 };
+ * in a generator wave that shares the SIMD; 2..16 assets, generator sources
+ * or a replay tape, n-step rings that fit LDS); MGN_SCHED_TRIO = k_step_trio
+ * (generator, ledger and finish waves pipelined one step apart, `done`
+ * speculated; 2..8 assets, generator sources, nstep 1, no window);
+ * MGN_SCHED_AUTO (default) = TRIO, else DUO where eligible and the layout is
+ * one asset per lane.  Results are bit-identical; only speed changes. */
+enum { MGN_SCHED_AUTO = 0, MGN_SCHED_SINGLE = 1, MGN_SCHED_DUO = 2, MGN_SCHED_TRIO = 3 };
 int mgn_set_schedule(mgn_env *env, int32_t schedule);
 int mgn_get_schedule(const mgn_env *env);
 /* DIAGNOSTIC ONLY (timing ablations, outputs become wrong): bit 0 skips the

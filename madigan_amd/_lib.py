@@ -30,7 +30,7 @@ REWARD_ENV_LOG, REWARD_AGENT_SUM, REWARD_AGENT_PER_ASSET = range(3)
  NORM_LOG_STANDARD_NORMAL) = range(6)
 RING_PLAIN, RING_PAIR_RATIO = range(2)
 STEP_NONE, STEP_UNITS, STEP_SINGLE = range(3)
-SCHED_AUTO, SCHED_SINGLE, SCHED_DUO = range(3)
+SCHED_AUTO, SCHED_SINGLE, SCHED_DUO, SCHED_TRIO = range(4)
 
 
 class MadiganError(RuntimeError):

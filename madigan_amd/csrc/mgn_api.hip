@@ -67,6 +67,7 @@ struct mgn_env {
   int sched = MGN_SCHED_AUTO;  // requested step schedule
   bool layout_auto = true;     // assets per lane chosen by auto_layout
   bool duo = false;            // the two-role kernel runs the steps
+  bool trio = false;           // the three-role pipelined kernel runs the steps
   // launch history (mgn_rollout_hist): grown on demand, owned by the handle;
   // two buffers when the gathers run on a window stream (one is written by
   // the next step launch while the other is gathered)
@@ -303,6 +304,7 @@ void launch(void (*const* fns)(int, const Arg&), int apad, int m, const Arg& a) 
 }
 void (*const kStep[7])(int, const mgn::StepArgs&) = {mgn::launch_step_a1, mgn::launch_step_a2, mgn::launch_step_a4, mgn::launch_step_a8, mgn::launch_step_a16, mgn::launch_step_a32, mgn::launch_step_a64};
 void (*const kDuo[7])(const mgn::StepArgs&) = {mgn::launch_duo_a1, mgn::launch_duo_a2, mgn::launch_duo_a4, mgn::launch_duo_a8, mgn::launch_duo_a16, mgn::launch_duo_a32, mgn::launch_duo_a64};
+void (*const kTrio[7])(const mgn::StepArgs&) = {mgn::launch_trio_a1, mgn::launch_trio_a2, mgn::launch_trio_a4, mgn::launch_trio_a8, mgn::launch_trio_a16, mgn::launch_trio_a32, mgn::launch_trio_a64};
 void (*const kInit[7])(int, const mgn::InitArgs&) = {mgn::launch_init_a1, mgn::launch_init_a2, mgn::launch_init_a4, mgn::launch_init_a8, mgn::launch_init_a16, mgn::launch_init_a32, mgn::launch_init_a64};
 void (*const kVal[7])(int, const mgn::ValArgs&) = {mgn::launch_val_a1, mgn::launch_val_a2, mgn::launch_val_a4, mgn::launch_val_a8, mgn::launch_val_a16, mgn::launch_val_a32, mgn::launch_val_a64};
 
@@ -327,12 +329,27 @@ bool duo_eligible(const mgn_env* e) {
   }
   return true;
 }
+// the three-role kernel: 2..8 assets, generator sources, one-step rewards, no
+// window (its speculative steps would need the window rows rolled back)
+bool trio_eligible(const mgn_env* e) {
+  return e->apad >= 2 && e->apad <= 8 && !e->cfg.aux && !e->replay && e->cfg.nstep == 1 && e->W == 0;
+}
 // automatic: where the single-role kernel would run one lane per asset (small
-// batches: one wave per SIMD), give every asset a second lane in a partner wave
+// batches: one wave per SIMD), give every asset a second (and a third) lane
+// in partner waves
 void choose_sched(mgn_env* e) {
-  if (e->sched == MGN_SCHED_SINGLE) e->duo = false;
-  else if (e->sched == MGN_SCHED_DUO) e->duo = duo_eligible(e);
-  else e->duo = duo_eligible(e) && e->m == 1;
+  e->trio = false;
+  if (e->sched == MGN_SCHED_SINGLE) {
+    e->duo = false;
+  } else if (e->sched == MGN_SCHED_DUO) {
+    e->duo = duo_eligible(e);
+  } else if (e->sched == MGN_SCHED_TRIO) {
+    e->trio = trio_eligible(e);
+    e->duo = !e->trio && duo_eligible(e);
+  } else {
+    e->trio = trio_eligible(e) && e->m == 1;
+    e->duo = !e->trio && duo_eligible(e) && e->m == 1;
+  }
 }
 int choose_m(int n_envs, int apad);
 // automatic layout: the two-role kernel wherever it is eligible (at C3 it runs
@@ -341,7 +358,7 @@ int choose_m(int n_envs, int apad);
 // lanes per env as keep >= 2 waves per SIMD
 void auto_layout(mgn_env* e) {
   if (e->layout_auto)
-    e->m = (e->sched != MGN_SCHED_SINGLE && duo_eligible(e)) ? 1 : choose_m(e->N, e->apad);
+    e->m = (e->sched != MGN_SCHED_SINGLE && (duo_eligible(e) || trio_eligible(e))) ? 1 : choose_m(e->N, e->apad);
   choose_sched(e);
 }
 
@@ -358,6 +375,11 @@ int choose_m(int n_envs, int apad) {
 void launch_step(const mgn_env* e, const mgn_traj& out, int in_kind, const double* units,
                  const int32_t* aidx, const int8_t* act, int K) {
   mgn::StepArgs a{kparams(e), out, in_kind, units, aidx, act, K, e->stream};
+  if (e->trio) {
+    const int idx = e->apad <= 2 ? 1 : e->apad <= 4 ? 2 : 3;
+    kTrio[idx](a);
+    return;
+  }
   if (e->duo) {
     const int idx = e->apad <= 2 ? 1 : e->apad <= 4 ? 2 : e->apad <= 8 ? 3 : 4;
     kDuo[idx](a);
@@ -934,17 +956,21 @@ int mgn_set_layout(mgn_env* e, int32_t assets_per_lane) {
 
 int mgn_set_schedule(mgn_env* e, int32_t schedule) {
   if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
-  if (schedule < MGN_SCHED_AUTO || schedule > MGN_SCHED_DUO)
-    return fail(e, MGN_ERR_CONFIG, "schedule must be MGN_SCHED_AUTO, _SINGLE or _DUO");
+  if (schedule < MGN_SCHED_AUTO || schedule > MGN_SCHED_TRIO)
+    return fail(e, MGN_ERR_CONFIG, "schedule must be MGN_SCHED_AUTO, _SINGLE, _DUO or _TRIO");
   if (schedule == MGN_SCHED_DUO && !duo_eligible(e))
-    return fail(e, MGN_ERR_CONFIG, "the two-role kernel needs 2..8 assets, nstep 1, no replay tape");
+    return fail(e, MGN_ERR_CONFIG,
+                "the two-role kernel needs 2..16 assets, no multi-component source, n-step rings within LDS");
+  if (schedule == MGN_SCHED_TRIO && !trio_eligible(e))
+    return fail(e, MGN_ERR_CONFIG,
+                "the three-role kernel needs 2..8 assets, generator sources, nstep 1, no window");
   e->sched = schedule;
   auto_layout(e);
   return MGN_OK;
 }
 
 int mgn_get_schedule(const mgn_env* e) {
-  return e ? (e->duo ? MGN_SCHED_DUO : MGN_SCHED_SINGLE) : 0;
+  return e ? (e->trio ? MGN_SCHED_TRIO : e->duo ? MGN_SCHED_DUO : MGN_SCHED_SINGLE) : 0;
 }
 
 int mgn_get_layout(const mgn_env* e) { return e ? e->m : 0; }

@@ -534,7 +534,7 @@ __device__ __forceinline__ Q4 tree4(const EnvRecs<S>& er, uint32_t post, Q4 (&si
   }
 }
 
-template <int S, bool RQ1>
+template <int S, bool RQ1, bool LOWREG>
 __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRecs<S>& er,
                                             double& cash, const double (&uc)[1], double (&tp)[1],
                                             double (&tu)[1], double (&tc)[1], int (&rk)[1], int ls,
@@ -555,9 +555,10 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
   int go = 0, mc = 0, insuff = 0;
   double cend = cash0;
   // S <= 8: the leaves of the last (consistent) pass in registers (measured
-  // ~1 % faster at S = 8 than the streaming tree); S = 16: the streaming tree,
-  // its rightmost-path left children kept
-  constexpr bool STREAM = S >= 16;
+  // ~1 % faster at S = 8 than the streaming tree); S = 16 or LOWREG (the
+  // three-role kernel's 168-VGPR budget): the streaming tree, its
+  // rightmost-path left children kept
+  constexpr bool STREAM = LOWREG || S >= 16;
   Q4 sib[6];
   double lv[4][STREAM ? 1 : S];
   for (int it = 0; it <= S; ++it) {
@@ -1101,7 +1102,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       prevVal = s.L[0] * s.P[0];
       MGN_T(Ta);
       if (in_kind != IN_NONE && !(ABL && (p.ablate & 1))) {
-        broker_spec<S, RQ1>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, sa, any_mc);
+        broker_spec<S, RQ1, false>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, sa, any_mc);
         mcall = margin_call(sa, cash, p.mainM) ? 1 : 0;  // Broker.cpp:156-157
       }
       MGN_T(Tb);

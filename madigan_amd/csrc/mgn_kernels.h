@@ -1254,7 +1254,7 @@ __device__ __forceinline__ void nstep_column(const KParams& p, RingP ring, OutP 
 // RQ1: required_margin == 1.0, where x / required_margin == x exactly and the
 // divisions are skipped.  NST: n-step aggregation (nstep > 1) compiled in.
 // speculative Broker resolution for one asset per lane (defined in mgn_duo.h)
-template <int S, bool RQ1>
+template <int S, bool RQ1, bool LOWREG>
 __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRecs<S>& er,
                                             double& cash, const double (&uc)[1], double (&tp)[1],
                                             double (&tu)[1], double (&tc)[1], int (&rk)[1], int ls,
@@ -1428,7 +1428,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
             if constexpr (M == 1) {
               // one asset per lane: the speculative resolution of the two-role
               // kernel (mgn_duo.h) -- one pass when no order is refused
-              broker_spec<S, RQ1>(s, p, recs[tid / S], cash, uc, tp, tu, tc, rk, ls, sa, any_mc);
+              broker_spec<S, RQ1, false>(s, p, recs[tid / S], cash, uc, tp, tu, tc, rk, ls, sa, any_mc);
             } else {
               broker_x<M, S, RQ1>(s, p, recs[tid / S], cash, s0, uc, tp, tu, tc, rk, ls, sa, any_mc);
             }

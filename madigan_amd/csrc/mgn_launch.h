@@ -37,6 +37,7 @@ constexpr int min_m(int apad) { return apad > 16 ? apad / 16 : 1; }
 
 #define MGN_DECLARE_APAD(A)                          \
   void launch_duo_a##A(const StepArgs& a);           \
+  void launch_trio_a##A(const StepArgs& a);          \
   void launch_step_a##A(int m, const StepArgs& a);   \
   void launch_init_a##A(int m, const InitArgs& a);   \
   void launch_val_a##A(int m, const ValArgs& a);

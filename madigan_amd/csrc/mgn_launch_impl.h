@@ -3,6 +3,7 @@
 #pragma once
 
 #include "mgn_launch.h"
+#include "mgn_trio.h"
 
 namespace mgn {
 
@@ -67,6 +68,25 @@ void launch_duo(const StepArgs& a) {
   }
 }
 
+// three-role pipelined step kernel (mgn_trio.h): S = APAD lanes per env per role
+template <int S>
+void launch_trio(const StepArgs& a) {
+  constexpr int epb = TRIO_W / S;
+  const int grid = (a.p.N + epb - 1) / epb;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(TRIO_BLOCK), 0, a.stream, a.p, a.out, a.in_kind,
+                       a.units, a.aidx, a.act, a.K);
+  };
+  const bool disc = a.in_kind == IN_DISCRETE;
+  if (disc) {
+    if (a.p.reqm_one) go(k_step_trio<S, true, true>);
+    else go(k_step_trio<S, false, true>);
+  } else {
+    if (a.p.reqm_one) go(k_step_trio<S, true, false>);
+    else go(k_step_trio<S, false, false>);
+  }
+}
+
 template <int M, int S>
 struct InitL {
   static void run(const InitArgs& a) {
@@ -106,6 +126,9 @@ void dispatch_m(int m, const Arg& a) {
   namespace mgn {                                                                            \
   void launch_duo_a##A(const StepArgs& a) {                                                  \
     if constexpr (A >= 2 && A <= 16) launch_duo<A>(a);                                       \
+  }                                                                                          \
+  void launch_trio_a##A(const StepArgs& a) {                                                 \
+    if constexpr (A >= 2 && A <= 8) launch_trio<A>(a);                                       \
   }                                                                                          \
   void launch_step_a##A(int m, const StepArgs& a) { dispatch_m<StepL, A>(m, a); }            \
   void launch_init_a##A(int m, const InitArgs& a) { dispatch_m<InitL, A>(m, a); }            \

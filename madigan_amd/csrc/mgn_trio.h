@@ -1,0 +1,589 @@
+// mgn_trio.h -- the fused step kernel with three wave roles, pipelined.
+//
+// k_step_duo splits an Env step between a generator role and a ledger role
+// but keeps the step's own order: orders, then the tick, then the post-tick
+// sums, done and reward -- two barriers per step, and each role idles for
+// part of both phases.  The step's dependencies allow a pipeline instead:
+//   * the Broker orders of step k (Broker.cpp:124-178) need the ledger after
+//     step k-1, the prices of tick k-1 and whether step k-1 ended the
+//     episode (Env::reset before step k, Env.h:181-187);
+//   * the tick of step k (DataSource::getData) needs the source state after
+//     tick k-1 (and the same reset);
+//   * step k-1's post-tick sums, equity, reward, done, ledgerNormedFull,
+//     agent reward, shaper and episode statistics (Env.h:211-223) need the
+//     ledger after the orders of step k-1 and the prices of tick k-1, and
+//     feed nothing but `done`.
+// So a 768-thread workgroup holds 32 envs three times (waves w, w + 4, w + 8
+// share a SIMD): in iteration j the ledger waves (L) run step j's orders, the
+// generator waves (G) run step j's tick, and the finish waves (F) evaluate
+// step j-1 -- one barrier per iteration, records double-buffered by
+// iteration parity.  `done` of step j-1 is known only at the end of
+// iteration j, after L and G have speculatively run step j on the assumption
+// that the episode goes on.  When F finds done (auto-reset), iteration j+1
+// rolls step j back: L resets the ledger (a fresh Broker), G restores the
+// source state saved before tick j, applies the source reset and ticks
+// (Env::reset's getData), and step j is run again from the fresh episode in
+// iteration j+2 at the same step index, overwriting the outputs the
+// speculative run stored.  Episodes end rarely, so almost every speculation
+// stands.  Every value is the same expression of the same operands as in
+// k_step, so every output is bit-identical to k_step / k_step_duo (and the
+// oracle).
+// Stores: L stores the BrokerResponse arrays of its step, G the tick's
+// State.price and timestamp, F everything that needs equity.
+// Scope: M = 1, APAD = S in {2, 4, 8}, n-step 1, no window, generator
+// sources (k_step_duo / k_step run the rest).
+#pragma once
+
+#include "mgn_duo.h"
+
+namespace mgn {
+
+constexpr int TRIO_BLOCK = 768;
+constexpr int TRIO_W = 256;  // lanes per role
+
+// which role stores what, and the roles' issue priorities (tuning switches;
+// the defaults are the measured best)
+#ifndef MGN_TRIO_LST
+#define MGN_TRIO_LST 0  // L stores the BrokerResponse arrays (else F)
+#endif
+#ifndef MGN_TRIO_GST
+#define MGN_TRIO_GST 0  // G stores State.price and timestamp (else F)
+#endif
+#ifndef MGN_TRIO_PG
+#define MGN_TRIO_PG 0
+#endif
+#ifndef MGN_TRIO_PL
+#define MGN_TRIO_PL 2
+#endif
+#ifndef MGN_TRIO_PF
+#define MGN_TRIO_PF 1
+#endif
+
+enum { TR_STEP = 1, TR_ANYMC = 2, TR_MCALL = 4 };
+
+template <int S>
+struct TrioShared {
+  static constexpr int EPB = TRIO_W / S;
+  // prices after the iteration's tick (G -> L, F)
+  double price[2][TRIO_W];
+  // the orders L ran (L -> F): ledger after the orders, responses, L*P before
+  double rL[2][TRIO_W], rTp[2][TRIO_W], rTu[2][TRIO_W], rTc[2][TRIO_W], rPv[2][TRIO_W];
+  int32_t rRk[2][TRIO_W];
+  // per env: cash and the three price-independent sums after the orders,
+  // equity before the step, the step index and TR_* flags
+  double rCash[2][EPB], rMl[2][EPB], rSh[2][EPB], rB[2][EPB], rPrevEq[2][EPB];
+  int32_t rK[2][EPB], rFlags[2][EPB];
+  // F -> G, L: the step F evaluated ended its episode and the env resets
+  int32_t reset[2][EPB];
+  uint64_t ts[2][EPB];  // timestamp after the tick (G -> F when F stores it)
+  int32_t more[3];
+};
+
+template <int S, bool RQ1, bool DISC>
+__global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj out, int in_kind_rt,
+                                                          const double* __restrict__ units_in,
+                                                          const int32_t* __restrict__ aidx_in,
+                                                          const int8_t* __restrict__ act_in, int K) {
+  warm_kernargs<(int)(sizeof(KParams) + sizeof(mgn_traj) + 48)>();
+  const int in_kind = DISC ? IN_DISCRETE : in_kind_rt;
+  constexpr int M = 1;
+  constexpr int EPB = TRIO_W / S;
+  __shared__ TrioShared<S> sh;
+  __shared__ EnvRecs<S> recs[EPB];
+  __shared__ mgn_asset_source s_src[S];
+  __shared__ double s_tgt[MGN_MAX_ASSETS + 1];
+  const int role = threadIdx.x / TRIO_W;  // 0 generator, 1 ledger, 2 finish
+  const int l = threadIdx.x % TRIO_W;
+  const int el = l / S;
+  const int ls = l % S;
+  const int env = blockIdx.x * EPB + el;
+  const bool live = env < p.N;
+  const int envc = live ? env : 0;
+  const int A = p.A;
+  Lane<M> s;
+  s.asset[0] = ls;
+  s.valid[0] = live && ls < A;
+  s.rcur = 0;
+  s.row = 0;
+  s.pf_ok = false;
+  s.fcol = -1;
+  const size_t li = (size_t)envc * A + (s.valid[0] ? ls : 0);
+  s.P[0] = s.valid[0] ? p.P[li] : 0.;
+  s.L[0] = s.mep[0] = s.Bm[0] = s.sx[0] = s.oum[0] = s.dy[0] = 0.;
+  s.tlen[0] = 0;
+  s.tfl[0] = 0;
+  // role state, loaded before the parameter staging (one round trip)
+  uint64_t ts = 0;                             // G
+  double cash = 0.;                            // L
+  int act_cur = 0;                             // L
+  const MGN_G int8_t* act_lane = vptr(act_in) + li;
+  double ep_ret = 0., ep_len = 0., n_done = 0.;  // F
+  double shA = 0., shB = 0.;                     // F
+  if (role == 0) {
+    if (s.valid[0]) {
+      s.sx[0] = p.sx[li];
+      s.oum[0] = p.oum[li];
+      s.dy[0] = p.dy[li];
+      s.tlen[0] = p.tlen[li];
+      s.tfl[0] = p.tfl[li];
+    }
+    ts = p.ts[envc];
+  } else if (role == 1) {
+    if (s.valid[0]) {
+      s.L[0] = p.L[li];
+      s.mep[0] = p.mep[li];
+      s.Bm[0] = p.Bm[li];
+    }
+    cash = p.cash[envc];
+    if (in_kind == IN_DISCRETE && K > 0) act_cur = act_lane[0];
+  } else {
+    ep_ret = p.ep[(size_t)envc * 2];
+    ep_len = p.ep[(size_t)envc * 2 + 1];
+    n_done = p.epstats[(size_t)envc * 4 + 3];
+    if (p.D == 1) {
+      shA = p.sA[envc];
+      shB = p.sB[envc];
+    } else if (s.valid[0]) {
+      shA = p.sA[li];
+      shB = p.sB[li];
+    }
+  }
+  {
+    const double* g = reinterpret_cast<const double*>(p.src);
+    double* d = reinterpret_cast<double*>(s_src);
+    const int n = p.A * (int)(sizeof(mgn_asset_source) / sizeof(double));
+    for (int i = threadIdx.x; i < n; i += TRIO_BLOCK) d[i] = g[i];
+    if (p.target)
+      for (int i = threadIdx.x; i <= p.A; i += TRIO_BLOCK) s_tgt[i] = p.target[i];
+    p.src = s_src;
+    if (p.target) p.target = s_tgt;
+  }
+  if (role == 1 && ls == 0) {  // no step before iteration 0, no reset pending
+    sh.rFlags[1][el] = 0;
+    sh.reset[1][el] = 0;
+  }
+  if (threadIdx.x == 0) {
+    sh.more[0] = 0;
+    sh.more[1] = 0;
+    sh.more[2] = 0;
+  }
+#ifdef MGN_STAMPS
+  if (threadIdx.x < 8) s_duo_sub[threadIdx.x] = 0;
+#endif
+  __syncthreads();
+  s.kind[0] = s.valid[0] ? s_src[ls].kind : -1;
+
+  if (role == 0) {
+    // ---------------- generator waves: tick of step j, State.price / timestamp
+    const uint32_t om = traj_mask(out);
+    const GTraj ov = traj_vgpr(out);
+    p.seed = in_vgpr(p.seed);
+    p.env_offset = in_vgpr(p.env_offset);
+    drain_vmem();
+    int k = 0;
+    // the source state before the last speculative tick (restored when F
+    // finds that the previous step ended the episode)
+    double svP = 0., svSx = 0., svOum = 0., svDy = 0.;
+    int32_t svTlen = 0;
+    uint8_t svTfl = 0;
+    uint64_t svTs = 0;
+    __builtin_amdgcn_s_setprio(MGN_TRIO_PG);
+#ifdef MGN_STAMPS
+    unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0;
+    int jn = 0;
+#endif
+    for (int j = 0;; ++j) {
+      const int cur = j & 1, prv = cur ^ 1;
+      MGN_T(T0);
+      if (threadIdx.x == 0) sh.more[(j + 1) % 3] = 0;
+      if (live) {
+        const bool rst = sh.reset[prv][el] != 0;
+        const bool prev_step = (sh.rFlags[prv][el] & TR_STEP) != 0;
+        if (rst) {
+          if (prev_step) {  // roll the speculative tick back
+            s.P[0] = svP;
+            s.sx[0] = svSx;
+            s.oum[0] = svOum;
+            s.dy[0] = svDy;
+            s.tlen[0] = svTlen;
+            s.tfl[0] = svTfl;
+            ts = svTs;
+            k -= 1;
+          }
+          // Env::reset -> dataSource->reset + getData (Env.h:181-187)
+          src_reset<M, false>(s, p, env, ts);
+          gen_tick<M, false, false>(s, p, env, ts);
+          ts = ts + 1;
+        } else if (k < K) {
+          svP = s.P[0];
+          svSx = s.sx[0];
+          svOum = s.oum[0];
+          svDy = s.dy[0];
+          svTlen = s.tlen[0];
+          svTfl = s.tfl[0];
+          svTs = ts;
+          gen_tick<M, false, false>(s, p, env, ts);
+          ts = ts + 1;
+          // State.price and timestamp of step k (overwritten if rolled back)
+          if (MGN_TRIO_GST) {
+            const size_t oN = (size_t)k * p.N;
+            if (s.valid[0] && (om & O_OPR)) ost(ov.obs_price + ((oN + env) * (size_t)p.F + s.asset[0]), s.P[0]);
+            if (ls == 0 && (om & O_TS)) ost(ov.timestamp + (oN + env), (uint64_t)ts);
+          }
+          k += 1;
+        }
+      }
+      sh.price[cur][l] = s.P[0];
+      if (!MGN_TRIO_GST && ls == 0) sh.ts[cur][el] = ts;
+      MGN_T(T1);
+      __syncthreads();
+      MGN_T(T2);
+#ifdef MGN_STAMPS
+      acc0 += T1 - T0;
+      acc1 += T2 - T1;
+      jn = j;
+#endif
+      if (!__builtin_amdgcn_readfirstlane(sh.more[j % 3])) break;
+    }
+#ifdef MGN_STAMPS
+    if (threadIdx.x == 0) {
+      atomicAdd(&g_duo_stamps[0], acc0);
+      atomicAdd(&g_duo_stamps[1], acc1);
+      atomicAdd(&g_duo_stamps[8], (unsigned long long)(jn + 1));
+      atomicAdd(&g_duo_stamps[10], 1ull);
+    }
+#endif
+    if (!live) return;
+    if (s.valid[0]) {
+      const size_t i = (size_t)env * A + s.asset[0];
+      p.P[i] = s.P[0];
+      p.sx[i] = s.sx[0];
+      p.oum[i] = s.oum[0];
+      p.dy[i] = s.dy[0];
+      p.tlen[i] = s.tlen[0];
+      p.tfl[i] = s.tfl[0];
+    }
+    if (ls == 0) p.ts[env] = ts;
+    return;
+  }
+
+  if (role == 1) {
+    // ---------------- ledger waves: Broker orders of step j
+    const uint32_t om = traj_mask(out);
+    const GTraj ov = traj_vgpr(out);
+    const MGN_G double* gunits = vptr(units_in);
+    const MGN_G int32_t* gaidx = vptr(aidx_in);
+    p.init_cash = in_vgpr(p.init_cash);
+    p.mainM = in_vgpr(p.mainM);
+    p.unit_size = in_vgpr(p.unit_size);
+    const size_t act_step = (size_t)p.N * A;
+    // sums of the ledger (canonical trees): ml, sh, b change only with the
+    // orders, lp with the prices; `fresh` = recompute all four (start, reset)
+    Sums sa = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
+    drain_vmem();
+    int k = 0;
+    __builtin_amdgcn_s_setprio(MGN_TRIO_PL);  // the orders are the critical path
+#ifdef MGN_STAMPS
+    unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0;
+#endif
+    for (int j = 0;; ++j) {
+      const int cur = j & 1, prv = cur ^ 1;
+      MGN_T(T0);
+      const bool rst = live && sh.reset[prv][el] != 0;
+      const bool prev_step = (sh.rFlags[prv][el] & TR_STEP) != 0;
+      // prices of the last tick (the step's pre-tick prices; iteration 0:
+      // the handle's current prices)
+      if (j > 0 && live && s.valid[0]) s.P[0] = sh.price[prv][l];
+      if (rst) {
+        // the episode ended at the step F evaluated: the speculative step of
+        // iteration j-1 is void; a fresh Broker (Env.h:181-187) waits for the
+        // reset tick's prices
+        if (prev_step) k -= 1;
+        s.L[0] = 0.;
+        s.mep[0] = 0.;
+        s.Bm[0] = 0.;
+        cash = p.init_cash;
+      }
+      const bool stepping = live && !rst && k < K;
+      const int act_now = act_cur;
+      if (in_kind == IN_DISCRETE && K > 0) {
+        // the action of the next step this lane runs (k + 1 if this one
+        // steps; a rollback re-reads step k's, clamped in range)
+        const int kn = k + (stepping ? 1 : 0);
+        act_cur = act_lane[(size_t)(kn < K ? kn : K - 1) * act_step];
+      }
+      int flags = 0;
+      if (stepping) {
+        const bool after_reset = prev_step ? false : true;
+        Sums s0;
+        if (after_reset && j > 0) {
+          s0 = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);  // after a reset tick
+        } else {
+          double tlp[M];
+          tlp[0] = s.L[0] * s.P[0];
+          s0 = sa;
+          s0.lp = canon<M, S>(tlp);
+          if (j == 0) s0 = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
+        }
+        const double prevEq = (cash + s0.lp) - s0.b;  // Env.h:208
+        double uc[M], tp[M], tu[M], tc[M];
+        int rk[M];
+        tp[0] = 0.;
+        tu[0] = 0.;
+        tc[0] = 0.;
+        rk[0] = MGN_GREEN;
+        uc[0] = 0.;
+        const size_t oN = (size_t)k * p.N, oNA = (size_t)k * p.N * A;
+        if (in_kind == IN_DISCRETE) {  // dqn.py:160-179
+          const double bp = (cash + s0.sh) + (s0.lp - s0.ml);
+          const double avM = RQ1 ? bp : bp / p.reqM;
+          const int half = p.atoms / 2;
+          if (s.valid[0]) {
+            const double u = p.unit_size * avM / s.P[0];
+            uc[0] = (double)(act_now - half) * u;
+            if (act_now == 0) uc[0] = (s.L[0] != 0) ? -s.L[0] : 0.;
+          }
+        } else if (in_kind == IN_UNITS) {
+          uc[0] = s.valid[0] ? gunits[oNA + (size_t)env * A + s.asset[0]] : 0.;
+        } else if (in_kind == IN_SINGLE) {
+          const int ai = gaidx[env];
+          const double u = gunits[oN + env];
+          uc[0] = (s.valid[0] && s.asset[0] == ai) ? u : 0.;
+        }
+        const double prevVal = s.L[0] * s.P[0];
+        Sums after = s0;
+        int any_mc = 0, mcall = 0;
+        if (in_kind != IN_NONE) {
+          broker_spec<S, RQ1, true>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, after, any_mc);
+          mcall = margin_call(after, cash, p.mainM) ? 1 : 0;  // Broker.cpp:156-157
+        }
+        sa = after;
+        // BrokerResponse of step k (overwritten if rolled back)
+        if (MGN_TRIO_LST && s.valid[0]) {
+          const size_t i = oNA + (size_t)env * A + s.asset[0];
+          if (om & O_TP) ost(ov.tprice + i, tp[0]);
+          if (om & O_TU) ost(ov.tunits + i, tu[0]);
+          if (om & O_TC) ost(ov.tcost + i, tc[0]);
+          if (om & O_RISK) ost(ov.risk + i, (uint8_t)rk[0]);
+        }
+        sh.rL[cur][l] = s.L[0];
+        sh.rTp[cur][l] = tp[0];
+        sh.rTu[cur][l] = tu[0];
+        sh.rTc[cur][l] = tc[0];
+        sh.rPv[cur][l] = prevVal;
+        sh.rRk[cur][l] = rk[0];
+        if (ls == 0) {
+          sh.rCash[cur][el] = cash;
+          sh.rMl[cur][el] = after.ml;
+          sh.rSh[cur][el] = after.sh;
+          sh.rB[cur][el] = after.b;
+          sh.rPrevEq[cur][el] = prevEq;
+          sh.rK[cur][el] = k;
+        }
+        flags = TR_STEP | (any_mc ? TR_ANYMC : 0) | (mcall ? TR_MCALL : 0);
+        k += 1;
+      }
+      if (ls == 0) sh.rFlags[cur][el] = flags;
+      // another iteration: F evaluates this step, or steps remain
+      if (live && (stepping || rst || k < K)) sh.more[j % 3] = 1;
+      MGN_T(T1);
+      __syncthreads();
+      MGN_T(T2);
+#ifdef MGN_STAMPS
+      acc0 += T1 - T0;
+      acc1 += T2 - T1;
+#endif
+      if (!__builtin_amdgcn_readfirstlane(sh.more[j % 3])) break;
+    }
+#ifdef MGN_STAMPS
+    if (l == 0) {
+      atomicAdd(&g_duo_stamps[4], acc0);
+      atomicAdd(&g_duo_stamps[5], acc1);
+      for (int i = 0; i < 3; ++i) atomicAdd(&g_duo_stamps[13 + i], s_duo_sub[i]);
+    }
+#endif
+    if (!live) return;
+    if (s.valid[0]) {
+      const size_t i = (size_t)env * A + s.asset[0];
+      p.L[i] = s.L[0];
+      p.mep[i] = s.mep[0];
+      p.Bm[i] = s.Bm[0];
+    }
+    if (ls == 0) p.cash[env] = cash;
+    return;
+  }
+
+  // ---------------- finish waves: step j-1's reward, done and outputs
+  const uint32_t om = traj_mask(out);
+  const GTraj ov = traj_vgpr(out);
+  GState gs;
+  gs.epstats = vptr(p.epstats);
+  p.init_cash = in_vgpr(p.init_cash);
+  p.mainM = in_vgpr(p.mainM);
+  p.eta = in_vgpr(p.eta);
+  p.cos_temp = in_vgpr(p.cos_temp);
+  const int D = p.D;
+  LedOut g;
+  g.shA = shA;
+  g.shB = shB;
+  g.cos_qn = 0.;
+  if (p.shaper == MGN_SHAPER_PPC) {
+    double qq[M];
+    const double q = s.valid[0] ? s_tgt[1 + s.asset[0]] : 0.;
+    qq[0] = q * q;
+    g.cos_qn = sqrt(s_tgt[0] * s_tgt[0] + canon<M, S>(qq));
+  }
+  const bool need_ar = (p.reward_mode != MGN_REWARD_ENV_LOG) || (out.agent_reward != nullptr);
+  drain_vmem();
+  __builtin_amdgcn_s_setprio(MGN_TRIO_PF);
+#ifdef MGN_STAMPS
+  unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0;
+#endif
+  for (int j = 0;; ++j) {
+    const int cur = j & 1, prv = cur ^ 1;
+    MGN_T(T0);
+    int rst_out = 0;
+    // the step L ran in iteration j-1, unless F voided it at iteration j-1
+    const int flags = sh.rFlags[prv][el];
+    if (live && (flags & TR_STEP) && !sh.reset[prv][el]) {
+      const int k = sh.rK[prv][el];
+      const size_t oN = (size_t)k * p.N, oNA = (size_t)k * p.N * A;
+      Lane<M> f = s;
+      f.L[0] = sh.rL[prv][l];
+      f.P[0] = sh.price[prv][l];
+      const double cashv = sh.rCash[prv][el];
+      const double prevEq = sh.rPrevEq[prv][el];
+      // post-tick sums, equity, reward, done (Env.h:211-223)
+      Sums q;
+      {
+        double tlp[M];
+        tlp[0] = f.L[0] * f.P[0];
+        q.lp = canon<M, S>(tlp);
+      }
+      q.ml = sh.rMl[prv][el];
+      q.sh = sh.rSh[prv][el];
+      q.b = sh.rB[prv][el];
+      const double curEq = (cashv + q.lp) - q.b;
+      const double ratio = curEq / prevEq;
+      const double clampv = (in_kind == IN_SINGLE) ? 0.01 : 0.3;
+      const double reward = log_ratio((ratio < clampv) ? clampv : ratio);
+      const bool done = (flags & TR_ANYMC) || margin_call(q, cashv, p.mainM) || (curEq < 0.1 * p.init_cash);
+      // ledgerNormedFull, agent reward, PPC, shaper (as k_step_duo's finish)
+      const double Lc = f.L[0], P = f.P[0];
+      double ar = 0.;
+      if (f.valid[0] && need_ar) {
+        double v = (((Lc * P) - sh.rPv[prv][l]) - (sh.rTu[prv][l] * sh.rTp[prv][l] + sh.rTc[prv][l])) / prevEq;
+        v += 1;
+        v = (v < .35) ? .35 : v;
+        ar = log_ratio(v);
+      }
+      const double port0 = (cashv - q.b) / curEq;
+      const double portA = (Lc * P) / curEq;
+      double cos_term = 0.;
+      if (p.shaper == MGN_SHAPER_PPC) {
+        double pp[M], pq[M];
+        const double qv = f.valid[0] ? s_tgt[1 + f.asset[0]] : 0.;
+        const double pv = f.valid[0] ? portA : 0.;
+        pp[0] = pv * pv;
+        pq[0] = pv * qv;
+        const double np_ = sqrt(port0 * port0 + canon<M, S>(pp));
+        const double dot = port0 * s_tgt[0] + canon<M, S>(pq);
+        cos_term = p.cos_temp * (dot / (np_ * g.cos_qn));
+      }
+      double shaped_s = 0., rin_s = 0., shaped_v = 0.;
+      if (D == 1) {
+        double arr[M];
+        arr[0] = ar;
+        rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(arr) : reward;
+        if (p.shaper == MGN_SHAPER_DDR) {  // shape() for DDR (nstep_buffer.py:128-162)
+          const double r = rin_s;
+          shaped_s = clip1((0.0 + 1.0 * ddr_one_pre(r, g.shA, g.shB, ddr_pre(g.shA, g.shB))) / 1);
+          double m = r < 0. ? r : 0.;
+          if (r != r) m = r;
+          g.shA += p.eta * (r - g.shA);
+          g.shB += p.eta * (m * m - g.shB);
+        } else {
+          shaped_s = shape(p.shaper, rin_s, g.shA, g.shB, p.eta, cos_term, p.sexp);
+        }
+      } else {
+        shaped_v = f.valid[0] ? shape(p.shaper, ar, g.shA, g.shB, p.eta, cos_term, p.sexp) : 0.;
+      }
+      // outputs of step k (the speculative runs never reach F)
+      if (f.valid[0]) {
+        const size_t i = oNA + (size_t)env * A + f.asset[0];
+        if (!MGN_TRIO_LST) {
+          if (om & O_TP) ost(ov.tprice + i, sh.rTp[prv][l]);
+          if (om & O_TU) ost(ov.tunits + i, sh.rTu[prv][l]);
+          if (om & O_TC) ost(ov.tcost + i, sh.rTc[prv][l]);
+          if (om & O_RISK) ost(ov.risk + i, (uint8_t)sh.rRk[prv][l]);
+        }
+        if (!MGN_TRIO_GST && (om & O_OPR)) ost(ov.obs_price + ((oN + env) * (size_t)p.F + f.asset[0]), P);
+        if (om & O_OPT) ost(ov.obs_port + ((size_t)k * p.N * (A + 1) + (size_t)env * (A + 1) + 1 + f.asset[0]), portA);
+        if (D != 1) {
+          if (om & O_AREW) ost(ov.agent_reward + i, ar);
+          if (om & O_SHP) ost(ov.shaped + i, shaped_v);
+        }
+      }
+      if (ls == 0) {
+        if (om & O_OPT) ost(ov.obs_port + ((size_t)k * p.N * (A + 1) + (size_t)env * (A + 1)), port0);
+        if (om & O_DONE) ost(ov.done + (oN + env), (uint8_t)(done ? 1 : 0));
+        if (om & O_MC) ost(ov.margin_call + (oN + env), (uint8_t)((flags & TR_MCALL) ? 1 : 0));
+        if (om & O_DEND) ost(ov.data_end + (oN + env), (uint8_t)0);
+        if (om & O_REW) ost(ov.reward + (oN + env), reward);
+        if (om & O_NSH) ost(ov.n_shaped + (oN + env), (uint8_t)1);
+        if (!MGN_TRIO_GST && (om & O_TS)) ost(ov.timestamp + (oN + env), (uint64_t)sh.ts[prv][el]);
+        if (D == 1) {
+          if (om & O_AREW) ost(ov.agent_reward + (oN + env), rin_s);
+          if (om & O_SHP) ost(ov.shaped + (oN + env), shaped_s);
+        }
+      }
+      // episode statistics
+      ep_ret += reward;
+      ep_len += 1;
+      if (done) {
+        if (ls == 0) {
+          MGN_G double* st = gs.epstats + (size_t)env * 4;
+          st[0] = ep_ret;
+          st[1] = ep_len;
+          st[2] = curEq;
+          n_done = n_done + 1;
+          st[3] = n_done;
+        }
+        ep_ret = 0;
+        ep_len = 0;
+        if (p.auto_reset) rst_out = 1;
+      }
+    }
+    if (ls == 0) sh.reset[cur][el] = rst_out;
+    if (rst_out) sh.more[j % 3] = 1;  // the reset tick runs next iteration
+    MGN_T(T1);
+    __syncthreads();
+    MGN_T(T2);
+#ifdef MGN_STAMPS
+    acc0 += T1 - T0;
+    acc1 += T2 - T1;
+#endif
+    if (!__builtin_amdgcn_readfirstlane(sh.more[j % 3])) break;
+  }
+#ifdef MGN_STAMPS
+  if (l == 0) {
+    atomicAdd(&g_duo_stamps[16], acc0);
+    atomicAdd(&g_duo_stamps[17], acc1);
+  }
+#endif
+  if (!live) return;
+  if (ls == 0) {
+    p.ep[(size_t)env * 2] = ep_ret;
+    p.ep[(size_t)env * 2 + 1] = ep_len;
+    if (D == 1) {
+      p.sA[env] = g.shA;
+      p.sB[env] = g.shB;
+    }
+  }
+  if (D != 1 && s.valid[0]) {
+    p.sA[(size_t)env * A + s.asset[0]] = g.shA;
+    p.sB[(size_t)env * A + s.asset[0]] = g.shB;
+  }
+}
+
+}  // namespace mgn

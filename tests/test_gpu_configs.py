@@ -118,7 +118,8 @@ def test_c4_composite_ppc_log_window(gpu):
 
 
 def test_large_batch_auto_layout_tail_block(gpu):
-    """ADVICE r1: the automatic layout runs the two-role kernel at large N;
+    """the automatic layout runs a multi-role kernel at large N
+    (k_step_trio here, k_step_duo where the three-role one is not eligible);
     32768 + 17 envs (a partial last workgroup), auto-reset forced by high
     leverage, against k_step at 4 assets per lane bit for bit."""
     from madigan_amd import BatchedEnv
@@ -133,7 +134,7 @@ def test_large_batch_auto_layout_tail_block(gpu):
     for mode in ("auto", "single4"):
         g = BatchedEnv(spec, N, **kw)
         if mode == "auto":
-            assert g.lib.mgn_get_schedule(g.h) == L.SCHED_DUO
+            assert g.lib.mgn_get_schedule(g.h) in (L.SCHED_DUO, L.SCHED_TRIO)
         else:
             L.check(g.lib.mgn_set_schedule(g.h, L.SCHED_SINGLE), g.h)
             L.check(g.lib.mgn_set_layout(g.h, 4), g.h)

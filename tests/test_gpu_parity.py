@@ -300,9 +300,10 @@ def test_nstep_rollout(gpu, shaper, mode, n):
     (2, dict(reward_shaper="sortino_shaperA", sortino_exp=2, reward_mode="agent_sum", window=5)),
 ])
 def test_schedules_bit_identical(gpu, A, kw):
-    """The two-role kernel (k_step_duo: generator waves + ledger waves) and the
-    single-role k_step produce identical bits, including auto-resets, windows
-    and every step overload."""
+    """The two-role kernel (k_step_duo: generator waves + ledger waves), the
+    three-role pipelined kernel (k_step_trio, where eligible: speculative
+    steps rolled back at every auto-reset) and the single-role k_step produce
+    identical bits, including auto-resets, windows and every step overload."""
     from madigan_amd import BatchedEnv
     from madigan_amd import _lib as L
     N, K = 300, 40
@@ -312,7 +313,8 @@ def test_schedules_bit_identical(gpu, A, kw):
     rng = np.random.default_rng(A)
     units = rng.normal(0, 3e3, (N, A))
     res = []
-    for sched in (L.SCHED_SINGLE, L.SCHED_DUO):
+    trio_ok = A <= 8 and not kw.get("window") and kw.get("nstep_return", 1) == 1
+    for sched in (L.SCHED_SINGLE, L.SCHED_DUO) + ((L.SCHED_TRIO,) if trio_ok else ()):
         g = BatchedEnv(spec, N, **base, **kw)
         L.check(g.lib.mgn_set_schedule(g.h, sched), g.h)
         assert g.lib.mgn_get_schedule(g.h) == sched
@@ -330,12 +332,13 @@ def test_schedules_bit_identical(gpu, A, kw):
             out.update({"w_" + str(i): t.cpu().numpy() for i, t in enumerate(g.window())})
         res.append(out)
     assert res[0]["done"].sum() > 0
-    for k, v in res[0].items():
-        w = res[1][k]
-        if np.asarray(v).dtype == np.float64:
-            assert_bits(w, v, f"duo vs single {k}")
-        else:
-            assert np.array_equal(np.asarray(w), np.asarray(v)), f"duo vs single {k}"
+    for other, name in zip(res[1:], ("duo", "trio")):
+        for k, v in res[0].items():
+            w = other[k]
+            if np.asarray(v).dtype == np.float64:
+                assert_bits(w, v, f"{name} vs single {k}")
+            else:
+                assert np.array_equal(np.asarray(w), np.asarray(v)), f"{name} vs single {k}"
 
 
 @pytest.mark.gpu

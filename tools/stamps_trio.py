@@ -1,0 +1,59 @@
+"""Per-role cycles of k_step_trio (diagnostic build with -DMGN_STAMPS).
+
+    MADIGAN_LIB_PATH=tools/_var/stamps/libmadigan_hip.so FUSE=64 python tools/stamps_trio.py
+
+Prints, per role (generator / ledger / finish), the mean cycles per
+iteration spent working before the iteration's barrier and waiting at it
+(s_memtime, one wave per role and block), the ledger's Broker parts, and the
+launch time.
+"""
+import ctypes as C
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from madigan_amd import _lib as L  # noqa: E402
+
+
+def main():
+    N = int(os.environ.get("N", 8192))
+    fuse = int(os.environ.get("FUSE", 64))
+    env, _, _ = bench.workload_env("C3", N, 8, 0, "cuda:0")
+    assert int(env.lib.mgn_get_schedule(env.h)) == L.SCHED_TRIO
+    fn = env.lib.mgn_diag_stamps
+    fn.argtypes = [C.POINTER(C.c_ulonglong)]
+    acts = env.generate_actions(fuse, seed=5)
+    out = env.alloc_traj(fuse, fields=["reward", "shaped", "done", "obs_price", "obs_port", "timestamp",
+                                       "tprice", "tunits", "tcost", "risk", "margin_call"])
+    for _ in range(3):
+        env.rollout(acts, out)
+    torch.cuda.synchronize()
+    buf = (C.c_ulonglong * 24)()
+    fn(buf)
+    reps = 10
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        env.rollout(acts, out)
+    e1.record()
+    torch.cuda.synchronize()
+    fn(buf)
+    v = list(buf)
+    it = max(v[8], 1)
+    res = {"N": N, "fuse": fuse, "us_per_launch": e0.elapsed_time(e1) * 1000 / reps,
+           "iters_per_block": v[8] / max(v[10], 1),
+           "gen": {"work": round(v[0] / it, 1), "wait": round(v[1] / it, 1)},
+           "ledger": {"work": round(v[4] / it, 1), "wait": round(v[5] / it, 1),
+                      "broker_parts": {k: round(v[13 + i] / it, 1)
+                                       for i, k in enumerate(("order_prep", "spec_loop", "post"))}},
+           "finish": {"work": round(v[16] / it, 1), "wait": round(v[17] / it, 1)}}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -332,7 +332,10 @@ bool duo_eligible(const mgn_env* e) {
 // the three-role kernel: 2..8 assets, generator sources, one-step rewards, no
 // window (its speculative steps would need the window rows rolled back)
 bool trio_eligible(const mgn_env* e) {
-  return e->apad >= 2 && e->apad <= 8 && !e->cfg.aux && !e->replay && e->cfg.nstep == 1 && e->W == 0;
+  // (its output indices are k x a 32-bit stride: N (A + 1) and N F fit 32 bits)
+  const uint64_t row = (uint64_t)(e->A + 1 > e->F ? e->A + 1 : e->F);
+  return e->apad >= 2 && e->apad <= 8 && !e->cfg.aux && !e->replay && e->cfg.nstep == 1 && e->W == 0 &&
+         (uint64_t)e->N * row < (1ull << 32);
 }
 // automatic: where the single-role kernel would run one lane per asset (small
 // batches: one wave per SIMD), give every asset a second (and a third) lane

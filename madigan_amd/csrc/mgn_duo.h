@@ -111,7 +111,7 @@ struct DuoShared {
 enum : uint32_t { O_REW = 1u, O_AREW = 2u, O_SHP = 4u, O_DONE = 8u, O_OPR = 16u, O_OPT = 32u,
                   O_TS = 64u, O_TP = 128u, O_TU = 256u, O_TC = 512u, O_RISK = 1024u,
                   O_MC = 2048u, O_NSH = 4096u, O_DEND = 8192u };
-__device__ __forceinline__ uint32_t traj_mask(const mgn_traj& o) {
+__host__ __device__ __forceinline__ uint32_t traj_mask(const mgn_traj& o) {
   return (o.reward ? O_REW : 0u) | (o.agent_reward ? O_AREW : 0u) | (o.shaped ? O_SHP : 0u) |
          (o.done ? O_DONE : 0u) | (o.obs_price ? O_OPR : 0u) | (o.obs_port ? O_OPT : 0u) |
          (o.timestamp ? O_TS : 0u) | (o.tprice ? O_TP : 0u) | (o.tunits ? O_TU : 0u) |
@@ -135,23 +135,37 @@ struct GTraj {
   MGN_G double *tprice, *tunits, *tcost;
   MGN_G uint8_t *risk, *margin_call, *n_shaped, *data_end;
 };
+// OMC != 0: the output set is known at compile time; the pointers of the
+// fields outside it are never loaded
+template <uint32_t OMC = 0>
 __device__ __forceinline__ GTraj traj_vgpr(const mgn_traj& o) {
-  GTraj v;
-  v.reward = vptr(o.reward);
-  v.agent_reward = vptr(o.agent_reward);
-  v.shaped = vptr(o.shaped);
-  v.done = vptr(o.done);
-  v.obs_price = vptr(o.obs_price);
-  v.obs_port = vptr(o.obs_port);
-  v.timestamp = vptr(o.timestamp);
-  v.tprice = vptr(o.tprice);
-  v.tunits = vptr(o.tunits);
-  v.tcost = vptr(o.tcost);
-  v.risk = vptr(o.risk);
-  v.margin_call = vptr(o.margin_call);
-  v.n_shaped = vptr(o.n_shaped);
-  v.data_end = vptr(o.data_end);
+  constexpr uint32_t M = OMC ? OMC : ~0u;
+  GTraj v = {};
+  if (M & O_REW) v.reward = vptr(o.reward);
+  if (M & O_AREW) v.agent_reward = vptr(o.agent_reward);
+  if (M & O_SHP) v.shaped = vptr(o.shaped);
+  if (M & O_DONE) v.done = vptr(o.done);
+  if (M & O_OPR) v.obs_price = vptr(o.obs_price);
+  if (M & O_OPT) v.obs_port = vptr(o.obs_port);
+  if (M & O_TS) v.timestamp = vptr(o.timestamp);
+  if (M & O_TP) v.tprice = vptr(o.tprice);
+  if (M & O_TU) v.tunits = vptr(o.tunits);
+  if (M & O_TC) v.tcost = vptr(o.tcost);
+  if (M & O_RISK) v.risk = vptr(o.risk);
+  if (M & O_MC) v.margin_call = vptr(o.margin_call);
+  if (M & O_NSH) v.n_shaped = vptr(o.n_shaped);
+  if (M & O_DEND) v.data_end = vptr(o.data_end);
   return v;
+}
+// the output sets with their own trio instantiations: every field, and the
+// agent loop's State + EnvInfo + reward + shaped reward (no agent reward,
+// n_shaped or data_end)
+constexpr uint32_t O_ALL = 16383u;
+constexpr uint32_t O_STD = O_REW | O_SHP | O_DONE | O_OPR | O_OPT | O_TS | O_TP | O_TU | O_TC | O_RISK | O_MC;
+// element index k * stride + base as one 32 x 32 + 64 multiply-add (the
+// host checks that every stride fits 32 bits)
+__device__ __forceinline__ size_t kidx(int k, uint32_t stride, size_t base) {
+  return (size_t)(uint32_t)k * stride + base;
 }
 // output stores (written once per launch, read after it)
 template <typename T>

@@ -362,9 +362,18 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
     const int a = s.asset[m];
     const double* q = p.src[a].p;
     const int kind = s.kind[m];
+    // the slot-0 variates, drawn once for every kind that reads them: a
+    // Composite source's lanes (Synth / OU / TrendOU in one wave) then run one
+    // Philox + Box-Muller instead of one per kind branch (same bits: the draw
+    // is a pure function of its counter)
+    const bool sine_fam = kind == MGN_SRC_SINE || kind == MGN_SRC_SAWTOOTH || kind == MGN_SRC_TRIANGLE;
+    const bool need0 = kind == MGN_SRC_TRENDOU || kind == MGN_SRC_OU || kind == MGN_SRC_SIMPLETREND ||
+                       kind == MGN_SRC_TRENDYOU || kind == MGN_SRC_GAUSSIAN || kind == MGN_SRC_OUPAIR ||
+                       (sine_fam && q[5] != 0.0);
+    Draw d = {0.0, 0.0, 0u};
+    if (need0) d = draw0(p.seed, genv, (uint32_t)a, tick);
     if (kind == MGN_SRC_TRENDOU) {
       double y = s.P[m];
-      const Draw d = draw0(p.seed, genv, (uint32_t)a, tick);
       if (s.tfl[m] & 1) {
         const double n = d.z * q[8] + 0.0;
         const double dir = (s.tfl[m] & 2) ? -1.0 : 1.0;
@@ -394,14 +403,14 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
       }
       s.P[m] = y;
     } else if (kind == MGN_SRC_OU) {
-      const double z = draw0(p.seed, genv, (uint32_t)a, tick).z * 1.0 + 0.0;
+      const double z = d.z * 1.0 + 0.0;
       double x = s.P[m];
       x += (q[1] * (q[0] - x)) + q[0] * q[2] * z;
       s.P[m] = x;
-    } else if (kind == MGN_SRC_SINE || kind == MGN_SRC_SAWTOOTH || kind == MGN_SRC_TRIANGLE) {
+    } else if (sine_fam) {
       // Synth / SawTooth / Triangle::getData (DataSource.cpp:535-543, 557-577)
       double noise = 0.0;
-      if (q[5] != 0.0) noise = draw0(p.seed, genv, (uint32_t)a, tick).z * q[5] + 0.0;
+      if (q[5] != 0.0) noise = d.z * q[5] + 0.0;
       const double PI2 = 3.141592653589793238463 * 2;
       double wave;
       if (kind == MGN_SRC_SINE) wave = q[2] * det_sin(PI2 * s.sx[m] * q[0]);
@@ -412,7 +421,6 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
     } else if (kind == MGN_SRC_SIMPLETREND) {
       // SimpleTrend::getData (DataSource.cpp:1322-1347)
       double y = s.P[m];
-      const Draw d = draw0(p.seed, genv, (uint32_t)a, tick);
       if (s.tfl[m] & 1) {
         const double dir = (s.tfl[m] & 2) ? -1.0 : 1.0;
         y += y * s.dy[m] * dir;
@@ -432,7 +440,6 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
       s.P[m] = (0.01 < y) ? y : 0.01;
     } else if (kind == MGN_SRC_TRENDYOU) {
       // TrendyOU::getData (DataSource.cpp:1608-1640): sx = ouComponent, oum = trendComponent
-      const Draw d = draw0(p.seed, genv, (uint32_t)a, tick);
       const double ou_noise = s.oum[m] * (d.z * q[7] + 0.0);
       const double ou_rev = q[6] * (-s.sx[m]);
       s.sx[m] += ou_rev + ou_noise;
@@ -463,7 +470,7 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
       s.P[m] = s.sx[m] + s.oum[m];
     } else if (kind == MGN_SRC_GAUSSIAN) {
       // Gaussian::getData (DataSource.cpp:1108-1114): normal(mean, var)
-      s.P[m] = draw0(p.seed, genv, (uint32_t)a, tick).z * q[1] + q[0];
+      s.P[m] = d.z * q[1] + q[0];
     } else if (kind == MGN_SRC_OUPAIR) {
       // OUPair::getData (DataSource.cpp:1236-1244): the pair's shared mean random
       // walk is recomputed identically by the lanes of both assets (its variate
@@ -471,7 +478,7 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
       const uint32_t a0 = (uint32_t)(a - (q[3] != 0.0 ? 1 : 0));
       double mean = s.oum[m];
       mean += mean * (draw_s(p.seed, genv, a0, 2, tick).z * q[2] + 0.0);
-      const double z = draw0(p.seed, genv, (uint32_t)a, tick).z * q[1] + 0.0;
+      const double z = d.z * q[1] + 0.0;
       double x = s.P[m];
       x += (q[0] * (mean - x)) + mean * z;
       s.P[m] = x;

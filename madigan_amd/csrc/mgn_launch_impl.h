@@ -78,7 +78,14 @@ void launch_trio(const StepArgs& a) {
                        a.units, a.aidx, a.act, a.K);
   };
   const bool disc = a.in_kind == IN_DISCRETE;
-  if (disc) {
+  const uint32_t om = traj_mask(a.out);
+  if (disc && om == O_STD) {  // the agent loop's output set
+    if (a.p.reqm_one) go(k_step_trio<S, true, true, O_STD>);
+    else go(k_step_trio<S, false, true, O_STD>);
+  } else if (disc && om == O_ALL) {
+    if (a.p.reqm_one) go(k_step_trio<S, true, true, O_ALL>);
+    else go(k_step_trio<S, false, true, O_ALL>);
+  } else if (disc) {
     if (a.p.reqm_one) go(k_step_trio<S, true, true>);
     else go(k_step_trio<S, false, true>);
   } else {

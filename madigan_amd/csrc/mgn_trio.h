@@ -79,7 +79,8 @@ struct TrioShared {
   int32_t more[3];
 };
 
-template <int S, bool RQ1, bool DISC>
+// OMC: the output set when known at compile time (O_ALL, O_STD), else 0
+template <int S, bool RQ1, bool DISC, uint32_t OMC = 0>
 __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj out, int in_kind_rt,
                                                           const double* __restrict__ units_in,
                                                           const int32_t* __restrict__ aidx_in,
@@ -175,8 +176,8 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
 
   if (role == 0) {
     // ---------------- generator waves: tick of step j, State.price / timestamp
-    const uint32_t om = traj_mask(out);
-    const GTraj ov = traj_vgpr(out);
+    const uint32_t om = OMC ? OMC : traj_mask(out);
+    const GTraj ov = traj_vgpr<MGN_TRIO_GST ? OMC : O_REW>(out);
     p.seed = in_vgpr(p.seed);
     p.env_offset = in_vgpr(p.env_offset);
     drain_vmem();
@@ -269,14 +270,14 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
 
   if (role == 1) {
     // ---------------- ledger waves: Broker orders of step j
-    const uint32_t om = traj_mask(out);
-    const GTraj ov = traj_vgpr(out);
+    const uint32_t om = OMC ? OMC : traj_mask(out);
+    const GTraj ov = traj_vgpr<MGN_TRIO_LST ? OMC : O_REW>(out);
     const MGN_G double* gunits = vptr(units_in);
     const MGN_G int32_t* gaidx = vptr(aidx_in);
     p.init_cash = in_vgpr(p.init_cash);
     p.mainM = in_vgpr(p.mainM);
     p.unit_size = in_vgpr(p.unit_size);
-    const size_t act_step = (size_t)p.N * A;
+    const uint32_t act_step = (uint32_t)p.N * (uint32_t)A;
     // sums of the ledger (canonical trees): ml, sh, b change only with the
     // orders, lp with the prices; `fresh` = recompute all four (start, reset)
     Sums sa = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
@@ -310,7 +311,7 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
         // the action of the next step this lane runs (k + 1 if this one
         // steps; a rollback re-reads step k's, clamped in range)
         const int kn = k + (stepping ? 1 : 0);
-        act_cur = act_lane[(size_t)(kn < K ? kn : K - 1) * act_step];
+        act_cur = act_lane[kidx(kn < K ? kn : K - 1, act_step, 0)];
       }
       int flags = 0;
       if (stepping) {
@@ -414,8 +415,8 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
   }
 
   // ---------------- finish waves: step j-1's reward, done and outputs
-  const uint32_t om = traj_mask(out);
-  const GTraj ov = traj_vgpr(out);
+  const uint32_t om = OMC ? OMC : traj_mask(out);
+  const GTraj ov = traj_vgpr<OMC>(out);
   GState gs;
   gs.epstats = vptr(p.epstats);
   p.init_cash = in_vgpr(p.init_cash);
@@ -433,7 +434,14 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
     qq[0] = q * q;
     g.cos_qn = sqrt(s_tgt[0] * s_tgt[0] + canon<M, S>(qq));
   }
-  const bool need_ar = (p.reward_mode != MGN_REWARD_ENV_LOG) || (out.agent_reward != nullptr);
+  const bool need_ar = (p.reward_mode != MGN_REWARD_ENV_LOG) || (om & O_AREW);
+  // output element strides per step (32-bit: checked on the host) and the
+  // lane's bases: per asset (k, env, asset), State.price (k, env, feature),
+  // State.portfolio (k, env, 0), per env (k, env)
+  const uint32_t sN = (uint32_t)p.N, sNA = (uint32_t)p.N * (uint32_t)A, sNF = (uint32_t)p.N * (uint32_t)p.F,
+                 sNA1 = (uint32_t)p.N * (uint32_t)(A + 1);
+  const size_t bA = (size_t)env * A + s.asset[0], bP = (size_t)env * p.F + s.asset[0],
+               bO = (size_t)env * (A + 1);
   drain_vmem();
   __builtin_amdgcn_s_setprio(MGN_TRIO_PF);
 #ifdef MGN_STAMPS
@@ -447,7 +455,6 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
     const int flags = sh.rFlags[prv][el];
     if (live && (flags & TR_STEP) && !sh.reset[prv][el]) {
       const int k = sh.rK[prv][el];
-      const size_t oN = (size_t)k * p.N, oNA = (size_t)k * p.N * A;
       Lane<M> f = s;
       f.L[0] = sh.rL[prv][l];
       f.P[0] = sh.price[prv][l];
@@ -510,31 +517,32 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
       }
       // outputs of step k (the speculative runs never reach F)
       if (f.valid[0]) {
-        const size_t i = oNA + (size_t)env * A + f.asset[0];
+        const size_t i = kidx(k, sNA, bA);
         if (!MGN_TRIO_LST) {
           if (om & O_TP) ost(ov.tprice + i, sh.rTp[prv][l]);
           if (om & O_TU) ost(ov.tunits + i, sh.rTu[prv][l]);
           if (om & O_TC) ost(ov.tcost + i, sh.rTc[prv][l]);
           if (om & O_RISK) ost(ov.risk + i, (uint8_t)sh.rRk[prv][l]);
         }
-        if (!MGN_TRIO_GST && (om & O_OPR)) ost(ov.obs_price + ((oN + env) * (size_t)p.F + f.asset[0]), P);
-        if (om & O_OPT) ost(ov.obs_port + ((size_t)k * p.N * (A + 1) + (size_t)env * (A + 1) + 1 + f.asset[0]), portA);
+        if (!MGN_TRIO_GST && (om & O_OPR)) ost(ov.obs_price + kidx(k, sNF, bP), P);
+        if (om & O_OPT) ost(ov.obs_port + (kidx(k, sNA1, bO) + 1 + f.asset[0]), portA);
         if (D != 1) {
           if (om & O_AREW) ost(ov.agent_reward + i, ar);
           if (om & O_SHP) ost(ov.shaped + i, shaped_v);
         }
       }
       if (ls == 0) {
-        if (om & O_OPT) ost(ov.obs_port + ((size_t)k * p.N * (A + 1) + (size_t)env * (A + 1)), port0);
-        if (om & O_DONE) ost(ov.done + (oN + env), (uint8_t)(done ? 1 : 0));
-        if (om & O_MC) ost(ov.margin_call + (oN + env), (uint8_t)((flags & TR_MCALL) ? 1 : 0));
-        if (om & O_DEND) ost(ov.data_end + (oN + env), (uint8_t)0);
-        if (om & O_REW) ost(ov.reward + (oN + env), reward);
-        if (om & O_NSH) ost(ov.n_shaped + (oN + env), (uint8_t)1);
-        if (!MGN_TRIO_GST && (om & O_TS)) ost(ov.timestamp + (oN + env), (uint64_t)sh.ts[prv][el]);
+        const size_t ie = kidx(k, sN, (size_t)env);
+        if (om & O_OPT) ost(ov.obs_port + kidx(k, sNA1, bO), port0);
+        if (om & O_DONE) ost(ov.done + ie, (uint8_t)(done ? 1 : 0));
+        if (om & O_MC) ost(ov.margin_call + ie, (uint8_t)((flags & TR_MCALL) ? 1 : 0));
+        if (om & O_DEND) ost(ov.data_end + ie, (uint8_t)0);
+        if (om & O_REW) ost(ov.reward + ie, reward);
+        if (om & O_NSH) ost(ov.n_shaped + ie, (uint8_t)1);
+        if (!MGN_TRIO_GST && (om & O_TS)) ost(ov.timestamp + ie, (uint64_t)sh.ts[prv][el]);
         if (D == 1) {
-          if (om & O_AREW) ost(ov.agent_reward + (oN + env), rin_s);
-          if (om & O_SHP) ost(ov.shaped + (oN + env), shaped_s);
+          if (om & O_AREW) ost(ov.agent_reward + ie, rin_s);
+          if (om & O_SHP) ost(ov.shaped + ie, shaped_s);
         }
       }
       // episode statistics

@@ -170,7 +170,9 @@ __device__ __forceinline__ size_t kidx(int k, uint32_t stride, size_t base) {
 // output stores (written once per launch, read after it)
 template <typename T>
 __device__ __forceinline__ void ost(MGN_G T* q, T v) {
-#ifdef MGN_X_NT
+#if defined(MGN_ABL_NOSTORE)  // diagnostic timing build: outputs not stored
+  (void)q; (void)v;
+#elif defined(MGN_X_NT)
   __builtin_nontemporal_store(v, q);
 #else
   *q = v;

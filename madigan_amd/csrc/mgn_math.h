@@ -190,7 +190,16 @@ __device__ __forceinline__ Draw draw_s(uint64_t seed, uint64_t env, uint32_t ass
 }
 
 __device__ __forceinline__ Draw draw0(uint64_t seed, uint64_t env, uint32_t asset, uint64_t tick) {
+#ifdef MGN_ABL_DRAW  // diagnostic timing build: a cheap stand-in for the variate (wrong values)
+  const uint32_t h = ((uint32_t)tick * 0x9E3779B1u) ^ ((uint32_t)env * 0x85EBCA6Bu) ^ (asset * 0xC2B2AE35u);
+  Draw d;
+  d.z = (double)(int32_t)(h & 0xffffu) * (1.0 / 32768.0) - 1.0;
+  d.ut = (double)(h >> 16) * (1.0 / 65536.0);
+  d.dbit = h & 1u;
+  return d;
+#else
   return draw_s(seed, env, asset, 0, tick);
+#endif
 }
 
 // std::modf's fractional part: x - trunc(x) is exact; its sign follows x (modf(-3.0) = -0.0)

@@ -516,6 +516,7 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
         shaped_v = f.valid[0] ? shape(p.shaper, ar, g.shA, g.shB, p.eta, cos_term, p.sexp) : 0.;
       }
       // outputs of step k (the speculative runs never reach F)
+#ifndef MGN_ABL_NOSTORE_ASSET
       if (f.valid[0]) {
         const size_t i = kidx(k, sNA, bA);
         if (!MGN_TRIO_LST) {
@@ -531,6 +532,8 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
           if (om & O_SHP) ost(ov.shaped + i, shaped_v);
         }
       }
+#endif
+#ifndef MGN_ABL_NOSTORE_ENV
       if (ls == 0) {
         const size_t ie = kidx(k, sN, (size_t)env);
         if (om & O_OPT) ost(ov.obs_port + kidx(k, sNA1, bO), port0);
@@ -545,6 +548,7 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
           if (om & O_SHP) ost(ov.shaped + ie, shaped_s);
         }
       }
+#endif
       // episode statistics
       ep_ret += reward;
       ep_len += 1;

@@ -53,6 +53,46 @@ def test_c3_bench_shape_launches(gpu):
         close(st[:, j], orc.scalar(name), name)
 
 
+STD_FIELDS = ("reward", "shaped", "done", "obs_price", "obs_port", "timestamp", "tprice", "tunits",
+              "tcost", "risk", "margin_call")
+
+
+@pytest.mark.parametrize("fields,misalign", [
+    ("std", False),     # the agent loop's / bench's output set: the fixed-set instantiation
+    ("all", False),     # every field: the fixed-set instantiation
+    ("std", True),      # the same set in buffers offset by one element
+    ("subset", False),  # no timestamps / costs: the runtime-mask instantiation
+])
+def test_c3_output_sets(gpu, fields, misalign):
+    """Every output set the three-role kernel serves, at the bench shape
+    (8192 x 8, 20-step launches), bit-exact against the oracle for every field
+    present (mgn_trio.h instantiates the kernel per fixed output set, with
+    the runtime-mask kernel for every other set)."""
+    import torch
+    N, A, K = 8192, 8, 20
+    g, orc = make_pair(trendou_sources(A, TRENDOU_P), N, seed=0x6D6164 + 3, **C3_KW)
+    acts = g.generate_actions(2 * K, seed=0x6D6164)
+    names = {"std": STD_FIELDS, "all": None,
+             "subset": ("reward", "shaped", "done", "obs_price", "obs_port", "tprice", "tunits", "risk")}[fields]
+    for rep in range(2):
+        traj = g.alloc_traj(K, fields=names)
+        if misalign:  # the same fields, each one element into a larger buffer
+            shp = g._traj_shapes(K)
+            traj = {k: torch.empty(v.numel() + 1, dtype=v.dtype, device=v.device)[1:].view(shp[k][0])
+                    for k, v in traj.items()}
+        out = _host(g.rollout(acts[rep * K:(rep + 1) * K], out=traj))
+        ref = orc.rollout(acts[rep * K:(rep + 1) * K].cpu().numpy(), threads=THREADS)
+        for f, v in out.items():
+            if v.dtype == np.float64 and f not in ("reward", "shaped", "agent_reward"):
+                assert_bits(v, ref[f], f"{fields} {f} launch {rep}")
+            elif f in ("reward", "shaped", "agent_reward"):
+                close(v, ref[f], f"{fields} {f} launch {rep}")
+            else:
+                assert np.array_equal(v.astype(np.uint64) if f == "timestamp" else v,
+                                      ref[f]), f"{fields} {f} launch {rep}"
+    state_check(g, orc, f"C3 {fields}")
+
+
 def _windowed_pair(sources, N, W, norm, shaper, **kw):
     base = dict(required_margin=1.0, maintenance_margin=0.25, transaction_cost_rel=0.02,
                 unit_size=0.05, auto_reset=1, init_cash=1_000_000.0, window=W, norm_type=norm,

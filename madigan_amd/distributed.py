@@ -59,7 +59,10 @@ def rccl_comm(group=None, device=None) -> int:
     if dist.get_backend(g) != "nccl":
         return 0
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-    return int(g._get_backend(dev)._comm_ptr())
+    try:  # a private accessor of torch's ProcessGroupNCCL: absent -> torch's all-gather
+        return int(g._get_backend(dev)._comm_ptr())
+    except (AttributeError, RuntimeError):
+        return 0
 
 
 def allgather_env_stats(env, n_total=None, group=None):

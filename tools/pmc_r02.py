@@ -42,7 +42,7 @@ def main():
     traffic = json.load(open(tj)) if os.path.exists(tj) else {}
     valu = json.load(open(vj)) if os.path.exists(vj) else {}
     out = {}
-    for K, pick in (("20", "last"), ("1", "mean")):
+    for K, pick in (("20", "last"), ("1", "mean"), ("256", "mean")):
         merged = {}
         for part in ("fetch", "write", "sq"):
             f = os.path.join(a.src, f"pmc{K}", part, "p_counter_collection.csv")
@@ -66,7 +66,7 @@ def main():
             s["valu_wave_insts_per_wave_step"] = merged["SQ_INSTS_VALU"] / merged["SQ_WAVES"] / int(K)
             s["wait_any_frac"] = merged["SQ_WAIT_ANY"] / merged["SQ_WAVE_CYCLES"]
         out[key] = s
-    for K in ("20", "1"):
+    for K in ("20", "1", "256"):
         ks = os.path.join(a.src, f"kt{K}", "kt_kernel_stats.csv")
         if os.path.exists(ks):
             shutil.copy(ks, os.path.join(prof, f"{a.tag}_kernel_stats_fuse{K}.csv"))

@@ -141,6 +141,21 @@ SYMBOLS = {
 }
 
 _lib = None
+_hip = None
+
+
+def hip():
+    """The process's HIP runtime (the instance torch loaded), for the few
+    stream-ordered copies the host wrappers issue directly."""
+    global _hip
+    if _hip is None:
+        h = C.CDLL("libamdhip64.so")
+        h.hipMemcpyAsync.restype = C.c_int
+        h.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+        h.hipStreamSynchronize.restype = C.c_int
+        h.hipStreamSynchronize.argtypes = [C.c_void_p]
+        _hip = h
+    return _hip
 
 
 def load(path: str = ""):

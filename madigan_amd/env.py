@@ -159,8 +159,12 @@ class BatchedEnv:
         nbytes = self.lib.mgn_arena_bytes(C.byref(self.cfg))
         if nbytes == 0:
             raise ValueError("invalid env dimensions")
+        # the arena and, after it (256-B aligned), the (N, 10) valuation rows,
+        # so a host snapshot of both is one copy (Env)
+        self._val_off = (nbytes + 255) // 256 * 256
         with torch.cuda.device(self.device):
-            self.arena = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            self._arena_buf = torch.empty(self._val_off + self.N * 80, dtype=torch.uint8, device=self.device)
+            self.arena = self._arena_buf[:nbytes]
             self.stream = torch.cuda.current_stream(self.device)
         h = C.c_void_p()
         L.check(self.lib.mgn_create(C.byref(self.cfg), self._srcs, C.c_void_p(self.stream.cuda_stream),
@@ -172,8 +176,11 @@ class BatchedEnv:
         self.D = v.reward_dim
         self.nstep = v.nstep
         self._build_views()
-        self._val = torch.empty((self.N, 10), dtype=torch.float64, device=self.device)
+        self._val = self._arena_buf[self._val_off:].view(torch.float64).view(self.N, 10)
         self._traj_cache = {}
+        # host-array inputs (_dev): pinned twins of the staging buffers, copied
+        # asynchronously on the handle's stream, each guarded by an event
+        self._pinned = {}
         self._tape = None
         if spec.replay:
             self._attach_replay(replay_tape, int(replay_stride))
@@ -282,11 +289,38 @@ class BatchedEnv:
         if isinstance(x, torch.Tensor) and x.device == self.device and x.dtype == dtype \
                 and x.is_contiguous() and tuple(x.shape) == tuple(shape):
             return x
-        t = torch.as_tensor(np.asarray(x) if not isinstance(x, torch.Tensor) else x)
-        if t.numel() != int(np.prod(shape)):
-            raise ValueError(f"expected {int(np.prod(shape))} values, got {t.numel()}")
-        staging.view(-1)[: t.numel()].copy_(t.reshape(-1).to(dtype), non_blocking=False)
-        return staging.view(-1)[: t.numel()].view(shape)
+        n = int(np.prod(shape))
+        dst = staging.view(-1)[:n]
+        if isinstance(x, torch.Tensor) and x.device.type != "cpu":
+            if x.numel() != n:
+                raise ValueError(f"expected {n} values, got {x.numel()}")
+            dst.copy_(x.reshape(-1).to(dtype), non_blocking=False)
+            return dst.view(shape)
+        xa = np.asarray(x.numpy() if isinstance(x, torch.Tensor) else x).reshape(-1)
+        if xa.size != n:
+            raise ValueError(f"expected {n} values, got {xa.size}")
+        # a host array: into the pinned twin of the staging buffer (after the
+        # previous asynchronous copy out of it has run), then one asynchronous
+        # H2D copy on the handle's stream, ordered before the launch that
+        # reads it -- no synchronous pageable copy per step
+        key = staging.data_ptr()
+        twin = self._pinned.get(key)
+        if twin is None:
+            hb = torch.empty(staging.numel(), dtype=staging.dtype, pin_memory=True)
+            twin = (hb, hb.numpy(), torch.cuda.Event())
+            self._pinned[key] = twin
+        else:
+            twin[2].synchronize()
+        hb, hnp, ev = twin
+        hnp[:n] = xa  # numpy casts to the staging dtype (exact for the int8 / int32 / f64 inputs)
+        hip = L.hip()
+        st = C.c_void_p(self.stream.cuda_stream)
+        nbytes = n * hb.element_size()
+        if hip.hipMemcpyAsync(C.c_void_p(dst.data_ptr()), C.c_void_p(hb.data_ptr()), C.c_size_t(nbytes),
+                              1, st) != 0:  # hipMemcpyHostToDevice
+            raise RuntimeError("hipMemcpyAsync (input staging) failed")
+        ev.record(self.stream)
+        return dst.view(shape)
 
     # ---- API ------------------------------------------------------------------
     def set_broker(self, required_margin=None, maintenance_margin=None, slippage_rel=None,
@@ -685,10 +719,35 @@ class Env:
         self._spec = spec
         self._b = BatchedEnv(spec, 1, device=self._device, seed=self._seed,
                              init_cash=self._init_cash, **self._broker)
-        torch = _torch()
-        self._h_arena = torch.empty(self._b.arena.numel(), dtype=torch.uint8, pin_memory=True)
-        self._h_val = torch.empty((1, 10), dtype=torch.float64, pin_memory=True)
+        self._init_snapshot()
         self._snap = None
+
+    def _init_snapshot(self):
+        """The pinned host image of the handle's arena + valuation row and numpy
+        views of the fields the accessors read, built once (the snapshot then
+        costs one valuation launch, one copy and one synchronise)."""
+        torch = _torch()
+        b = self._b
+        n = b._val_off + 80
+        self._h_buf = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        blob = self._h_buf.numpy()
+        base = b.arena.data_ptr()
+
+        def arr(ptr, dtype, shape):
+            off = ptr - base
+            k = int(np.prod(shape)) * np.dtype(dtype).itemsize
+            return blob[off:off + k].view(dtype).reshape(shape)
+        v, A, F = b._v, b.A, b.F
+        o = v.out
+        self._h_views = dict(
+            val=blob[b._val_off:b._val_off + 80].view(np.float64),
+            prices=arr(v.prices, np.float64, (A,)), ledger=arr(v.ledger, np.float64, (A,)),
+            mean_entry=arr(v.mean_entry, np.float64, (A,)), timestamp=arr(v.timestamp, np.uint64, (1,)),
+            reward=arr(o.reward, np.float64, (1,)), done=arr(o.done, np.uint8, (1,)),
+            obs_price=arr(o.obs_price, np.float64, (F,)), obs_port=arr(o.obs_port, np.float64, (A + 1,)),
+            obs_ts=arr(o.timestamp, np.uint64, (1,)), tprice=arr(o.tprice, np.float64, (A,)),
+            tunits=arr(o.tunits, np.float64, (A,)), tcost=arr(o.tcost, np.float64, (A,)),
+            risk=arr(o.risk, np.uint8, (A,)), margin_call=arr(o.margin_call, np.uint8, (1,)))
 
     # ---- host snapshot of the device state ------------------------------------------
     def _dirty(self):
@@ -699,30 +758,18 @@ class Env:
             return self._snap
         b = self._b
         L.check(b.lib.mgn_valuation(b.h, C.c_void_p(b._val.data_ptr())), b.h)
-        with _torch().cuda.stream(b.stream):
-            self._h_arena.copy_(b.arena, non_blocking=True)
-            self._h_val.copy_(b._val, non_blocking=True)
-        b.stream.synchronize()
-        blob = self._h_arena.numpy()
-        base = b.arena.data_ptr()
-
-        def arr(ptr, dtype, shape):
-            off = ptr - base
-            n = int(np.prod(shape)) * np.dtype(dtype).itemsize
-            return blob[off:off + n].view(dtype).reshape(shape)
-        v, A, F = b._v, b.A, b.F
-        o = v.out
-        self._snap = dict(
-            val=dict(zip(VALUATION_FIELDS, self._h_val.numpy()[0])),
-            prices=arr(v.prices, np.float64, (A,)), ledger=arr(v.ledger, np.float64, (A,)),
-            mean_entry=arr(v.mean_entry, np.float64, (A,)),
-            timestamp=int(arr(v.timestamp, np.uint64, (1,))[0]),
-            reward=float(arr(o.reward, np.float64, (1,))[0]), done=bool(arr(o.done, np.uint8, (1,))[0]),
-            obs_price=arr(o.obs_price, np.float64, (F,)), obs_port=arr(o.obs_port, np.float64, (A + 1,)),
-            obs_ts=int(arr(o.timestamp, np.uint64, (1,))[0]),
-            tprice=arr(o.tprice, np.float64, (A,)), tunits=arr(o.tunits, np.float64, (A,)),
-            tcost=arr(o.tcost, np.float64, (A,)), risk=arr(o.risk, np.uint8, (A,)),
-            margin_call=bool(arr(o.margin_call, np.uint8, (1,))[0]))
+        hip = L.hip()
+        st = C.c_void_p(b.stream.cuda_stream)
+        if hip.hipMemcpyAsync(C.c_void_p(self._h_buf.data_ptr()), C.c_void_p(b._arena_buf.data_ptr()),
+                              C.c_size_t(self._h_buf.numel()), 2, st) != 0 or \
+                hip.hipStreamSynchronize(st) != 0:  # hipMemcpyDeviceToHost
+            raise RuntimeError("snapshot copy failed")
+        h = self._h_views
+        # the arrays stay views of the pinned image: State / accessors copy them
+        self._snap = dict(h, val=dict(zip(VALUATION_FIELDS, h["val"].tolist())),
+                          timestamp=int(h["timestamp"][0]), reward=float(h["reward"][0]),
+                          done=bool(h["done"][0]), obs_ts=int(h["obs_ts"][0]),
+                          margin_call=bool(h["margin_call"][0]))
         return self._snap
 
     # ---- setters (Env.h:94-111) ------------------------------------------------

@@ -154,8 +154,25 @@ def hip():
         h.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
         h.hipStreamSynchronize.restype = C.c_int
         h.hipStreamSynchronize.argtypes = [C.c_void_p]
+        h.hipPointerGetAttributes.restype = C.c_int
+        h.hipPointerGetAttributes.argtypes = [C.c_void_p, C.c_void_p]
         _hip = h
     return _hip
+
+
+class _PtrAttr(C.Structure):  # hipPointerAttribute_t (hip_runtime_api.h)
+    _fields_ = [("type", C.c_int), ("device", C.c_int), ("devicePointer", C.c_void_p),
+                ("hostPointer", C.c_void_p), ("isManaged", C.c_int), ("allocationFlags", C.c_uint)]
+
+
+def device_view(host_ptr: int) -> int:
+    """The device address of pinned host memory the kernels may read in place
+    (hipHostMalloc memory is mapped into the device address space), or 0 when
+    the runtime reports none."""
+    a = _PtrAttr()
+    if hip().hipPointerGetAttributes(C.byref(a), C.c_void_p(host_ptr)) != 0:
+        return 0
+    return int(a.devicePointer or 0)
 
 
 def load(path: str = ""):

@@ -721,6 +721,7 @@ class Env:
                              init_cash=self._init_cash, **self._broker)
         self._init_snapshot()
         self._snap = None
+        self._vsnap = None
 
     def _init_snapshot(self):
         """The pinned host image of the handle's arena + valuation row and numpy
@@ -739,6 +740,12 @@ class Env:
             return blob[off:off + k].view(dtype).reshape(shape)
         v, A, F = b._v, b.A, b.F
         o = v.out
+        # step inputs read by the kernel in place from pinned host memory (Env.step
+        # synchronises before it returns, so the next write never races a read)
+        self._h_units = torch.zeros(max(A, 1), dtype=torch.float64, pin_memory=True)
+        self._h_aidx = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self._d_units = L.device_view(self._h_units.data_ptr())
+        self._d_aidx = L.device_view(self._h_aidx.data_ptr())
         self._h_views = dict(
             val=blob[b._val_off:b._val_off + 80].view(np.float64),
             prices=arr(v.prices, np.float64, (A,)), ledger=arr(v.ledger, np.float64, (A,)),
@@ -752,25 +759,39 @@ class Env:
     # ---- host snapshot of the device state ------------------------------------------
     def _dirty(self):
         self._snap = None
+        self._vsnap = None
 
     def _snapshot(self) -> dict:
         if self._snap is not None:
             return self._snap
         b = self._b
-        L.check(b.lib.mgn_valuation(b.h, C.c_void_p(b._val.data_ptr())), b.h)
         hip = L.hip()
         st = C.c_void_p(b.stream.cuda_stream)
         if hip.hipMemcpyAsync(C.c_void_p(self._h_buf.data_ptr()), C.c_void_p(b._arena_buf.data_ptr()),
-                              C.c_size_t(self._h_buf.numel()), 2, st) != 0 or \
+                              C.c_size_t(b._val_off), 2, st) != 0 or \
                 hip.hipStreamSynchronize(st) != 0:  # hipMemcpyDeviceToHost
             raise RuntimeError("snapshot copy failed")
         h = self._h_views
         # the arrays stay views of the pinned image: State / accessors copy them
-        self._snap = dict(h, val=dict(zip(VALUATION_FIELDS, h["val"].tolist())),
-                          timestamp=int(h["timestamp"][0]), reward=float(h["reward"][0]),
+        self._snap = dict(h, timestamp=int(h["timestamp"][0]), reward=float(h["reward"][0]),
                           done=bool(h["done"][0]), obs_ts=int(h["obs_ts"][0]),
                           margin_call=bool(h["margin_call"][0]))
         return self._snap
+
+    def _valuation(self) -> dict:
+        """Portfolio valuation (k_valuation) of the current state, launched
+        only when an accessor needs it (Env.step's own returns do not)."""
+        if self._vsnap is not None:
+            return self._vsnap
+        b = self._b
+        L.check(b.lib.mgn_valuation(b.h, C.c_void_p(b._val.data_ptr())), b.h)
+        hip = L.hip()
+        st = C.c_void_p(b.stream.cuda_stream)
+        if hip.hipMemcpyAsync(C.c_void_p(self._h_buf.data_ptr() + b._val_off), C.c_void_p(b._val.data_ptr()),
+                              C.c_size_t(80), 2, st) != 0 or hip.hipStreamSynchronize(st) != 0:
+            raise RuntimeError("valuation copy failed")
+        self._vsnap = dict(zip(VALUATION_FIELDS, self._h_views["val"].tolist()))
+        return self._vsnap
 
     # ---- setters (Env.h:94-111) ------------------------------------------------
     def setRequiredMargin(self, requiredMargin):
@@ -847,7 +868,14 @@ class Env:
             if not 0 <= idx < self.nAssets:
                 raise IndexError(f"asset index {idx} out of range")
             self._feed_external()
-            self._b.step(units=np.array([float(units)]), asset_idx=np.array([idx], np.int32))
+            if self._d_units and self._d_aidx:
+                self._h_units.numpy()[0] = float(units)
+                self._h_aidx.numpy()[0] = idx
+                b = self._b
+                L.check(b.lib.mgn_step(b.h, L.STEP_SINGLE, C.c_void_p(self._d_units),
+                                       C.c_void_p(self._d_aidx)), b.h)
+            else:
+                self._b.step(units=np.array([float(units)]), asset_idx=np.array([idx], np.int32))
             self._dirty()
             o = self._snapshot()
             resp = BrokerResponse(float(o["tprice"][idx]), float(o["tunits"][idx]),
@@ -859,7 +887,12 @@ class Env:
             if units.shape[0] != self.nAssets:
                 raise ValueError(f"units must have {self.nAssets} entries, got {units.shape[0]}")
             self._feed_external()
-            self._b.step(units=units.reshape(1, -1))
+            if self._d_units:
+                self._h_units.numpy()[:self.nAssets] = units
+                b = self._b
+                L.check(b.lib.mgn_step(b.h, L.STEP_UNITS, C.c_void_p(self._d_units), None), b.h)
+            else:
+                self._b.step(units=units.reshape(1, -1))
             self._dirty()
             o = self._snapshot()
             resp = BrokerResponse(o["tprice"].copy(), o["tunits"].copy(), o["tcost"].copy(),
@@ -869,7 +902,7 @@ class Env:
 
     # ---- accessors (env.cpp:872-969) --------------------------------------------------
     def _vals(self):
-        return self._snapshot()["val"]
+        return self._valuation()
 
     @property
     def currentPrices(self):

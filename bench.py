@@ -587,6 +587,9 @@ def windowed(args, world, rank, dev):
     import ctypes as C
     from madigan_amd import _lib as L
     lib, h = env.lib, env.h
+    if args.schedule != "auto":
+        L.check(lib.mgn_set_schedule(h, {"single": L.SCHED_SINGLE, "duo": L.SCHED_DUO,
+                                         "trio": L.SCHED_TRIO}[args.schedule]), h)
     if args.win_overlap:
         # gathers on a second stream, the history double-buffered: launch L's
         # gather (HBM-bound) runs beside launch L+1's steps (latency-bound).

@@ -338,7 +338,7 @@ int mgn_get_layout(const mgn_env *env);
  * in a generator wave that shares the SIMD; 2..16 assets, generator sources
  * or a replay tape, n-step rings that fit LDS); MGN_SCHED_TRIO = k_step_trio
  * (generator, ledger and finish waves pipelined one step apart, `done`
- * speculated; 2..8 assets, generator sources, nstep 1, no window);
+ * speculated; 2..8 assets, generator sources, nstep 1);
  * MGN_SCHED_AUTO (default) = TRIO, else DUO where eligible and the layout is
  * one asset per lane.  Results are bit-identical; only speed changes. */
 enum { MGN_SCHED_AUTO = 0, MGN_SCHED_SINGLE = 1, MGN_SCHED_DUO = 2, MGN_SCHED_TRIO = 3 };

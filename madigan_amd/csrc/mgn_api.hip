@@ -329,12 +329,12 @@ bool duo_eligible(const mgn_env* e) {
   }
   return true;
 }
-// the three-role kernel: 2..8 assets, generator sources, one-step rewards, no
-// window (its speculative steps would need the window rows rolled back)
+// the three-role kernel: 2..8 assets, generator sources, one-step rewards
+// (windows included: the confirmed steps' rows are pushed by its finish role)
 bool trio_eligible(const mgn_env* e) {
   // (its output indices are k x a 32-bit stride: N (A + 1) and N F fit 32 bits)
   const uint64_t row = (uint64_t)(e->A + 1 > e->F ? e->A + 1 : e->F);
-  return e->apad >= 2 && e->apad <= 8 && !e->cfg.aux && !e->replay && e->cfg.nstep == 1 && e->W == 0 &&
+  return e->apad >= 2 && e->apad <= 8 && !e->cfg.aux && !e->replay && e->cfg.nstep == 1 &&
          (uint64_t)e->N * row < (1ull << 32);
 }
 // automatic: where the single-role kernel would run one lane per asset (small
@@ -966,7 +966,7 @@ int mgn_set_schedule(mgn_env* e, int32_t schedule) {
                 "the two-role kernel needs 2..16 assets, no multi-component source, n-step rings within LDS");
   if (schedule == MGN_SCHED_TRIO && !trio_eligible(e))
     return fail(e, MGN_ERR_CONFIG,
-                "the three-role kernel needs 2..8 assets, generator sources, nstep 1, no window");
+                "the three-role kernel needs 2..8 assets, generator sources, nstep 1");
   e->sched = schedule;
   auto_layout(e);
   return MGN_OK;

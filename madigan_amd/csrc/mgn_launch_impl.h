@@ -79,7 +79,15 @@ void launch_trio(const StepArgs& a) {
   };
   const bool disc = a.in_kind == IN_DISCRETE;
   const uint32_t om = traj_mask(a.out);
-  if (disc && om == O_STD) {  // the agent loop's output set
+  if (a.p.W > 0) {  // window handles: the ring / history pushes (runtime output mask)
+    if (disc) {
+      if (a.p.reqm_one) go(k_step_trio<S, true, true, 0, true>);
+      else go(k_step_trio<S, false, true, 0, true>);
+    } else {
+      if (a.p.reqm_one) go(k_step_trio<S, true, false, 0, true>);
+      else go(k_step_trio<S, false, false, 0, true>);
+    }
+  } else if (disc && om == O_STD) {  // the agent loop's output set
     if (a.p.reqm_one) go(k_step_trio<S, true, true, O_STD>);
     else go(k_step_trio<S, false, true, O_STD>);
   } else if (disc && om == O_ALL) {

@@ -59,7 +59,10 @@ constexpr int TRIO_W = 256;  // lanes per role
 #define MGN_TRIO_PF 1
 #endif
 
-enum { TR_STEP = 1, TR_ANYMC = 2, TR_MCALL = 4 };
+// TR_REFILL (WIN): the iteration's tick was an auto-reset refill tick
+// (initialize_history's env.step(), preprocessor.py:191-194): F pushes its
+// window row, nothing else
+enum { TR_STEP = 1, TR_ANYMC = 2, TR_MCALL = 4, TR_REFILL = 8 };
 
 template <int S>
 struct TrioShared {
@@ -79,8 +82,15 @@ struct TrioShared {
   int32_t more[3];
 };
 
-// OMC: the output set when known at compile time (O_ALL, O_STD), else 0
-template <int S, bool RQ1, bool DISC, uint32_t OMC = 0>
+// OMC: the output set when known at compile time (O_ALL, O_STD), else 0.
+// WIN: the handle keeps a window (StackerDiscrete ring, and the launch
+// history under mgn_rollout_hist).  The window rows are pushed by F, which
+// only ever sees confirmed steps, so a rolled-back speculative step leaves no
+// row; an auto-reset refills the window with W ticks (the rollback
+// iteration's reset tick and W - 1 more) during which L does not step and F
+// pushes one refill row per tick -- the rows, order and history marks of
+// k_step_duo / k_step.
+template <int S, bool RQ1, bool DISC, uint32_t OMC = 0, bool WIN = false>
 __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj out, int in_kind_rt,
                                                           const double* __restrict__ units_in,
                                                           const int32_t* __restrict__ aidx_in,
@@ -120,6 +130,7 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
   const MGN_G int8_t* act_lane = vptr(act_in) + li;
   double ep_ret = 0., ep_len = 0., n_done = 0.;  // F
   double shA = 0., shB = 0.;                     // F
+  int32_t rhead = 0, rlen = 0;                   // F (WIN): the window ring
   if (role == 0) {
     if (s.valid[0]) {
       s.sx[0] = p.sx[li];
@@ -141,6 +152,10 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
     ep_ret = p.ep[(size_t)envc * 2];
     ep_len = p.ep[(size_t)envc * 2 + 1];
     n_done = p.epstats[(size_t)envc * 4 + 3];
+    if (WIN) {
+      rhead = p.rhead[envc];
+      rlen = p.rlen[envc];
+    }
     if (p.D == 1) {
       shA = p.sA[envc];
       shB = p.sB[envc];
@@ -193,6 +208,7 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
     unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0;
     int jn = 0;
 #endif
+    int gpend = 0;  // WIN: refill ticks still to come after the reset tick
     for (int j = 0;; ++j) {
       const int cur = j & 1, prv = cur ^ 1;
       MGN_T(T0);
@@ -200,7 +216,12 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
       if (live) {
         const bool rst = sh.reset[prv][el] != 0;
         const bool prev_step = (sh.rFlags[prv][el] & TR_STEP) != 0;
-        if (rst) {
+        if (WIN && !rst && gpend > 0) {
+          // a refill tick (not speculative: the reset is confirmed)
+          gen_tick<M, false, false>(s, p, env, ts);
+          ts = ts + 1;
+          gpend -= 1;
+        } else if (rst) {
           if (prev_step) {  // roll the speculative tick back
             s.P[0] = svP;
             s.sx[0] = svSx;
@@ -215,6 +236,7 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
           src_reset<M, false>(s, p, env, ts);
           gen_tick<M, false, false>(s, p, env, ts);
           ts = ts + 1;
+          if (WIN) gpend = p.W - 1;
         } else if (k < K) {
           svP = s.P[0];
           svSx = s.sx[0];
@@ -283,6 +305,7 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
     Sums sa = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
     drain_vmem();
     int k = 0;
+    int lpend = 0;  // WIN: refill ticks still to come after the reset tick
     __builtin_amdgcn_s_setprio(MGN_TRIO_PL);  // the orders are the critical path
 #ifdef MGN_STAMPS
     unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0;
@@ -292,6 +315,10 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
       MGN_T(T0);
       const bool rst = live && sh.reset[prv][el] != 0;
       const bool prev_step = (sh.rFlags[prv][el] & TR_STEP) != 0;
+      // WIN: this iteration's tick refills the window (the reset tick or one
+      // of the W - 1 after it): no step
+      const bool refill = WIN && live && (rst || lpend > 0);
+      if (WIN && !rst && lpend > 0) lpend -= 1;
       // prices of the last tick (the step's pre-tick prices; iteration 0:
       // the handle's current prices)
       if (j > 0 && live && s.valid[0]) s.P[0] = sh.price[prv][l];
@@ -304,8 +331,9 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
         s.mep[0] = 0.;
         s.Bm[0] = 0.;
         cash = p.init_cash;
+        if (WIN) lpend = p.W - 1;
       }
-      const bool stepping = live && !rst && k < K;
+      const bool stepping = live && !rst && !refill && k < K;
       const int act_now = act_cur;
       if (in_kind == IN_DISCRETE && K > 0) {
         // the action of the next step this lane runs (k + 1 if this one
@@ -384,9 +412,18 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
         flags = TR_STEP | (any_mc ? TR_ANYMC : 0) | (mcall ? TR_MCALL : 0);
         k += 1;
       }
+      if (WIN && refill) {
+        // the refill row's portfolio (the fresh Broker's): F evaluates it
+        sh.rL[cur][l] = s.L[0];
+        if (ls == 0) {
+          sh.rCash[cur][el] = cash;
+          sh.rB[cur][el] = 0.;  // canonical sum of the fresh Broker's borrowed margins (+0)
+        }
+        flags = TR_REFILL;
+      }
       if (ls == 0) sh.rFlags[cur][el] = flags;
       // another iteration: F evaluates this step, or steps remain
-      if (live && (stepping || rst || k < K)) sh.more[j % 3] = 1;
+      if (live && (stepping || rst || refill || k < K || (WIN && lpend > 0))) sh.more[j % 3] = 1;
       MGN_T(T1);
       __syncthreads();
       MGN_T(T2);
@@ -419,6 +456,18 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
   const GTraj ov = traj_vgpr<OMC>(out);
   GState gs;
   gs.epstats = vptr(p.epstats);
+  // WIN: the ring / launch-history pointers (global, as every store of the
+  // loop) and the history cursor: next row, the step its rows belong to
+  int hcnt = p.W, klast = 0;
+  MGN_G int32_t *ghend = nullptr, *ghlen = nullptr;
+  if (WIN) {
+    gs.ring = vptr(p.ring);
+    gs.ring_ts = vptr(p.ring_ts);
+    gs.hist = vptr(p.hist);
+    gs.hist_ts = vptr(p.hist_ts);
+    ghend = vptr(p.hend);
+    ghlen = vptr(p.hlen);
+  }
   p.init_cash = in_vgpr(p.init_cash);
   p.mainM = in_vgpr(p.mainM);
   p.eta = in_vgpr(p.eta);
@@ -442,6 +491,42 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
                  sNA1 = (uint32_t)p.N * (uint32_t)(A + 1);
   const size_t bA = (size_t)env * A + s.asset[0], bP = (size_t)env * p.F + s.asset[0],
                bO = (size_t)env * (A + 1);
+  // WIN: StackerDiscrete.stream_state of a State (preprocessor.py:172-175):
+  // log-normalised (as the ring stores them) prices, ledgerNormedFull and the
+  // timestamp into ring slot head + 1 and history row hcnt (ring_push's
+  // values; duo_store's order)
+  const auto push_row = [&](double P, double portA, double port0, uint64_t tsv, int kmark) {
+    rhead = (rhead + 1) % p.W;
+    if (rlen < p.W) rlen += 1;
+    const int R = p.F + A + 1;
+    MGN_G double* row = gs.ring + ((size_t)env * p.W + rhead) * R;
+    MGN_G double* hrow = p.hist ? gs.hist + ((size_t)env * p.hrows + hcnt) * R : nullptr;
+    if (s.valid[0]) {
+      const double fv = p.ring_log ? log_norm(P) : P;
+      ost(row + s.asset[0], fv);
+      ost(row + (p.F + 1 + s.asset[0]), portA);
+      if (hrow) {
+        ost(hrow + s.asset[0], fv);
+        ost(hrow + (p.F + 1 + s.asset[0]), portA);
+      }
+    }
+    if (ls == 0) {
+      ost(row + p.F, port0);
+      ost(gs.ring_ts + ((size_t)env * p.W + rhead), tsv);
+      if (hrow) {
+        ost(hrow + p.F, port0);
+        ost(gs.hist_ts + ((size_t)env * p.hrows + hcnt), tsv);
+      }
+    }
+    if (hrow) {  // hist_mark
+      klast = kmark;
+      hcnt += 1;
+      if (ls == 0) {
+        ost(ghend + ((size_t)klast * p.N + env), (int32_t)hcnt);
+        ost(ghlen + ((size_t)klast * p.N + env), (int32_t)rlen);
+      }
+    }
+  };
   drain_vmem();
   __builtin_amdgcn_s_setprio(MGN_TRIO_PF);
 #ifdef MGN_STAMPS
@@ -549,6 +634,13 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
         }
       }
 #endif
+      if (WIN) {
+        push_row(P, portA, port0, (uint64_t)sh.ts[prv][el], k);
+        if (done && p.auto_reset) {  // a reset empties the window before its refill ticks
+          rlen = 0;
+          rhead = p.W - 1;
+        }
+      }
       // episode statistics
       ep_ret += reward;
       ep_len += 1;
@@ -565,6 +657,17 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
         ep_len = 0;
         if (p.auto_reset) rst_out = 1;
       }
+    }
+    if (WIN && live && (flags & TR_REFILL)) {
+      // a refill tick's row: the fresh Broker's portfolio on the tick's prices
+      // (the sums ring_push / k_step_duo's refill record evaluate)
+      const double Pf = sh.price[prv][l];
+      const double Lf = sh.rL[prv][l];
+      const double cashf = sh.rCash[prv][el], bf = sh.rB[prv][el];
+      double tlp[M];
+      tlp[0] = Lf * Pf;
+      const double eq = (cashf + canon<M, S>(tlp)) - bf;
+      push_row(Pf, (Lf * Pf) / eq, (cashf - bf) / eq, (uint64_t)sh.ts[prv][el], klast);
     }
     if (ls == 0) sh.reset[cur][el] = rst_out;
     if (rst_out) sh.more[j % 3] = 1;  // the reset tick runs next iteration
@@ -585,6 +688,10 @@ __global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj ou
 #endif
   if (!live) return;
   if (ls == 0) {
+    if (WIN) {
+      p.rhead[env] = rhead;
+      p.rlen[env] = rlen;
+    }
     p.ep[(size_t)env * 2] = ep_ret;
     p.ep[(size_t)env * 2 + 1] = ep_len;
     if (D == 1) {

@@ -150,7 +150,7 @@ def test_c4_composite_ppc_log_window(gpu):
     A = len(src)
     g, orc = _windowed_pair(src, N, W, "log", "PPC", cosine_temp=0.01,
                             desired_portfolio=[1.0] + [0.0] * A, seed=0x6D6164 + 4)
-    assert g.lib.mgn_get_schedule(g.h) == L.SCHED_DUO
+    assert g.lib.mgn_get_schedule(g.h) == L.SCHED_TRIO
     acts = g.generate_actions(K, seed=0x6D6164)
     _check_windows(g, orc, acts, K, "log", "C4")
     state_check(g, orc, "C4")

@@ -313,7 +313,7 @@ def test_schedules_bit_identical(gpu, A, kw):
     rng = np.random.default_rng(A)
     units = rng.normal(0, 3e3, (N, A))
     res = []
-    trio_ok = A <= 8 and not kw.get("window") and kw.get("nstep_return", 1) == 1
+    trio_ok = A <= 8 and kw.get("nstep_return", 1) == 1
     for sched in (L.SCHED_SINGLE, L.SCHED_DUO) + ((L.SCHED_TRIO,) if trio_ok else ()):
         g = BatchedEnv(spec, N, **base, **kw)
         L.check(g.lib.mgn_set_schedule(g.h, sched), g.h)
@@ -344,7 +344,9 @@ def test_schedules_bit_identical(gpu, A, kw):
 @pytest.mark.gpu
 @pytest.mark.parametrize("norm,W,N,sched", [(None, 8, 96, "duo"), ("log", 8, 96, "duo"),
                                             ("lookback", 6, 50, "single"), ("log", 8, 70, "single"),
-                                            (None, 256, 20, "duo"), ("lookback_log", 1024, 12, "duo")])
+                                            (None, 256, 20, "duo"), ("lookback_log", 1024, 12, "duo"),
+                                            (None, 8, 96, "trio"), ("log", 16, 70, "trio"),
+                                            ("lookback_log", 256, 20, "trio")])
 def test_rollout_window_per_step(gpu, norm, W, N, sched):
     """mgn_rollout_window per_step (K steps in one launch, the launch history,
     then every step's window) against the oracle's window after every step;
@@ -360,7 +362,10 @@ def test_rollout_window_per_step(gpu, norm, W, N, sched):
 
     def handle():
         g, orc = make_pair(src, N, **kw)
-        L.check(g.lib.mgn_set_schedule(g.h, L.SCHED_DUO if sched == "duo" else L.SCHED_SINGLE), g.h)
+        L.check(g.lib.mgn_set_schedule(g.h, {"duo": L.SCHED_DUO, "trio": L.SCHED_TRIO,
+                                              "single": L.SCHED_SINGLE}[sched]), g.h)
+        assert g.lib.mgn_get_schedule(g.h) == {"duo": L.SCHED_DUO, "trio": L.SCHED_TRIO,
+                                               "single": L.SCHED_SINGLE}[sched]
         g.reset()
         orc.reset()
         return g, orc
@@ -402,7 +407,7 @@ def test_rollout_window_per_step(gpu, norm, W, N, sched):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sched", ["duo", "single"])
+@pytest.mark.parametrize("sched", ["duo", "single", "trio"])
 def test_window_stream_overlap(gpu, sched):
     """Gathers on a second stream (mgn_set_window_stream): the launch history
     alternates buffers, launch L's gather overlaps launch L+1's steps; every
@@ -417,7 +422,8 @@ def test_window_stream_overlap(gpu, sched):
               window=W, norm_type=None, auto_reset=1)
     src = trendou_sources(A, [0.2, 2, 6, 0.05, 0.2, 5.0, 0.15, 0.3, 0.2, 0.99])
     g, orc = make_pair(src, N, **kw)
-    L.check(g.lib.mgn_set_schedule(g.h, L.SCHED_DUO if sched == "duo" else L.SCHED_SINGLE), g.h)
+    L.check(g.lib.mgn_set_schedule(g.h, {"duo": L.SCHED_DUO, "trio": L.SCHED_TRIO,
+                                          "single": L.SCHED_SINGLE}[sched]), g.h)
     g.reset()
     orc.reset()
     ws = torch.cuda.Stream(g.device)

@@ -10,7 +10,8 @@ for r in $(seq 1 ${R:-3}); do
   for v in $VARIANTS; do
     name=${v%%=*}; path=${v#*=}
     [ "$path" = base ] && path=madigan_amd/libmadigan_hip.so
-    MADIGAN_LIB_PATH=$path timeout -k 10 200 python bench.py --workload $wl --no-cpu-baseline > $O/$wl.$name.$r.json 2>> $O/err.log || { echo "fail $name"; tail -5 $O/err.log; exit 1; }
+    extra=""; case "$name" in duo|trio|single) extra="--schedule $name";; esac
+    MADIGAN_LIB_PATH=$path timeout -k 10 200 python bench.py --workload $wl --no-cpu-baseline $extra > $O/$wl.$name.$r.json 2>> $O/err.log || { echo "fail $name"; tail -5 $O/err.log; exit 1; }
     python -c "import json;a=json.load(open('$O/$wl.$name.$r.json'));print('$wl', '$name', $r, 'value', round(a['value']/1e6,1), 'step_us', round(a['step_launch_avg_us'],1), 'gather_us', round(a['roofline']['avg_launch_us'],1), 'episodes', a['episodes_completed'])"
   done
   done

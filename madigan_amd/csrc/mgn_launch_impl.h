@@ -71,15 +71,33 @@ void launch_duo(const StepArgs& a) {
 // three-role pipelined step kernel (mgn_trio.h): S = APAD lanes per env per role
 template <int S>
 void launch_trio(const StepArgs& a) {
-  constexpr int epb = TRIO_W / S;
+  // one wave per role when 256 lanes per role would leave CUs idle
+  const bool small = (long long)a.p.N * S < 256LL * TRIO_W;
+  const int epb = (small ? 64 : TRIO_W) / S;
   const int grid = (a.p.N + epb - 1) / epb;
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(TRIO_BLOCK), 0, a.stream, a.p, a.out, a.in_kind,
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(small ? 192 : TRIO_BLOCK), 0, a.stream, a.p, a.out, a.in_kind,
                        a.units, a.aidx, a.act, a.K);
   };
   const bool disc = a.in_kind == IN_DISCRETE;
   const uint32_t om = traj_mask(a.out);
-  if (a.p.W > 0) {  // window handles: the ring / history pushes (runtime output mask)
+  if (small) {  // runtime output mask, window or not
+    if (a.p.W > 0) {
+      if (disc) {
+        if (a.p.reqm_one) go(k_step_trio<S, true, true, 0, true, 64>);
+        else go(k_step_trio<S, false, true, 0, true, 64>);
+      } else {
+        if (a.p.reqm_one) go(k_step_trio<S, true, false, 0, true, 64>);
+        else go(k_step_trio<S, false, false, 0, true, 64>);
+      }
+    } else if (disc) {
+      if (a.p.reqm_one) go(k_step_trio<S, true, true, 0, false, 64>);
+      else go(k_step_trio<S, false, true, 0, false, 64>);
+    } else {
+      if (a.p.reqm_one) go(k_step_trio<S, true, false, 0, false, 64>);
+      else go(k_step_trio<S, false, false, 0, false, 64>);
+    }
+  } else if (a.p.W > 0) {  // window handles: the ring / history pushes (runtime output mask)
     if (disc) {
       if (a.p.reqm_one) go(k_step_trio<S, true, true, 0, true>);
       else go(k_step_trio<S, false, true, 0, true>);

@@ -40,6 +40,9 @@ namespace mgn {
 
 constexpr int TRIO_BLOCK = 768;
 constexpr int TRIO_W = 256;  // lanes per role
+// TW = 64 (one wave per role, 192-thread workgroups): small batches, whose
+// 256-lane workgroups would leave CUs idle (C2: 4096 envs x 4 assets fill 64
+// of 256 CUs at 256 lanes per role, all of them at 64)
 
 // which role stores what, and the roles' issue priorities (tuning switches;
 // the defaults are the measured best)
@@ -64,8 +67,9 @@ constexpr int TRIO_W = 256;  // lanes per role
 // window row, nothing else
 enum { TR_STEP = 1, TR_ANYMC = 2, TR_MCALL = 4, TR_REFILL = 8 };
 
-template <int S>
+template <int S, int TW = TRIO_W>
 struct TrioShared {
+  static constexpr int TRIO_W = TW;
   static constexpr int EPB = TRIO_W / S;
   // prices after the iteration's tick (G -> L, F)
   double price[2][TRIO_W];
@@ -90,16 +94,18 @@ struct TrioShared {
 // iteration's reset tick and W - 1 more) during which L does not step and F
 // pushes one refill row per tick -- the rows, order and history marks of
 // k_step_duo / k_step.
-template <int S, bool RQ1, bool DISC, uint32_t OMC = 0, bool WIN = false>
-__global__ __launch_bounds__(TRIO_BLOCK) void k_step_trio(KParams p, mgn_traj out, int in_kind_rt,
+template <int S, bool RQ1, bool DISC, uint32_t OMC = 0, bool WIN = false, int TW = TRIO_W>
+__global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out, int in_kind_rt,
                                                           const double* __restrict__ units_in,
                                                           const int32_t* __restrict__ aidx_in,
                                                           const int8_t* __restrict__ act_in, int K) {
   warm_kernargs<(int)(sizeof(KParams) + sizeof(mgn_traj) + 48)>();
   const int in_kind = DISC ? IN_DISCRETE : in_kind_rt;
   constexpr int M = 1;
+  constexpr int TRIO_W = TW;
+  constexpr int TRIO_BLOCK = 3 * TW;
   constexpr int EPB = TRIO_W / S;
-  __shared__ TrioShared<S> sh;
+  __shared__ TrioShared<S, TW> sh;
   __shared__ EnvRecs<S> recs[EPB];
   __shared__ mgn_asset_source s_src[S];
   __shared__ double s_tgt[MGN_MAX_ASSETS + 1];

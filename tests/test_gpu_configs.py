@@ -143,9 +143,12 @@ def test_c2_window64_4096(gpu):
     state_check(g, orc, "C2")
 
 
-def test_c4_composite_ppc_log_window(gpu):
+@pytest.mark.parametrize("N", [2048, 8192])
+def test_c4_composite_ppc_log_window(gpu, N):
+    """2048 envs run the three-role kernel at one wave per role, 8192 (the
+    bench shape) at 256 lanes per role."""
     from madigan_amd import _lib as L
-    N, W, K = 2048, 64, 64
+    W, K = 64, 64
     src = composite_sources()
     A = len(src)
     g, orc = _windowed_pair(src, N, W, "log", "PPC", cosine_temp=0.01,

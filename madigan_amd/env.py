@@ -296,7 +296,7 @@ class BatchedEnv:
                 raise ValueError(f"expected {n} values, got {x.numel()}")
             dst.copy_(x.reshape(-1).to(dtype), non_blocking=False)
             return dst.view(shape)
-        xa = np.asarray(x.numpy() if isinstance(x, torch.Tensor) else x).reshape(-1)
+        xa = np.asarray(x.detach().numpy() if isinstance(x, torch.Tensor) else x).reshape(-1)
         if xa.size != n:
             raise ValueError(f"expected {n} values, got {xa.size}")
         # a host array: into the pinned twin of the staging buffer (after the

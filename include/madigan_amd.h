@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MGN_ABI_VERSION 6
+#define MGN_ABI_VERSION 7
 #define MGN_MAX_ASSETS 64
 #define MGN_MAX_NSTEP 64
 
@@ -344,10 +344,31 @@ int mgn_get_layout(const mgn_env *env);
 enum { MGN_SCHED_AUTO = 0, MGN_SCHED_SINGLE = 1, MGN_SCHED_DUO = 2, MGN_SCHED_TRIO = 3 };
 int mgn_set_schedule(mgn_env *env, int32_t schedule);
 int mgn_get_schedule(const mgn_env *env);
-/* DIAGNOSTIC ONLY (timing ablations, outputs become wrong): bit 0 skips the
- * Broker rounds, bit 1 the generators, bit 2 the output stores, bit 3 the
- * logarithms of the agent reward.  Never set in product or parity runs. */
-int mgn_set_ablation(mgn_env *env, int32_t flags);
+/* Broker / Portfolio operations outside a step (no tick, no reward): the
+ * drop-in's env.broker / env.portfolio objects, per env on device.
+ *   MGN_OP_BROKER_UNITS  Broker::handleTransaction(units) / handleAction /
+ *                        handleEvent (Broker.cpp:144-158, Broker.h:96-101):
+ *                        units_dev (N, A); responses (N, A)
+ *   MGN_OP_BROKER_SINGLE Broker::handleTransaction(assetIdx, units)
+ *                        (Broker.cpp:124-142): asset_idx_dev, units_dev (N);
+ *                        responses (N)
+ *   MGN_OP_BROKER_CLOSE  Broker::close(assetIdx) (Broker.cpp:160-169): the
+ *                        position closed at slippage and cost, always green;
+ *                        responses (N)
+ *   MGN_OP_PORT_TXN      Portfolio::handleTransaction(assetIdx, transactionPrice,
+ *                        units, transactionCost) (Portfolio.cpp:284-323), no
+ *                        risk check: asset_idx_dev, units_dev, tprice_dev,
+ *                        tcost_dev (N; null = 0)
+ *   MGN_OP_PORT_CLOSE    Portfolio::close(assetIdx, transactionPrice,
+ *                        transactionCost) (Portfolio.cpp:327-333)
+ *   MGN_OP_CHECK_ORDER   Portfolio::checkRisk(assetIdx, units)
+ *                        (Portfolio.cpp:254-279) into out->risk (N); no change
+ * out: tprice / tunits / tcost / risk / margin_call device pointers (null =
+ * not written); margin_call = Portfolio::checkRisk() after the operation. */
+enum { MGN_OP_BROKER_UNITS = 0, MGN_OP_BROKER_SINGLE = 1, MGN_OP_BROKER_CLOSE = 2,
+       MGN_OP_PORT_TXN = 3, MGN_OP_PORT_CLOSE = 4, MGN_OP_CHECK_ORDER = 5 };
+int mgn_ledger_op(mgn_env *env, int32_t op, const int32_t *asset_idx_dev, const double *units_dev,
+                  const double *tprice_dev, const double *tcost_dev, const mgn_traj *out);
 /* The one collective of the sharded path: all-gather the (N,4)
  * episode statistics of every rank over a caller-provided RCCL communicator
  * (an ncclComm_t, e.g. torch's ProcessGroupNCCL._comm_ptr()), ordered on the

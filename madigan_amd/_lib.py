@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmadigan_hip.so")
 MAX_ASSETS = 64
-ABI_VERSION = 6
+ABI_VERSION = 7
 SRC_PARAMS = 64
 AUX_WIDTH = 24
 MAX_NSTEP = 64
@@ -31,6 +31,7 @@ REWARD_ENV_LOG, REWARD_AGENT_SUM, REWARD_AGENT_PER_ASSET = range(3)
 RING_PLAIN, RING_PAIR_RATIO = range(2)
 STEP_NONE, STEP_UNITS, STEP_SINGLE = range(3)
 SCHED_AUTO, SCHED_SINGLE, SCHED_DUO, SCHED_TRIO = range(4)
+OP_BROKER_UNITS, OP_BROKER_SINGLE, OP_BROKER_CLOSE, OP_PORT_TXN, OP_PORT_CLOSE, OP_CHECK_ORDER = range(6)
 
 
 class MadiganError(RuntimeError):
@@ -132,12 +133,18 @@ SYMBOLS = {
     "mgn_get_layout": (C.c_int, [C.c_void_p]),
     "mgn_set_schedule": (C.c_int, [C.c_void_p, C.c_int32]),
     "mgn_get_schedule": (C.c_int, [C.c_void_p]),
-    "mgn_set_ablation": (C.c_int, [C.c_void_p, C.c_int32]),
+    "mgn_ledger_op": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                C.POINTER(Traj)]),
     "mgn_bandwidth_probe": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int32, C.c_void_p,
                                       C.POINTER(C.c_double)]),
     "mgn_synchronize": (C.c_int, [C.c_void_p]),
     "mgn_last_error": (C.c_char_p, [C.c_void_p]),
     "mgn_global_error": (C.c_char_p, []),
+}
+
+# exported by the diagnostic builds only (timing ablations; never in the product ABI)
+DIAG_SYMBOLS = {
+    "mgn_set_ablation": (C.c_int, [C.c_void_p, C.c_int32]),
 }
 
 _lib = None
@@ -191,6 +198,12 @@ def load(path: str = ""):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    # diagnostic builds only (tools/build_variant.py defines MGN_DIAG)
+    for name, (res, args) in DIAG_SYMBOLS.items():
+        fn = getattr(lib, name, None)
+        if fn is not None:
+            fn.restype = res
+            fn.argtypes = args
     if lib.mgn_abi_version() != ABI_VERSION:
         raise ImportError("libmadigan_hip.so ABI version mismatch; rebuild the extension")
     _lib = lib

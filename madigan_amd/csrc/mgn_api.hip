@@ -89,6 +89,7 @@ struct mgn_env {
   std::vector<hipEvent_t> t_step, t_gather;  // event pools, reused across mgn_set_timing calls
   size_t t_step_n = 0, t_gather_n = 0;        // events recorded since mgn_set_timing
   bool hist_on = false;  // kparams() hands the history to the step kernel
+  std::vector<int32_t> kinds;  // the source kind of every asset (host copy of src_dev's)
   // mgn_stats_allgather: the rank's padded send rows (rows_per_rank x 4)
   double* ag_send = nullptr;
   size_t ag_rows = 0;
@@ -470,6 +471,8 @@ int mgn_create(const mgn_config* cfg, const mgn_asset_source* sources, void* str
   e->F = cfg->n_feats > 0 ? cfg->n_feats : e->A;
   e->cfg.n_feats = e->F;
   e->replay = sources[0].kind == MGN_SRC_REPLAY;
+  e->kinds.resize(e->A);
+  for (int i = 0; i < e->A; ++i) e->kinds[i] = sources[i].kind;
   e->apad = next_pow2(e->A);
   auto_layout(e);
   e->stream = (hipStream_t)stream;
@@ -669,6 +672,7 @@ int mgn_set_sources(mgn_env* e, const mgn_asset_source* sources, const double* p
   const int st = validate(&e->cfg, sources, msg);
   if (st != MGN_OK) return fail(e, st, msg);
   std::memcpy(cur.data(), sources, sizeof(mgn_asset_source) * e->A);
+  for (int i = 0; i < e->A; ++i) e->kinds[i] = sources[i].kind;
   rc = check_hip(e, hipMemcpyAsync(e->src_dev, cur.data(), sizeof(mgn_asset_source) * e->A,
                                    hipMemcpyHostToDevice, e->stream), "mgn_set_sources (write)");
   if (rc == MGN_OK && prices_dev)
@@ -864,6 +868,34 @@ int mgn_generate_actions(mgn_env* e, int8_t* actions_dev, int32_t k_steps, uint6
   return check_hip(e, hipGetLastError(), "mgn_generate_actions");
 }
 
+int mgn_ledger_op(mgn_env* e, int32_t op, const int32_t* aidx_dev, const double* units_dev,
+                  const double* tprice_dev, const double* tcost_dev, const mgn_traj* out) {
+  if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
+  if (op < MGN_OP_BROKER_UNITS || op > MGN_OP_CHECK_ORDER) return fail(e, MGN_ERR_CONFIG, "unknown ledger op");
+  if (!units_dev && op != MGN_OP_BROKER_CLOSE && op != MGN_OP_PORT_CLOSE)
+    return fail(e, MGN_ERR_ARG, "units pointer is null");
+  if (!aidx_dev && op != MGN_OP_BROKER_UNITS) return fail(e, MGN_ERR_ARG, "asset index pointer is null");
+  if (!tprice_dev && (op == MGN_OP_PORT_TXN || op == MGN_OP_PORT_CLOSE))
+    return fail(e, MGN_ERR_ARG, "transaction price pointer is null");
+  if (need_tape(e) != MGN_OK) return MGN_ERR_CONFIG;
+  mgn::LedgerOp o{};
+  o.op = op;
+  o.aidx = aidx_dev;
+  o.units = units_dev;
+  o.tprice = tprice_dev;
+  o.tcost = tcost_dev;
+  if (out) {
+    o.o_tp = out->tprice;
+    o.o_tu = out->tunits;
+    o.o_tc = out->tcost;
+    o.o_risk = out->risk;
+    o.o_mc = out->margin_call;
+  }
+  hipLaunchKernelGGL(mgn::k_ledger_op, dim3((unsigned)((e->N + mgn::BLOCK - 1) / mgn::BLOCK)), dim3(mgn::BLOCK), 0,
+                     e->stream, kparams(e), o);
+  return check_hip(e, hipGetLastError(), "mgn_ledger_op");
+}
+
 int mgn_valuation(mgn_env* e, double* out_dev) {
   if (!e || !out_dev) return fail(e, MGN_ERR_ARG, "null handle/out");
   launch_val(e, out_dev);
@@ -978,11 +1010,17 @@ int mgn_get_schedule(const mgn_env* e) {
 
 int mgn_get_layout(const mgn_env* e) { return e ? e->m : 0; }
 
+#ifdef MGN_DIAG
+// diagnostic builds only (tools/build_variant.py), not part of the product
+// ABI: timing ablations whose outputs are wrong -- bit 0 skips the Broker
+// rounds, bit 1 the generators, bit 2 the output stores, bit 3 the agent
+// reward's logarithms (k_step / k_step_duo)
 int mgn_set_ablation(mgn_env* e, int32_t flags) {
   if (!e) return MGN_ERR_ARG;
   e->ablate = flags;
   return MGN_OK;
 }
+#endif
 
 // RCCL entry points from the library instance the process already has loaded
 // (torch's, when the communicator is torch's); librccl.so.1 otherwise
@@ -1031,7 +1069,8 @@ int mgn_stats_allgather(mgn_env* e, void* comm, int32_t rows_per_rank, double* o
 namespace {
 struct StateHeader {
   char magic[8];
-  int32_t abi, pad_;
+  int32_t abi;
+  int32_t replay;  // the handle's sources are a replay tape (MGN_SRC_REPLAY)
   uint64_t arena_bytes;
   mgn_config cfg;
 };
@@ -1046,6 +1085,7 @@ int mgn_save_state(mgn_env* e, void* dst, size_t bytes) {
   StateHeader h{};
   std::memcpy(h.magic, kStateMagic, 8);
   h.abi = MGN_ABI_VERSION;
+  h.replay = e->replay ? 1 : 0;
   h.arena_bytes = e->arena_bytes;
   h.cfg = e->cfg;
   std::memcpy(dst, &h, sizeof h);
@@ -1068,11 +1108,32 @@ int mgn_load_state(mgn_env* e, const void* src, size_t bytes) {
       c.n_assets != m.n_assets || c.window != m.window || c.reward_mode != m.reward_mode ||
       c.nstep != m.nstep || c.n_feats != m.n_feats || c.aux != m.aux)
     return fail(e, MGN_ERR_LENGTH, "state blob of a handle with other dimensions");
+  // the blob carries its own source table: it must describe the same kinds
+  // of source as the handle's (a replay blob into a generator handle, or the
+  // reverse, would leave e->replay and the restored table disagreeing)
+  if ((h.replay != 0) != e->replay)
+    return fail(e, MGN_ERR_CONFIG, "state blob of a replay handle loaded into a generator handle, or the reverse");
+  {
+    const mgn_asset_source* bs = reinterpret_cast<const mgn_asset_source*>(
+        static_cast<const char*>(src) + sizeof h + plan(&c).src);
+    for (int i = 0; i < e->A; ++i) {
+      int32_t k;
+      std::memcpy(&k, &bs[i].kind, sizeof k);
+      if (k != e->kinds[i] && k != MGN_SRC_EXTERNAL && e->kinds[i] != MGN_SRC_EXTERNAL)
+        return fail(e, MGN_ERR_CONFIG, "state blob's source kind differs from the handle's for asset " +
+                                           std::to_string(i));
+    }
+  }
   int rc = check_hip(e, hipMemcpyAsync(e->arena, (const char*)src + sizeof h, e->arena_bytes,
                                        hipMemcpyHostToDevice, e->stream), "mgn_load_state");
   if (rc == MGN_OK) rc = check_hip(e, hipStreamSynchronize(e->stream), "mgn_load_state (sync)");
   if (rc != MGN_OK) return rc;
   e->cfg = c;
+  {
+    const mgn_asset_source* bs = reinterpret_cast<const mgn_asset_source*>(
+        static_cast<const char*>(src) + sizeof h + plan(&c).src);
+    for (int i = 0; i < e->A; ++i) std::memcpy(&e->kinds[i], &bs[i].kind, sizeof(int32_t));
+  }
   auto_layout(e);
   return MGN_OK;
 }

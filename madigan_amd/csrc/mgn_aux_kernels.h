@@ -553,4 +553,191 @@ __global__ __launch_bounds__(BLOCK) void k_copy_probe(const probe_v2* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------
+// Broker / Portfolio operations outside a step (the drop-in's env.broker and
+// env.portfolio objects): no tick, no reward, only the ledger and the
+// responses.  One thread per env; the assets in the reference's serial order,
+// every risk check re-evaluating the canonical sums from the current ledger
+// (Portfolio.cpp:170-279), as the step kernels' serial form does.  Off the
+// step path (one call per Python-level Broker / Portfolio method).
+struct LedgerOp {
+  int op;  // MGN_OP_*
+  const int32_t* aidx;   // (N) asset index (single-asset ops)
+  const double* units;   // (N, A) BROKER_UNITS, else (N)
+  const double* tprice;  // (N) PORT_TXN / PORT_CLOSE transaction price
+  const double* tcost;   // (N) PORT_TXN / PORT_CLOSE transaction cost
+  double *o_tp, *o_tu, *o_tc;  // responses: (N, A) BROKER_UNITS, else (N)
+  uint8_t *o_risk, *o_mc;      // risk (N, A) / (N); marginCall (N)
+};
+
+// the canonical pairwise tree of v[0..A) padded with +0.0 to APAD
+__device__ double lop_canon(const double* v, int A, int apad) {
+  double t[MGN_MAX_ASSETS];
+  for (int i = 0; i < apad; ++i) t[i] = i < A ? v[i] : 0.0;
+  for (int w = apad; w > 1; w >>= 1)
+    for (int i = 0; i < w / 2; ++i) t[i] = t[2 * i] + t[2 * i + 1];
+  return t[0];
+}
+__device__ Sums lop_sums(const double* L, const double* mep, const double* Bm, const double* P, int A,
+                         int apad) {
+  double a[MGN_MAX_ASSETS], b[MGN_MAX_ASSETS], c[MGN_MAX_ASSETS];
+  for (int i = 0; i < A; ++i) {
+    a[i] = L[i] * P[i];
+    b[i] = mep[i] * L[i];
+    const double mask = (L[i] < 0.) ? 1.0 : 0.0;
+    c[i] = L[i] * (mep[i] * mask);
+  }
+  Sums s;
+  s.lp = lop_canon(a, A, apad);
+  s.ml = lop_canon(b, A, apad);
+  s.sh = lop_canon(c, A, apad);
+  s.b = lop_canon(Bm, A, apad);
+  return s;
+}
+// Portfolio::checkRisk(assetIdx, units), Portfolio.cpp:254-279
+__device__ int lop_check_order(const KParams& p, const double* L, const double* mep, const double* Bm,
+                               const double* P, double cash, int A, int apad, int i, double u) {
+  const Sums q = lop_sums(L, mep, Bm, P, A, apad);
+  const double pnl = q.lp - q.ml;
+  const double balance = cash + q.sh;
+  const double availM = (balance + pnl) / p.reqM;
+  const double cur = L[i];
+  if (signbit(u) != signbit(cur)) {
+    if (u > -1 * cur) {
+      const double excess = u + cur;
+      if (availM <= fabs(P[i] * excess) || balance <= 0.) return MGN_INSUFF_MARGIN;
+    }
+    return MGN_GREEN;
+  }
+  if (margin_call(q, cash, p.mainM)) return MGN_MARGIN_CALL;
+  if (availM <= fabs(P[i] * u) || balance <= 0.) return MGN_INSUFF_MARGIN;
+  return MGN_GREEN;
+}
+// Portfolio::handleTransaction, Portfolio.cpp:284-323
+__device__ void lop_txn(const KParams& p, double* L, double* mep, double* Bm, double& cash, int i,
+                        double tp, double u, double cost) {
+  double& cur = L[i];
+  double& me = mep[i];
+  if (signbit(cur) != signbit(u)) {
+    if (fabs(u) > fabs(cur)) {
+      u += cur;
+      cash += cur * tp;
+      cur = 0.;
+      me = tp;
+    }
+  } else {
+    me += (tp - me) * (u / (u + cur));
+  }
+  const double amt = tp * u;
+  const double use = amt * p.reqM;
+  const double brw = amt - use;
+  Bm[i] += brw;
+  cash -= (use + cost);
+  cur += u;
+  if (fabs(cur) < 0.000001) {
+    me = 0.;
+    if (Bm[i] > 0.) {
+      cash -= Bm[i];
+      Bm[i] = 0.;
+    }
+  }
+  if (Bm[i] < 0.) {
+    cash -= Bm[i];
+    Bm[i] = 0.;
+  }
+}
+// Broker::applySlippage / getTransactionCost (Broker.cpp:171-178)
+__device__ double lop_slip(const KParams& p, double price, double u) {
+  const double slippage = (price * p.slip_rel) + p.slip_abs;
+  return u < 0 ? (price - slippage) : (price + slippage);
+}
+__device__ double lop_cost(const KParams& p, double amount) { return fabs(amount) * p.tc_rel + p.tc_abs; }
+
+__global__ __launch_bounds__(BLOCK) void k_ledger_op(KParams p, LedgerOp o) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= p.N) return;
+  const int A = p.A;
+  int apad = 1;
+  while (apad < A) apad <<= 1;
+  double L[MGN_MAX_ASSETS], mep[MGN_MAX_ASSETS], Bm[MGN_MAX_ASSETS], P[MGN_MAX_ASSETS];
+  const size_t b = (size_t)env * A;
+  for (int i = 0; i < A; ++i) {
+    L[i] = p.L[b + i];
+    mep[i] = p.mep[b + i];
+    Bm[i] = p.Bm[b + i];
+    P[i] = p.P[b + i];
+  }
+  double cash = p.cash[env];
+  if (o.op == MGN_OP_BROKER_UNITS) {
+    // Broker::handleTransaction(port, units), Broker.cpp:144-158
+    for (int i = 0; i < A; ++i) {
+      const double u = o.units[b + i];
+      double tp = 0., tu = 0., tc = 0.;
+      int risk = MGN_GREEN;
+      if (u != 0.) {
+        risk = lop_check_order(p, L, mep, Bm, P, cash, A, apad, i, u);
+        if (risk == MGN_GREEN) {
+          tp = lop_slip(p, P[i], u);
+          tc = lop_cost(p, u * P[i]);
+          tu = u;
+          lop_txn(p, L, mep, Bm, cash, i, tp, u, tc);
+        }
+      }
+      if (o.o_tp) o.o_tp[b + i] = tp;
+      if (o.o_tu) o.o_tu[b + i] = tu;
+      if (o.o_tc) o.o_tc[b + i] = tc;
+      if (o.o_risk) o.o_risk[b + i] = (uint8_t)risk;
+    }
+  } else if (o.op == MGN_OP_BROKER_SINGLE || o.op == MGN_OP_CHECK_ORDER) {
+    // Broker::handleTransaction(port, assetIdx, units), Broker.cpp:124-142;
+    // CHECK_ORDER: Portfolio::checkRisk(assetIdx, units) alone
+    const int i = o.aidx[env];
+    const double u = o.units[env];
+    double tp = 0., tu = 0., tc = 0.;
+    int risk = MGN_GREEN;
+    if (o.op == MGN_OP_CHECK_ORDER) {
+      risk = lop_check_order(p, L, mep, Bm, P, cash, A, apad, i, u);
+    } else if (u != 0.) {
+      risk = lop_check_order(p, L, mep, Bm, P, cash, A, apad, i, u);
+      if (risk == MGN_GREEN) {
+        tp = lop_slip(p, P[i], u);
+        tc = lop_cost(p, u * P[i]);
+        tu = u;
+        lop_txn(p, L, mep, Bm, cash, i, tp, u, tc);
+      }
+    }
+    if (o.o_tp) o.o_tp[env] = tp;
+    if (o.o_tu) o.o_tu[env] = tu;
+    if (o.o_tc) o.o_tc[env] = tc;
+    if (o.o_risk) o.o_risk[env] = (uint8_t)risk;
+  } else if (o.op == MGN_OP_BROKER_CLOSE) {
+    // Broker::close(assetIdx), Broker.cpp:160-169: units = -ledger, slippage and
+    // cost as an order, Portfolio::close, always green
+    const int i = o.aidx[env];
+    const double u = -(L[i]);
+    const double tp = lop_slip(p, P[i], u);
+    const double tc = lop_cost(p, P[i] * u);
+    if (L[i] != 0.) lop_txn(p, L, mep, Bm, cash, i, tp, -1 * L[i], tc);  // Portfolio.cpp:327-333
+    if (o.o_tp) o.o_tp[env] = tp;
+    if (o.o_tu) o.o_tu[env] = u;
+    if (o.o_tc) o.o_tc[env] = tc;
+    if (o.o_risk) o.o_risk[env] = (uint8_t)MGN_GREEN;
+  } else if (o.op == MGN_OP_PORT_TXN) {
+    // Portfolio::handleTransaction(assetIdx, transactionPrice, units, cost)
+    lop_txn(p, L, mep, Bm, cash, o.aidx[env], o.tprice[env], o.units[env], o.tcost ? o.tcost[env] : 0.);
+  } else if (o.op == MGN_OP_PORT_CLOSE) {
+    // Portfolio::close(assetIdx, transactionPrice, cost), Portfolio.cpp:327-333
+    const int i = o.aidx[env];
+    if (L[i] != 0.) lop_txn(p, L, mep, Bm, cash, i, o.tprice[env], -1 * L[i], o.tcost ? o.tcost[env] : 0.);
+  }
+  if (o.o_mc) o.o_mc[env] = margin_call(lop_sums(L, mep, Bm, P, A, apad), cash, p.mainM) ? 1 : 0;
+  if (o.op == MGN_OP_CHECK_ORDER) return;
+  for (int i = 0; i < A; ++i) {
+    p.L[b + i] = L[i];
+    p.mep[b + i] = mep[i];
+    p.Bm[b + i] = Bm[i];
+  }
+  p.cash[env] = cash;
+}
+
 }  // namespace mgn

@@ -56,9 +56,11 @@ void launch_duo(const StepArgs& a) {
       if (a.p.reqm_one) go(k_step_duo<S, true, false, false, true, false>);
       else go(k_step_duo<S, false, false, false, true, false>);
     }
+#ifdef MGN_DIAG
   } else if (a.p.ablate) {  // diagnostic timing builds: discrete actions only
     if (a.p.reqm_one) go(k_step_duo<S, true, true, true, false, false>);
     else go(k_step_duo<S, false, true, true, false, false>);
+#endif
   } else if (disc) {
     if (a.p.reqm_one) go(k_step_duo<S, true, false, true, false, false>);
     else go(k_step_duo<S, false, false, true, false, false>);

@@ -30,8 +30,10 @@
 // oracle).
 // Stores: L stores the BrokerResponse arrays of its step, G the tick's
 // State.price and timestamp, F everything that needs equity.
-// Scope: M = 1, APAD = S in {2, 4, 8}, n-step 1, no window, generator
-// sources (k_step_duo / k_step run the rest).
+// Scope: M = 1, APAD = S in {2, 4, 8}, n-step 1, generator sources, with or
+// without a window (WIN: the finish role pushes the ring / launch-history row
+// of every step it confirms, and the refill rows after an auto-reset);
+// k_step_duo / k_step run the rest.
 #pragma once
 
 #include "mgn_duo.h"
@@ -125,7 +127,11 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
   s.pf_ok = false;
   s.fcol = -1;
   const size_t li = (size_t)envc * A + (s.valid[0] ? ls : 0);
+#ifdef MGN_TRIO_ABL_PRO
+  s.P[0] = 5.0;
+#else
   s.P[0] = s.valid[0] ? p.P[li] : 0.;
+#endif
   s.L[0] = s.mep[0] = s.Bm[0] = s.sx[0] = s.oum[0] = s.dy[0] = 0.;
   s.tlen[0] = 0;
   s.tfl[0] = 0;
@@ -137,7 +143,11 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
   double ep_ret = 0., ep_len = 0., n_done = 0.;  // F
   double shA = 0., shB = 0.;                     // F
   int32_t rhead = 0, rlen = 0;                   // F (WIN): the window ring
+#ifdef MGN_TRIO_ABL_PRO  // diagnostic timing build: no state loads (outputs wrong)
+  if (false) {
+#else
   if (role == 0) {
+#endif
     if (s.valid[0]) {
       s.sx[0] = p.sx[li];
       s.oum[0] = p.oum[li];
@@ -251,7 +261,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
           svTlen = s.tlen[0];
           svTfl = s.tfl[0];
           svTs = ts;
+#ifndef MGN_TRIO_ABL_G  // diagnostic timing build: no tick (prices frozen)
           gen_tick<M, false, false>(s, p, env, ts);
+#endif
           ts = ts + 1;
           // State.price and timestamp of step k (overwritten if rolled back)
           if (MGN_TRIO_GST) {
@@ -281,6 +293,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
       atomicAdd(&g_duo_stamps[8], (unsigned long long)(jn + 1));
       atomicAdd(&g_duo_stamps[10], 1ull);
     }
+#endif
+#ifdef MGN_TRIO_ABL_EPI  // diagnostic timing build: no state write-back
+    return;
 #endif
     if (!live) return;
     if (s.valid[0]) {
@@ -388,7 +403,11 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
         const double prevVal = s.L[0] * s.P[0];
         Sums after = s0;
         int any_mc = 0, mcall = 0;
+#ifdef MGN_TRIO_ABL_L  // diagnostic timing build: no Broker orders
+        if (false) {
+#else
         if (in_kind != IN_NONE) {
+#endif
           broker_spec<S, RQ1, true>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, after, any_mc);
           mcall = margin_call(after, cash, p.mainM) ? 1 : 0;  // Broker.cpp:156-157
         }
@@ -445,6 +464,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
       atomicAdd(&g_duo_stamps[5], acc1);
       for (int i = 0; i < 3; ++i) atomicAdd(&g_duo_stamps[13 + i], s_duo_sub[i]);
     }
+#endif
+#ifdef MGN_TRIO_ABL_EPI  // diagnostic timing build: no state write-back
+    return;
 #endif
     if (!live) return;
     if (s.valid[0]) {
@@ -544,7 +566,11 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     int rst_out = 0;
     // the step L ran in iteration j-1, unless F voided it at iteration j-1
     const int flags = sh.rFlags[prv][el];
+#ifdef MGN_TRIO_ABL_F  // diagnostic timing build: no step finish, no outputs
+    if (false) {
+#else
     if (live && (flags & TR_STEP) && !sh.reset[prv][el]) {
+#endif
       const int k = sh.rK[prv][el];
       Lane<M> f = s;
       f.L[0] = sh.rL[prv][l];
@@ -691,6 +717,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     atomicAdd(&g_duo_stamps[16], acc0);
     atomicAdd(&g_duo_stamps[17], acc1);
   }
+#endif
+#ifdef MGN_TRIO_ABL_EPI
+  return;
 #endif
   if (!live) return;
   if (ls == 0) {

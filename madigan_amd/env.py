@@ -365,6 +365,46 @@ class BatchedEnv:
                                       C.c_void_p(ix.data_ptr())), self.h)
         return self.out
 
+    def ledger_op(self, op: int, asset_idx=None, units=None, tprice=None, tcost=None) -> dict:
+        """A Broker / Portfolio operation outside a step on every env
+        (mgn_ledger_op; no tick, no reward).  op: L.OP_*.  units (N, A) for
+        OP_BROKER_UNITS, else (N,); asset_idx / tprice / tcost (N,).  Returns
+        the responses as device tensors (tprice / tunits / tcost / risk of
+        shape (N, A) for OP_BROKER_UNITS, else (N,); margin_call (N,)), valid
+        until the next ledger_op."""
+        torch = _torch()
+        N, A = self.N, self.A
+        if not hasattr(self, "_op"):
+            f64, u8 = torch.float64, torch.uint8
+            self._op = dict(tprice=torch.zeros((N, A), dtype=f64, device=self.device),
+                            tunits=torch.zeros((N, A), dtype=f64, device=self.device),
+                            tcost=torch.zeros((N, A), dtype=f64, device=self.device),
+                            risk=torch.zeros((N, A), dtype=u8, device=self.device),
+                            margin_call=torch.zeros((N,), dtype=u8, device=self.device))
+            self._op_in = dict(tprice=torch.zeros(N, dtype=f64, device=self.device),
+                               tcost=torch.zeros(N, dtype=f64, device=self.device))
+            self._op_traj = self._traj_struct(self._op)
+        multi = op == L.OP_BROKER_UNITS
+        ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
+        u = ix = tp = tc = None
+        if units is not None:
+            u = self._dev(units, torch.float64, (N, A) if multi else (N,), self.units_buf)
+        if asset_idx is not None:
+            ix = self._dev(asset_idx, torch.int32, (N,), self.asset_idx_buf)
+            bad = (ix < 0) | (ix >= A)
+            if bool(bad.any()):
+                raise IndexError(f"asset index out of range [0, {A})")
+        if tprice is not None:
+            tp = self._dev(tprice, torch.float64, (N,), self._op_in["tprice"])
+        if tcost is not None:
+            tc = self._dev(tcost, torch.float64, (N,), self._op_in["tcost"])
+        L.check(self.lib.mgn_ledger_op(self.h, int(op), ptr(ix), ptr(u), ptr(tp), ptr(tc),
+                                       C.byref(self._op_traj)), self.h)
+        o = self._op
+        if multi:
+            return dict(o)
+        return {k: (v.view(-1)[:N] if k != "margin_call" else v) for k, v in o.items()}
+
     def _shaped_shape(self) -> tuple:
         N, A, D, n = self.N, self.A, self.D, self.nstep
         col = (N,) if D == 1 else (N, A)
@@ -416,18 +456,31 @@ class BatchedEnv:
             setattr(t, k, None if v is None else v.data_ptr())
         return t
 
-    def _traj_for(self, out: dict, K: int):
+    # caller-owned output dicts whose validated mgn_traj is kept (the most
+    # recently used ones; an evicted dict is released, so a loop that builds a
+    # fresh dict per launch holds at most this many)
+    TRAJ_CACHE_SLOTS = 4
+
+    def _traj_for(self, out: dict, K: int, cache: bool = True):
         """The validated mgn_traj of an output dict: validated and built once per
         (dict, K, buffer addresses), then reused, so a loop over launches with
-        the same buffers pays one address comparison per launch."""
+        the same buffers pays one address comparison per launch.  cache=False
+        (buffers allocated by the call itself): validate and build, keep nothing."""
+        if not cache:
+            self._check_traj(out, K)
+            return self._traj_struct(out)
         key = (id(out), K)
         ptrs = tuple(None if v is None else v.data_ptr() for v in out.values())
-        hit = self._traj_cache.get(key)
+        tc = self._traj_cache
+        hit = tc.pop(key, None)
         if hit is not None and hit[0] is out and hit[1] == ptrs:
+            tc[key] = hit  # most recently used last
             return hit[2]
         self._check_traj(out, K)
         t = self._traj_struct(out)
-        self._traj_cache[key] = (out, ptrs, t, C.byref(t))
+        tc[key] = (out, ptrs, t, C.byref(t))
+        while len(tc) > self.TRAJ_CACHE_SLOTS:
+            tc.pop(next(iter(tc)))
         return t
 
     def rollout(self, actions, out: Optional[dict] = None) -> dict:
@@ -439,8 +492,9 @@ class BatchedEnv:
         if actions.dim() != 3 or actions.shape[1] != self.N or actions.shape[2] != self.A:
             raise ValueError(f"actions must be (K, {self.N}, {self.A}), got {tuple(actions.shape)}")
         K = int(actions.shape[0])
-        out = self.alloc_traj(K) if out is None else out
-        t = self._traj_for(out, K)
+        own = out is None
+        out = self.alloc_traj(K) if own else out
+        t = self._traj_for(out, K, cache=not own)
         L.check(self.lib.mgn_rollout(self.h, C.c_void_p(actions.data_ptr()), K, C.byref(t)), self.h)
         return out
 
@@ -504,8 +558,9 @@ class BatchedEnv:
         if u.dim() != 3 or u.shape[1] != self.N or u.shape[2] != self.A:
             raise ValueError(f"units must be (K, {self.N}, {self.A}), got {tuple(u.shape)}")
         K = int(u.shape[0])
-        out = self.alloc_traj(K) if out is None else out
-        t = self._traj_for(out, K)
+        own = out is None
+        out = self.alloc_traj(K) if own else out
+        t = self._traj_for(out, K, cache=not own)
         L.check(self.lib.mgn_rollout_units(self.h, C.c_void_p(u.data_ptr()), K, C.byref(t)), self.h)
         return out
 
@@ -676,7 +731,10 @@ class _DeviceSourceView:
 
 
 class PortfolioView:
-    """Env.portfolio: the default Portfolio's accessors (Portfolio.h)."""
+    """Env.portfolio / Env.account: the default Portfolio (env.cpp:440-570).
+
+    Accessors read the Env's state; handleTransaction / close mutate the
+    device ledger directly (Portfolio.cpp:284-333, no risk check, no tick)."""
 
     def __init__(self, env):
         self._env = env
@@ -686,8 +744,111 @@ class PortfolioView:
             raise AttributeError(name)
         return getattr(self._env, name)
 
+    def _idx(self, asset):
+        return self._env._asset_index(asset)
+
     def checkRisk(self, *args):
-        return self._env.checkRisk()
+        """checkRisk() (Portfolio.cpp:243-252) or checkRisk(assetIdx | assetCode,
+        units) (:254-279)."""
+        if len(args) == 0:
+            return self._env.checkRisk()
+        if len(args) != 2:
+            raise TypeError("checkRisk() takes () or (assetIdx | assetCode, units)")
+        e = self._env
+        r = e._b.ledger_op(L.OP_CHECK_ORDER, asset_idx=[self._idx(args[0])], units=[float(args[1])])
+        return RiskInfo(int(r["risk"][0].item()))
+
+    def handleTransaction(self, asset, transactionPrice, units, transactionCost=0.0):
+        """Portfolio::handleTransaction(assetIdx | asset, transactionPrice, units,
+        transactionCost=0.) (Portfolio.cpp:284-323): the accounting alone."""
+        e = self._env
+        e._b.ledger_op(L.OP_PORT_TXN, asset_idx=[self._idx(asset)], units=[float(units)],
+                       tprice=[float(transactionPrice)], tcost=[float(transactionCost)])
+        e._dirty()
+
+    def close(self, assetIdx, transactionPrice, transactionCost=0.0):
+        """Portfolio::close(assetIdx, transactionPrice, transactionCost=0.)
+        (Portfolio.cpp:327-333): sell / cover the whole position, if any."""
+        e = self._env
+        e._b.ledger_op(L.OP_PORT_CLOSE, asset_idx=[self._idx(assetIdx)],
+                       tprice=[float(transactionPrice)], tcost=[float(transactionCost)])
+        e._dirty()
+
+    def setRequiredMargin(self, requiredMargin):
+        self._env.setRequiredMargin(requiredMargin)
+
+    def setMaintenanceMargin(self, maintenanceMargin):
+        self._env.setMaintenanceMargin(maintenanceMargin)
+
+
+class BrokerView:
+    """Env.broker: the Env's Broker (Broker.h, env.cpp:700-840) over the
+    default account and portfolio.  Orders run the reference's risk checks,
+    slippage and transaction cost on the device ledger, without a tick."""
+
+    def __init__(self, env):
+        self._env = env
+
+    def __getattr__(self, name):
+        if name.startswith("_"):
+            raise AttributeError(name)
+        return getattr(self._env, name)
+
+    def _multi(self, units):
+        e = self._env
+        u = np.asarray(units, dtype=np.float64).reshape(-1)
+        if u.shape[0] != e.nAssets:
+            raise ValueError(f"units must have {e.nAssets} entries, got {u.shape[0]}")
+        r = e._b.ledger_op(L.OP_BROKER_UNITS, units=u.reshape(1, -1))
+        e._dirty()
+        h = {k: v.cpu().numpy() for k, v in r.items()}
+        return BrokerResponse(h["tprice"][0].copy(), h["tunits"][0].copy(), h["tcost"][0].copy(),
+                              [RiskInfo(int(x)) for x in h["risk"][0]], bool(h["margin_call"][0]))
+
+    def _single(self, op, asset, units=None):
+        e = self._env
+        r = e._b.ledger_op(op, asset_idx=[e._asset_index(asset)],
+                           units=None if units is None else [float(units)])
+        e._dirty()
+        h = {k: v.cpu().numpy() for k, v in r.items()}
+        return BrokerResponse(float(h["tprice"][0]), float(h["tunits"][0]), float(h["tcost"][0]),
+                              RiskInfo(int(h["risk"][0])), bool(h["margin_call"][0]))
+
+    def handleTransaction(self, *args):
+        """handleTransaction(units) -> BrokerResponseMulti (Broker.cpp:144-158);
+        handleTransaction(assetIdx | assetCode, units) -> BrokerResponseSingle
+        (:124-142)."""
+        if len(args) == 1:
+            return self._multi(args[0])
+        if len(args) == 2:
+            return self._single(L.OP_BROKER_SINGLE, args[0], args[1])
+        raise TypeError("handleTransaction takes (units) or (assetIdx | assetCode, units) "
+                        "on the Env's default account / portfolio")
+
+    def handleAction(self, units):
+        """Broker::handleAction (Broker.h:99-101): handleTransaction(units)."""
+        return self._multi(units)
+
+    def handleEvent(self, units):
+        """Broker::handleEvent (Broker.h:95-97): handleTransaction(units)."""
+        return self._multi(units)
+
+    def close(self, assetIdx):
+        """Broker::close(assetIdx) (Broker.cpp:160-169): close the position at
+        the current price with slippage and transaction cost; always green."""
+        return self._single(L.OP_BROKER_CLOSE, assetIdx)
+
+    def portfolio(self, *args):
+        return PortfolioView(self._env)
+
+    def account(self, *args):
+        return PortfolioView(self._env)
+
+    def setSlippage(self, relativeSlippage=0.0, absSlippage=0.0):
+        self._env.setSlippage(relativeSlippage, absSlippage)
+
+    def setTransactionCost(self, relativeCost=0.0, absCost=0.0):
+        self._env.setTransactionCost(relativeCost, absCost)
 
 
 class Env:
@@ -1042,7 +1203,20 @@ class Env:
 
     @property
     def broker(self):
-        return PortfolioView(self)
+        return BrokerView(self)
+
+    def _asset_index(self, asset) -> int:
+        """An asset index or code -> index; IndexError out of range (the
+        reference's std::out_of_range, envTest.py:246-248)."""
+        if isinstance(asset, str):
+            codes = [a.code for a in self.assets]
+            if asset not in codes:
+                raise IndexError(f"asset code {asset} not found")
+            return codes.index(asset)
+        idx = int(asset)
+        if not 0 <= idx < self.nAssets:
+            raise IndexError(f"asset index {idx} out of range")
+        return idx
 
     @property
     def account(self):

@@ -1513,6 +1513,32 @@ void orc_broker_handle_transaction(orc_batch *b, int e, int asset, double units,
   resp[3] = r;
 }
 
+/* Broker::close(assetIdx) -- Broker.cpp:160-169: units = -ledger, slippage
+ * and cost as for an order (:171-178), Portfolio::close (Portfolio.cpp:327-333);
+ * the response is always green */
+void orc_broker_close(orc_batch *b, int e, int asset, double *resp) {
+  const orc_config *c = &b->cfg;
+  orc_env *s = &b->envs[e];
+  double units = -(s->L[asset]);
+  double currentPrice = s->P[asset];
+  double slippage = (currentPrice * c->slippage_rel) + c->slippage_abs;
+  double transactionPrice = units < 0 ? (currentPrice - slippage) : (currentPrice + slippage);
+  double transactionCost = fabs(currentPrice * units) * c->tc_rel + c->tc_abs;
+  if (s->L[asset] != 0.)
+    p_handle_transaction(s, c->required_margin, asset, transactionPrice, -1 * s->L[asset], transactionCost);
+  resp[0] = transactionPrice;
+  resp[1] = units;
+  resp[2] = transactionCost;
+  resp[3] = ORC_GREEN;
+}
+
+/* Portfolio::close(assetIdx, transactionPrice, transactionCost) -- Portfolio.cpp:327-333 */
+void orc_port_close(orc_batch *b, int e, int asset, double tprice, double cost) {
+  orc_env *s = &b->envs[e];
+  if (s->L[asset] != 0.)
+    p_handle_transaction(s, b->cfg.required_margin, asset, tprice, -1 * s->L[asset], cost);
+}
+
 /* ---- window output (StackerDiscrete.current_data, preprocessor.py:177-185) */
 
 void orc_window_stream(orc_batch *b) {

@@ -196,6 +196,10 @@ void orc_port_ledger_normed_full(const orc_batch *b, int e, double *out); /* (A+
 /* Broker::handleTransaction(port, i, u) on env e: fills resp[4] = {tp,u,cost,risk} */
 void orc_broker_handle_transaction(orc_batch *b, int e, int asset, double units,
                                    double *resp);
+/* Broker::close(assetIdx) on env e: resp[4] = {tp, units, cost, risk (green)} */
+void orc_broker_close(orc_batch *b, int e, int asset, double *resp);
+/* Portfolio::close(assetIdx, transactionPrice, transactionCost) on env e */
+void orc_port_close(orc_batch *b, int e, int asset, double tprice, double cost);
 
 /* Sliding window (StackerDiscrete.current_data) for all envs:
  * price (N,W,A) normalised, port (N,W,A+1), ts (N,W). */

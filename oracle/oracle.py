@@ -103,6 +103,8 @@ def lib(fast: bool = False):
         L.orc_port_check_risk_order.restype = C.c_int
         L.orc_port_ledger_normed_full.argtypes = [P, C.c_int, P]
         L.orc_broker_handle_transaction.argtypes = [P, C.c_int, C.c_int, C.c_double, P]
+        L.orc_broker_close.argtypes = [P, C.c_int, C.c_int, P]
+        L.orc_port_close.argtypes = [P, C.c_int, C.c_int, C.c_double, C.c_double]
         L.orc_window.argtypes = [P, P, P, P]
         L.orc_window_stream.argtypes = [P]
         for fn in (L.orc_dsr, L.orc_ddr):
@@ -306,6 +308,14 @@ class OracleBatch:
         r = np.zeros(4)
         self.L.orc_broker_handle_transaction(self.h, e, asset, units, _ptr(r))
         return r
+
+    def broker_close(self, e, asset):
+        r = np.zeros(4)
+        self.L.orc_broker_close(self.h, e, asset, _ptr(r))
+        return r
+
+    def port_close(self, e, asset, tprice, cost=0.0):
+        self.L.orc_port_close(self.h, e, asset, tprice, cost)
 
 
 def dsr(rewards, discounts, eta, A, B, ddr=False):

@@ -249,3 +249,39 @@ def test_reset_restores_accounting():  # Env.h:181-187
     assert b.scalar("cash")[0] == 1_000_000
     assert not b.field(O.F_LEDGER).any()
     assert b.scalar("timestamp")[0] == ts + 1  # reset ticks the source once (Env.h:160)
+
+
+def test_broker_close_kat():  # Broker.cpp:160-169 (bound at env.cpp:825-829)
+    """Broker::close(assetIdx): the position closed at the current price with
+    slippage and transaction cost applied as for an order, always green; the
+    closed form below follows Portfolio.cpp:284-323 statement by statement."""
+    sr, tc = 1e-4, 0.02
+    for units in (1000., -1000.):
+        b = port(reqM=1.0, slippage_rel=sr, transaction_cost_rel=tc)
+        P = b.field(O.F_PRICE)[0][0]
+        tp1, u1, c1, r1 = b.broker_handle_transaction(0, 0, units)
+        slip = P * sr + 0.0
+        assert tp1 == (P - slip if units < 0 else P + slip) and u1 == units and r1 == O.GREEN
+        assert c1 == abs(units * P) * tc + 0.0
+        cash1 = 1_000_000 - ((tp1 * units) * 1.0 + c1)
+        assert b.scalar("cash")[0] == cash1
+        tp2, u2, c2, r2 = b.broker_close(0, 0)
+        cu = -units
+        assert u2 == cu and r2 == O.GREEN
+        assert tp2 == (P - slip if cu < 0 else P + slip)
+        assert c2 == abs(P * cu) * tc + 0.0
+        amt = tp2 * cu
+        assert b.scalar("cash")[0] == cash1 - (amt * 1.0 + c2)
+        assert b.field(O.F_LEDGER)[0][0] == 0.0 and b.field(O.F_MEP)[0][0] == 0.0
+        # closing a flat position moves nothing and still answers green
+        tp3, u3, c3, r3 = b.broker_close(0, 0)
+        assert u3 == 0.0 and r3 == O.GREEN and b.scalar("cash")[0] == cash1 - (amt * 1.0 + c2)
+
+
+def test_port_close_kat():  # Portfolio.cpp:327-333
+    b = port(reqM=.1)
+    P = b.field(O.F_PRICE)[0]
+    b.port_handle_transaction(0, 2, P[2], -4000., 0.)
+    b.port_close(0, 2, P[2] * 1.01, 5.0)
+    assert b.field(O.F_LEDGER)[0][2] == 0.0
+    assert b.field(O.F_BORROWED)[0][2] == 0.0

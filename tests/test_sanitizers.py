@@ -1,6 +1,6 @@
 """Host sanitizer builds (ASan / UBSan on the host code).
 
-`make -C oracle sanitize` builds, with -fsanitize=address,undefined and
+`make -B -C oracle sanitize` (always rebuilt from the current sources) builds, with -fsanitize=address,undefined and
 -fno-sanitize-recover=all:
   * oracle/_build/sanitize_oracle: the C oracle under a driver that calls
     every entry point of madigan_oracle.h over the parity tests'
@@ -23,7 +23,7 @@ ORACLE = os.path.join(ROOT, "oracle")
 
 @pytest.fixture(scope="module")
 def built():
-    r = subprocess.run(["make", "-s", "-C", ORACLE, "sanitize"], capture_output=True, text=True)
+    r = subprocess.run(["make", "-s", "-B", "-C", ORACLE, "sanitize"], capture_output=True, text=True)
     if r.returncode != 0:
         pytest.fail(f"sanitizer build failed:\n{r.stdout}\n{r.stderr}")
     return os.path.join(ORACLE, "_build")

@@ -32,7 +32,7 @@ def main():
         if base not in redo:
             return os.path.join(B.OBJ, base.replace(".hip", ".o"))
         obj = os.path.join(out_dir, base.replace(".hip", ".o"))
-        subprocess.run([cc, *B.FLAGS, *extra, "-c", "-o", obj, src], check=True)
+        subprocess.run([cc, *B.FLAGS, "-DMGN_DIAG", *extra, "-c", "-o", obj, src], check=True)
         return obj
 
     with ThreadPoolExecutor(4) as ex:

@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round-3 first GPU pass: GPU tests at round start, the dispatch-ramp probe,
+# per-role ablation timings of the three-role kernel (diagnostic builds) and a
+# driver-shape kernel trace.  Each GPU step has its own limit; a failure ends it.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+export TMPDIR=/tmp
+O=gpurun_out/r03a
+mkdir -p $O
+PT="python -u -m pytest -v --timeout 180 --timeout-method thread -p no:cacheprovider"
+timeout -k 10 600 $PT -m gpu tests > $O/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -30 $O/pytest_gpu.log; exit 1; }
+tail -2 $O/pytest_gpu.log
+timeout -k 10 120 tools/_var/ramp/dispatch_ramp > $O/ramp.jsonl 2> $O/ramp.err || { echo "ramp failed"; tail $O/ramp.err; exit 1; }
+cat $O/ramp.jsonl
+for r in 1 2; do
+  for v in base ablG ablL ablF ablDraw; do
+    path=tools/_var/$v/libmadigan_hip.so; [ $v = base ] && path=madigan_amd/libmadigan_hip.so
+    MADIGAN_LIB_PATH=$path timeout -k 10 120 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-probe > $O/$v.$r.20.json 2>> $O/err.log || { echo "fail $v"; tail -5 $O/err.log; exit 1; }
+    MADIGAN_LIB_PATH=$path timeout -k 10 120 python bench.py --steps 1024 --warmup 256 --no-cpu-baseline --no-probe > $O/$v.$r.256.json 2>> $O/err.log || { echo "fail $v"; tail -5 $O/err.log; exit 1; }
+    MADIGAN_LIB_PATH=$path timeout -k 10 120 python bench.py --steps 64 --warmup 8 --fuse 1 --no-cpu-baseline --no-probe > $O/$v.$r.1.json 2>> $O/err.log || { echo "fail $v"; tail -5 $O/err.log; exit 1; }
+    python -c "import json;a=json.load(open('$O/$v.$r.256.json'));b=json.load(open('$O/$v.$r.20.json'));c=json.load(open('$O/$v.$r.1.json'));print('$v', $r, 'k256', round(a['kernel_us_per_step'],3), 'drv', round(b['value']/1e9,3), round(b['roofline']['avg_launch_us'],2), 'k1', round(c['kernel_us_per_step'],3))"
+  done
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt20 -o kt -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-probe > $O/kt20.log 2>&1 || { echo "kt20 failed"; tail -20 $O/kt20.log; exit 1; }
+echo r03a done

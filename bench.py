@@ -202,11 +202,10 @@ def composite_spec():
     return s
 
 
-def c5_replay_file(A: int, T: int, path: str) -> None:
-    """Synthetic OU paths (mu 10, theta .08, phi .04, as C2) in the replay
-    layout: price (T, A), features = prices, timestamps 1-minute bars."""
+def c5_paths(A: int, T: int):
+    """Synthetic OU paths (mu 10, theta .08, phi .04, as C2): price (T, A)
+    and 1-minute-bar timestamps (T,)."""
     from scipy.signal import lfilter
-    from madigan_amd import write_hdf
     rng = np.random.default_rng(0x6D6164 + 5)
     mu, th, phi = 10.0, 0.08, 0.04
     z = rng.standard_normal((T, A))
@@ -214,6 +213,13 @@ def c5_replay_file(A: int, T: int, path: str) -> None:
     x = lfilter([1.0], [1.0, -(1.0 - th)], th * mu + mu * phi * z, axis=0,
                 zi=np.full((1, A), (1.0 - th) * mu))[0]
     ts = (np.arange(T, dtype=np.uint64) + np.uint64(27_000_000)) * np.uint64(60_000_000_000)
+    return x, ts
+
+
+def c5_replay_file(A: int, T: int, path: str) -> None:
+    """c5_paths in the replay layout: price (T, A), features = prices."""
+    from madigan_amd import write_hdf
+    x, ts = c5_paths(A, T)
     write_hdf(path, "synth/ou", [f"OU_{i}" for i in range(A)], x, x, ts,
               price_key="price", feature_key="features", timestamp_key="timestamps")
 
@@ -415,11 +421,9 @@ def main():
     # the sharded path's one collective, issued at log intervals
     # in a training loop, not per step: after the timed steps, timed on its own
     ta = time.perf_counter()
-    if world > 1:
-        from madigan_amd.distributed import allgather_env_stats
-        gathered = allgather_env_stats(env, n_total=world * N)
-    else:
-        gathered = env.episode_stats
+    from madigan_amd import distributed as D
+    gathered = D.allgather_env_stats(env, n_total=world * N)
+    allgather_path = D.last_allgather_path
     torch.cuda.synchronize()
     allgather_us = (time.perf_counter() - ta) * 1e6
     if world > 1:
@@ -503,6 +507,7 @@ def main():
             "kernel_us_per_step": avg_launch_s * 1e6 / steps_per_launch,
             "episodes_completed": episodes,
             "stats_allgather_us": allgather_us,
+            "allgather_path": allgather_path,
         }
         if sweep:
             res["fusion_sweep"] = sweep
@@ -625,11 +630,9 @@ def windowed(args, world, rank, dev):
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     # the episode-statistics all-gather (log intervals, not per step): after the timed steps
-    if world > 1:
-        from madigan_amd.distributed import allgather_env_stats
-        gathered = allgather_env_stats(env, n_total=world * N)
-    else:
-        gathered = env.episode_stats
+    from madigan_amd import distributed as D
+    gathered = D.allgather_env_stats(env, n_total=world * N)
+    allgather_path = D.last_allgather_path
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         if args.dist_backend == "gloo":
@@ -666,6 +669,7 @@ def windowed(args, world, rank, dev):
                 " (the previous launch's k_hist_gather runs beside it on a second stream)"
                 if args.win_overlap else ""),
             "episodes_completed": int(gathered[:, 3].sum().item()),
+            "allgather_path": allgather_path,
         }
         if wl == "C5":
             tape_bytes = sum(t.numel() * t.element_size() for t in env._tape.values())

@@ -344,6 +344,23 @@ int mgn_get_layout(const mgn_env *env);
 enum { MGN_SCHED_AUTO = 0, MGN_SCHED_SINGLE = 1, MGN_SCHED_DUO = 2, MGN_SCHED_TRIO = 3 };
 int mgn_set_schedule(mgn_env *env, int32_t schedule);
 int mgn_get_schedule(const mgn_env *env);
+/* Zero-copy per-step windows (element-wise normalisers: none, log).  After
+ * mgn_rollout_hist, the launch history holds every ring push of the launch,
+ * oldest first, per env: window k of env e (StackerDiscrete.current_data after
+ * step k, preprocessor.py:177-189) is history rows [hend - hlen, hend) of env
+ * e, hend / hlen at [k * n_envs + e], and its rows hlen..W-1 are the zero
+ * padding mgn_window_hist writes.  The price columns are log-normalised at push
+ * for norm "log", so each window is a contiguous row range read in place --
+ * no (K, N, W, .) copy.  The pointers are the handle's and stay valid until
+ * its next mgn_rollout_hist (with a window stream: until the one after). */
+typedef struct {
+  const double *hist;       /* (n_envs, rows, cols): price features, then ledgerNormedFull */
+  const uint64_t *hist_ts;  /* (n_envs, rows) */
+  const int32_t *hend;      /* (k_steps, n_envs) one past window k's last row */
+  const int32_t *hlen;      /* (k_steps, n_envs) window k's fill (<= window) */
+  int32_t rows, cols, k_steps, window, n_feats, pad_;
+} mgn_hist_view;
+int mgn_window_hist_view(mgn_env *env, mgn_hist_view *out);
 /* Broker / Portfolio operations outside a step (no tick, no reward): the
  * drop-in's env.broker / env.portfolio objects, per env on device.
  *   MGN_OP_BROKER_UNITS  Broker::handleTransaction(units) / handleAction /

@@ -85,6 +85,12 @@ class ReplayTape(C.Structure):
                 ("data_end", C.c_void_p), ("rows", C.c_int64), ("stride", C.c_int64)]
 
 
+class HistView(C.Structure):  # mgn_hist_view
+    _fields_ = [("hist", C.c_void_p), ("hist_ts", C.c_void_p), ("hend", C.c_void_p), ("hlen", C.c_void_p),
+                ("rows", C.c_int32), ("cols", C.c_int32), ("k_steps", C.c_int32), ("window", C.c_int32),
+                ("n_feats", C.c_int32), ("pad_", C.c_int32)]
+
+
 class Ring(C.Structure):
     _fields_ = [("n_envs", C.c_int32), ("n_price", C.c_int32), ("n_port", C.c_int32),
                 ("window", C.c_int32), ("norm_type", C.c_int32), ("transform", C.c_int32),
@@ -133,6 +139,7 @@ SYMBOLS = {
     "mgn_get_layout": (C.c_int, [C.c_void_p]),
     "mgn_set_schedule": (C.c_int, [C.c_void_p, C.c_int32]),
     "mgn_get_schedule": (C.c_int, [C.c_void_p]),
+    "mgn_window_hist_view": (C.c_int, [C.c_void_p, C.POINTER(HistView)]),
     "mgn_ledger_op": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                 C.POINTER(Traj)]),
     "mgn_bandwidth_probe": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int32, C.c_void_p,

@@ -845,6 +845,29 @@ int mgn_window_hist(mgn_env* e, double* price_dev, double* port_dev, uint64_t* t
   return check_hip(e, hipGetLastError(), "mgn_window_hist");
 }
 
+int mgn_window_hist_view(mgn_env* e, mgn_hist_view* out) {
+  if (!e || !out) return fail(e, MGN_ERR_ARG, "null handle/out");
+  const auto& hb = e->hb[e->hcur];
+  if (hb.k == 0) return fail(e, MGN_ERR_CONFIG, "no mgn_rollout_hist to view");
+  const int nt = e->cfg.norm_type;
+  if (nt != MGN_NORM_NONE && nt != MGN_NORM_LOG)
+    return fail(e, MGN_ERR_CONFIG, "mgn_window_hist_view: windows are history rows only for norm none / log");
+  out->hist = hb.hist;
+  out->hist_ts = hb.ts;
+  out->hend = hb.hend;
+  out->hlen = hb.hlen;
+  out->rows = hb.rows;
+  out->cols = e->F + e->A + 1;
+  out->k_steps = hb.k;
+  out->window = e->W;
+  out->n_feats = e->F;
+  out->pad_ = 0;
+  // the history is written on the handle's stream: order a window-stream
+  // consumer after it as mgn_window_hist would
+  if (e->wstream) (void)hipStreamWaitEvent(e->wstream, hb.ready, 0);
+  return MGN_OK;
+}
+
 int mgn_rollout_window(mgn_env* e, const int8_t* actions_dev, int32_t k_steps, const mgn_traj* out,
                        double* price_dev, double* port_dev, uint64_t* ts_dev, int32_t per_step) {
   if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");

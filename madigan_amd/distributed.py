@@ -50,40 +50,72 @@ def allgather_episode_stats(stats, group=None):
     return torch.cat([out[r * n_max:r * n_max + sizes[r]] for r in range(world)])
 
 
+class CollectiveUnavailable(RuntimeError):
+    """An "nccl" process group whose RCCL communicator cannot be reached, so
+    the C ABI's mgn_stats_allgather cannot run on it."""
+
+
 def rccl_comm(group=None, device=None) -> int:
     """The raw RCCL communicator (ncclComm_t) of a torch "nccl" process group,
-    for mgn_stats_allgather; 0 if the group has none (gloo)."""
+    for mgn_stats_allgather; 0 for other backends (gloo).  Over "nccl" a
+    communicator that cannot be reached raises CollectiveUnavailable -- it is
+    taken through a private accessor of torch's ProcessGroupNCCL, and a torch
+    without it must not silently route the sharded path's collective around
+    the library."""
     import torch
     import torch.distributed as dist
     g = group if group is not None else dist.group.WORLD
     if dist.get_backend(g) != "nccl":
         return 0
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-    try:  # a private accessor of torch's ProcessGroupNCCL: absent -> torch's all-gather
-        return int(g._get_backend(dev)._comm_ptr())
-    except (AttributeError, RuntimeError):
-        return 0
+    try:
+        comm = int(g._get_backend(dev)._comm_ptr())
+    except (AttributeError, RuntimeError) as e:
+        raise CollectiveUnavailable(
+            "nccl process group without a reachable RCCL communicator (ProcessGroupNCCL._comm_ptr): "
+            f"{e!r}; pass allow_torch_fallback=True to all-gather through torch.distributed") from e
+    if not comm:
+        raise CollectiveUnavailable("nccl process group returned a null RCCL communicator")
+    return comm
 
 
-def allgather_env_stats(env, n_total=None, group=None):
+# which path the last allgather_env_stats took: "mgn_stats_allgather" (the
+# C ABI's ncclAllGather on the caller's RCCL communicator), "torch" (torch's
+# all-gather: gloo, or nccl with allow_torch_fallback), "local" (one process)
+last_allgather_path = None
+
+
+def allgather_env_stats(env, n_total=None, group=None, allow_torch_fallback=False):
     """All-gather a BatchedEnv's (N_local, 4) episode statistics into
     (n_total, 4) in global env order.  Over "nccl" the collective is the C
     ABI's mgn_stats_allgather on the handle's stream (one ncclAllGather of
     ceil(n_total / world) rows per rank; ragged shards are zero-padded by the
-    library and trimmed here); other backends use torch's all-gather.  With
-    n_total given (the shard() partition) no size exchange is needed."""
+    library and trimmed here); gloo uses torch's all-gather.  An nccl group
+    whose communicator cannot be reached raises CollectiveUnavailable unless
+    allow_torch_fallback.  The path taken is recorded in
+    ``last_allgather_path``.  With n_total given (the shard() partition) no
+    size exchange is needed."""
     import ctypes as C
     import torch
     import torch.distributed as dist
     from . import _lib as L
+    global last_allgather_path
     stats = env.episode_stats
     if not (dist.is_available() and dist.is_initialized()):
+        last_allgather_path = "local"
         return stats
     world = dist.get_world_size(group)
-    comm = rccl_comm(group, env.device)
+    try:
+        comm = rccl_comm(group, env.device)
+    except CollectiveUnavailable:
+        if not allow_torch_fallback:
+            raise
+        comm = 0
     if not comm:
+        last_allgather_path = "torch"
         return allgather_episode_stats(stats.cpu() if dist.get_backend(group) == "gloo" else stats,
                                        group)
+    last_allgather_path = "mgn_stats_allgather"
     if n_total is None:
         n = torch.tensor([env.N], dtype=torch.int64, device=env.device)
         sizes = [torch.zeros_like(n) for _ in range(world)]

@@ -618,6 +618,49 @@ class BatchedEnv:
                                             *ptrs, int(per_step)), self.h)
         return out, win
 
+    def window_hist_view(self) -> dict:
+        """The last mgn_rollout_hist's launch history, read in place
+        (mgn_window_hist_view; norm none / log): window k of env e is rows
+        [hend[k, e] - hlen[k, e], hend[k, e]) of ``hist[e]`` (price columns
+        first, then ledgerNormedFull), zero-padded to W rows.  Device tensors
+        over the handle's buffers, valid until the next rollout_window /
+        mgn_rollout_hist; no copy is made."""
+        torch = _torch()
+        v = L.HistView()
+        L.check(self.lib.mgn_window_hist_view(self.h, C.byref(v)), self.h)
+
+        class _Dev:  # __cuda_array_interface__ over the library's device buffer
+            def __init__(self, ptr, shape, typestr):
+                self.__cuda_array_interface__ = {"shape": shape, "typestr": typestr, "data": (ptr, False),
+                                                 "version": 2, "strides": None}
+
+        def dev(ptr, shape, typestr):
+            return torch.as_tensor(_Dev(int(ptr), shape, typestr), device=self.device)
+        N, K = self.N, int(v.k_steps)
+        return dict(hist=dev(v.hist, (N, int(v.rows), int(v.cols)), "<f8"),
+                    hist_ts=dev(v.hist_ts, (N, int(v.rows)), "<i8"),
+                    hend=dev(v.hend, (K, N), "<i4"), hlen=dev(v.hlen, (K, N), "<i4"),
+                    window=int(v.window), n_feats=int(v.n_feats))
+
+    @staticmethod
+    def window_from_view(view: dict, k: int):
+        """Window k of every env from a window_hist_view, as (N, W, F),
+        (N, W, A+1), (N, W) tensors (a consumer-side gather; what
+        mgn_window_hist writes)."""
+        torch = _torch()
+        hist, W, F = view["hist"], view["window"], view["n_feats"]
+        end = view["hend"][k].long()
+        ln = view["hlen"][k].long()
+        w = torch.arange(W, device=hist.device)
+        rows = (end - ln)[:, None] + w[None, :]
+        ok = w[None, :] < ln[:, None]
+        rows = torch.where(ok, rows, torch.zeros_like(rows))
+        g = torch.gather(hist, 1, rows[:, :, None].expand(-1, -1, hist.shape[2]))
+        g = torch.where(ok[:, :, None], g, torch.zeros((), dtype=g.dtype, device=g.device))
+        ts = torch.gather(view["hist_ts"], 1, rows)
+        ts = torch.where(ok, ts, torch.zeros((), dtype=ts.dtype, device=ts.device))
+        return g[:, :, :F], g[:, :, F:], ts
+
     def window_push(self, price=None, port=None, ts=None):
         ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
         L.check(self.lib.mgn_window_push(self.h, ptr(price), ptr(port), ptr(ts)), self.h)

@@ -58,15 +58,16 @@ LAYOUT_C = r"""
 #define F(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
 int main(void) {
   printf("mgn_config %zu\nmgn_traj %zu\nmgn_views %zu\nmgn_asset_source %zu\nmgn_ring %zu\n"
-         "mgn_replay_tape %zu\n",
+         "mgn_replay_tape %zu\nmgn_hist_view %zu\n",
          sizeof(mgn_config), sizeof(mgn_traj), sizeof(mgn_views), sizeof(mgn_asset_source),
-         sizeof(mgn_ring), sizeof(mgn_replay_tape));
+         sizeof(mgn_ring), sizeof(mgn_replay_tape), sizeof(mgn_hist_view));
   F(mgn_config, seed) F(mgn_config, shaper) F(mgn_config, adaptation_rate)
   F(mgn_config, desired_portfolio) F(mgn_config, window) F(mgn_config, unit_size)
   F(mgn_views, out) F(mgn_views, n_envs) F(mgn_views, reward_dim) F(mgn_views, reset_mask)
   F(mgn_ring, ring) F(mgn_ring, len) F(mgn_asset_source, p) F(mgn_config, n_feats)
   F(mgn_traj, data_end) F(mgn_views, replay_cursor) F(mgn_views, n_feats)
   F(mgn_replay_tape, rows) F(mgn_replay_tape, stride)
+  F(mgn_hist_view, hlen) F(mgn_hist_view, rows) F(mgn_hist_view, n_feats)
   return 0;
 }
 """
@@ -81,7 +82,8 @@ def test_struct_layouts_match_ctypes(tmp_path):
     got = dict(line.split() for line in subprocess.run([str(exe)], capture_output=True, text=True,
                                                         check=True).stdout.splitlines())
     py = {"mgn_config": L.Config, "mgn_traj": L.Traj, "mgn_views": L.Views,
-          "mgn_asset_source": L.AssetSource, "mgn_ring": L.Ring, "mgn_replay_tape": L.ReplayTape}
+          "mgn_asset_source": L.AssetSource, "mgn_ring": L.Ring, "mgn_replay_tape": L.ReplayTape,
+          "mgn_hist_view": L.HistView}
     for k, v in got.items():
         if "." in k:
             t, f = k.split(".")

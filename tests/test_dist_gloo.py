@@ -78,3 +78,20 @@ def test_gloo_allgather_matches_unsharded():
     assert np.array_equal(got.view(np.int64), ref.view(np.int64))
     s = summarize(torch.from_numpy(got))
     assert s["episodes"] == int(ref[:, 3].sum())
+
+
+def test_nccl_without_communicator_fails_loudly(monkeypatch):
+    """Over "nccl" the statistics all-gather is the C ABI's
+    mgn_stats_allgather; a torch whose ProcessGroupNCCL hides the RCCL
+    communicator raises instead of silently taking torch's all-gather."""
+    from madigan_amd import distributed as D
+
+    class NoComm:
+        def _get_backend(self, dev):
+            raise AttributeError("_comm_ptr")
+
+    monkeypatch.setattr(dist, "get_backend", lambda g=None: "nccl")
+    with pytest.raises(D.CollectiveUnavailable):
+        D.rccl_comm(NoComm(), device=torch.device("cpu"))
+    monkeypatch.setattr(dist, "get_backend", lambda g=None: "gloo")
+    assert D.rccl_comm(NoComm(), device=torch.device("cpu")) == 0

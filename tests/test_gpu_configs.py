@@ -250,6 +250,8 @@ def test_stats_allgather_rccl_single_rank(gpu):
     try:
         assert rccl_comm(device=g.device) != 0
         got = allgather_env_stats(g, n_total=N)
+        from madigan_amd import distributed as D
+        assert D.last_allgather_path == "mgn_stats_allgather"
         torch.cuda.synchronize()
         ref = g.episode_stats.cpu().numpy()
         assert ref[:, 3].sum() > 0

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 O=gpurun_out/r03b
 mkdir -p $O
 PT="python -u -m pytest -v --timeout 180 --timeout-method thread -p no:cacheprovider"
-timeout -k 10 300 $PT -m gpu tests/test_gpu_broker.py tests/test_abi.py > $O/pytest_broker.log 2>&1 || { echo "broker tests failed"; tail -40 $O/pytest_broker.log; exit 1; }
+timeout -k 10 300 $PT -m gpu tests/test_gpu_broker.py tests/test_abi.py tests/test_gpu_bench_shapes.py tests/test_gpu_window_view.py tests/test_gpu_configs.py::test_stats_allgather_rccl_single_rank > $O/pytest_broker.log 2>&1 || { echo "broker tests failed"; tail -40 $O/pytest_broker.log; exit 1; }
 tail -2 $O/pytest_broker.log
 for r in 1 2; do
   for v in base xnt nostore ablEpi ablPro; do

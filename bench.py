@@ -331,6 +331,9 @@ def main():
                     help="rank 0 saves the gathered (n_total, 4) episode statistics (.npy)")
     ap.add_argument("--no-probe", dest="probe", action="store_false",
                     help="skip the attainable-bandwidth copy probe")
+    ap.add_argument("--timing", default="launch", choices=["launch", "marker"],
+                    help="kernel duration events: recorded by the step launch itself "
+                         "(hipExtLaunchKernel, the kernel's begin / end) or marker events around it")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1: nccl (RCCL; the statistics all-gather is the C ABI's "
                          "mgn_stats_allgather) or gloo (several ranks may share one GPU)")
@@ -402,13 +405,14 @@ def main():
     warm, timed = plan(0, args.warmup), plan(args.warmup, total)
     # kernel durations: HIP events around each step launch on the handle's
     # stream (mgn_set_timing; pooled events, created during the warmup)
-    L.check(lib.mgn_set_timing(h, 1), h)
+    tmode = 2 if args.timing == "launch" else 1
+    L.check(lib.mgn_set_timing(h, tmode), h)
     L.check(run(warm), h)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    L.check(lib.mgn_set_timing(h, 1), h)
+    L.check(lib.mgn_set_timing(h, tmode), h)
     t0 = time.perf_counter()
     rc = run(timed)
     torch.cuda.synchronize()
@@ -481,6 +485,8 @@ def main():
                 "bytes_note": "SURVEY 8d algorithmic bytes per env-step (C3: 8 x (113 + 48) + 105): "
                               "state r/w + actions + outputs per step",
                 "units_per_launch": units_per_launch, "avg_launch_us": avg_launch_s * 1e6,
+                "timing": ("HIP events recorded by the step launch (hipExtLaunchKernel start / stop)"
+                           if args.timing == "launch" else "HIP marker events around the step launch"),
                 "fused_bytes_per_env_step": fused,
                 "fused_achieved_GBs": units_per_launch * fused / avg_launch_s / 1e9,
                 "fused_note": "what the fused kernel must move (state held in registers across "

@@ -299,11 +299,14 @@ int mgn_rollout_window(mgn_env *env, const int8_t *actions_dev, int32_t k_steps,
  * L+1 (ordered by events; the caller's window buffers of launch L are
  * complete once `stream` has passed the gather) */
 int mgn_set_window_stream(mgn_env *env, void *stream);
-/* kernel timing with HIP events on each kernel's own stream: on != 0 starts
- * (and clears) recording around the step kernel of mgn_rollout /
- * mgn_rollout_hist and the gather of mgn_window_hist (events come from a
- * per-handle pool, created once); mgn_get_timing waits for them and returns
- * {step ms total, step launches, gather ms total, gather launches} */
+/* kernel timing with HIP events on each kernel's own stream: on = 1 starts
+ * (and clears) recording marker events around the step kernel of mgn_rollout /
+ * mgn_rollout_hist and the gather of mgn_window_hist; on = 2 has mgn_rollout's
+ * step launch record its own start / stop events (hipExtLaunchKernel: the
+ * kernel's begin and end, without the marker packets' dispatch gaps); events
+ * come from a per-handle pool, created once; 0 stops.  mgn_get_timing waits
+ * for them and returns {step ms total, step launches, gather ms total,
+ * gather launches} */
 int mgn_set_timing(mgn_env *env, int32_t on);
 int mgn_get_timing(mgn_env *env, double *out4);
 /* uniform discrete actions U{0..atoms-1} (K,N,A) from Philox (benchmark input) */

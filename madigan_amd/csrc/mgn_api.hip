@@ -85,7 +85,7 @@ struct mgn_env {
   int hcur = 0;
   hipStream_t wstream = nullptr;  // window stream (mgn_set_window_stream), null: the handle's
   // kernel timing (mgn_set_timing): start/stop event pairs on each kernel's stream
-  bool timing = false;
+  int timing = 0;  // 1: marker events around each launch; 2: events recorded by the step launch
   std::vector<hipEvent_t> t_step, t_gather;  // event pools, reused across mgn_set_timing calls
   size_t t_step_n = 0, t_gather_n = 0;        // events recorded since mgn_set_timing
   bool hist_on = false;  // kparams() hands the history to the step kernel
@@ -310,7 +310,8 @@ void (*const kInit[7])(int, const mgn::InitArgs&) = {mgn::launch_init_a1, mgn::l
 void (*const kVal[7])(int, const mgn::ValArgs&) = {mgn::launch_val_a1, mgn::launch_val_a2, mgn::launch_val_a4, mgn::launch_val_a8, mgn::launch_val_a16, mgn::launch_val_a32, mgn::launch_val_a64};
 
 void launch_step(const mgn_env* e, const mgn_traj& out, int in_kind, const double* units,
-                 const int32_t* aidx, const int8_t* act, int K);
+                 const int32_t* aidx, const int8_t* act, int K, hipEvent_t ev0 = nullptr,
+                 hipEvent_t ev1 = nullptr);
 void launch_init(const mgn_env* e, int mode, const uint8_t* mask);
 void launch_val(const mgn_env* e, double* out);
 
@@ -330,13 +331,16 @@ bool duo_eligible(const mgn_env* e) {
   }
   return true;
 }
-// the three-role kernel: 2..8 assets, generator sources, one-step rewards
+// the three-role kernel: 2..8 assets, generator sources; one-step rewards
 // (windows included: the confirmed steps' rows are pushed by its finish role)
+// or n-step aggregation of a scalar reward without a window (the finish
+// role's rings in dynamic LDS)
 bool trio_eligible(const mgn_env* e) {
-  // (its output indices are k x a 32-bit stride: N (A + 1) and N F fit 32 bits)
+  // (its output indices are k x a 32-bit stride: N (A + 1), N F and N n fit 32 bits)
   const uint64_t row = (uint64_t)(e->A + 1 > e->F ? e->A + 1 : e->F);
-  return e->apad >= 2 && e->apad <= 8 && !e->cfg.aux && !e->replay && e->cfg.nstep == 1 &&
-         (uint64_t)e->N * row < (1ull << 32);
+  const bool nst_ok = e->cfg.nstep == 1 || (e->D == 1 && e->W == 0 && e->cfg.shaper < MGN_SHAPER_SHARPE);
+  return e->apad >= 2 && e->apad <= 8 && !e->cfg.aux && !e->replay && nst_ok &&
+         (uint64_t)e->N * row < (1ull << 32) && (uint64_t)e->N * (uint64_t)e->cfg.nstep < (1ull << 32);
 }
 // automatic: where the single-role kernel would run one lane per asset (small
 // batches: one wave per SIMD), give every asset a second (and a third) lane
@@ -377,8 +381,8 @@ int choose_m(int n_envs, int apad) {
 }
 
 void launch_step(const mgn_env* e, const mgn_traj& out, int in_kind, const double* units,
-                 const int32_t* aidx, const int8_t* act, int K) {
-  mgn::StepArgs a{kparams(e), out, in_kind, units, aidx, act, K, e->stream};
+                 const int32_t* aidx, const int8_t* act, int K, hipEvent_t ev0, hipEvent_t ev1) {
+  mgn::StepArgs a{kparams(e), out, in_kind, units, aidx, act, K, e->stream, ev0, ev1};
   if (e->trio) {
     const int idx = e->apad <= 2 ? 1 : e->apad <= 4 ? 2 : 3;
     kTrio[idx](a);
@@ -626,15 +630,18 @@ int mgn_step(mgn_env* e, int32_t kind, const double* units_dev, const int32_t* a
 }
 
 static void time_mark(mgn_env* e, std::vector<hipEvent_t>& v, size_t& n, hipStream_t st);
+static bool time_pair(mgn_env* e, hipEvent_t& a, hipEvent_t& b);
 
 int mgn_rollout(mgn_env* e, const int8_t* actions_dev, int32_t k_steps, const mgn_traj* out) {
   if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
   if (!actions_dev || !out) return fail(e, MGN_ERR_ARG, "null actions/out");
   if (k_steps < 1) return fail(e, MGN_ERR_LENGTH, "k_steps must be >= 1");
   if (need_tape(e) != MGN_OK) return MGN_ERR_CONFIG;
-  time_mark(e, e->t_step, e->t_step_n, e->stream);
-  launch_step(e, *out, mgn::IN_DISCRETE, nullptr, nullptr, actions_dev, (int)k_steps);
-  time_mark(e, e->t_step, e->t_step_n, e->stream);
+  hipEvent_t a = nullptr, b = nullptr;
+  if (e->timing == 2) (void)time_pair(e, a, b);
+  else time_mark(e, e->t_step, e->t_step_n, e->stream);
+  launch_step(e, *out, mgn::IN_DISCRETE, nullptr, nullptr, actions_dev, (int)k_steps, a, b);
+  if (e->timing != 2) time_mark(e, e->t_step, e->t_step_n, e->stream);
   return check_hip(e, hipGetLastError(), "mgn_rollout");
 }
 
@@ -719,6 +726,19 @@ static void time_mark(mgn_env* e, std::vector<hipEvent_t>& v, size_t& n, hipStre
   (void)hipEventRecord(v[n++], st);
 }
 
+// mode 2: the next start / stop pair of the step pool, recorded by the launch
+static bool time_pair(mgn_env* e, hipEvent_t& a, hipEvent_t& b) {
+  while (e->t_step.size() < e->t_step_n + 2) {
+    hipEvent_t ev;
+    if (hipEventCreate(&ev) != hipSuccess) return false;
+    e->t_step.push_back(ev);
+  }
+  a = e->t_step[e->t_step_n];
+  b = e->t_step[e->t_step_n + 1];
+  e->t_step_n += 2;
+  return true;
+}
+
 static int grow(mgn_env* e, void** p, size_t bytes) {
   (void)hipDeviceSynchronize();  // first use / larger K only
   if (*p) (void)hipFree(*p);
@@ -745,7 +765,8 @@ int mgn_set_timing(mgn_env* e, int32_t on) {
   (void)hipDeviceSynchronize();
   e->t_step_n = 0;
   e->t_gather_n = 0;
-  e->timing = on != 0;
+  if (on < 0 || on > 2) return fail(e, MGN_ERR_CONFIG, "mgn_set_timing: 0 off, 1 marker events, 2 launch events");
+  e->timing = on;
   return MGN_OK;
 }
 
@@ -1021,7 +1042,7 @@ int mgn_set_schedule(mgn_env* e, int32_t schedule) {
                 "the two-role kernel needs 2..16 assets, no multi-component source, n-step rings within LDS");
   if (schedule == MGN_SCHED_TRIO && !trio_eligible(e))
     return fail(e, MGN_ERR_CONFIG,
-                "the three-role kernel needs 2..8 assets, generator sources, nstep 1");
+                "the three-role kernel needs 2..8 assets, generator sources, nstep 1 or a scalar n-step reward without a window");
   e->sched = schedule;
   auto_layout(e);
   return MGN_OK;

@@ -3,6 +3,7 @@
 // so the (M, S) instantiations compile in parallel.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "mgn_duo.h"
@@ -19,7 +20,18 @@ struct StepArgs {
   const int8_t* act;
   int K;
   hipStream_t stream;
+  // mgn_set_timing(env, 2): start / stop events recorded by the launch
+  // itself (hipExtLaunchKernel: the kernel's own begin / end, no marker
+  // packets around it); null otherwise
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
+// hipLaunchKernelGGL, or the event-recording launch when the step's events are set
+template <typename Kern, typename... Args>
+inline void launch_timed(const hipEvent_t ev0, const hipEvent_t ev1, Kern kern, dim3 grid, dim3 block,
+                         uint32_t lds, hipStream_t st, Args... args) {
+  if (ev0) hipExtLaunchKernelGGL(kern, grid, block, lds, st, ev0, ev1, 0u, args...);
+  else hipLaunchKernelGGL(kern, grid, block, lds, st, args...);
+}
 struct InitArgs {
   KParams p;
   int mode;

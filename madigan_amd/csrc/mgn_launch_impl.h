@@ -13,8 +13,8 @@ struct StepL {
     const int epb = BLOCK / S;
     const int grid = (a.p.N + epb - 1) / epb;
     auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, a.stream, a.p, a.out, a.in_kind,
-                         a.units, a.aidx, a.act, a.K);
+      launch_timed(a.ev0, a.ev1, kern, dim3(grid), dim3(BLOCK), 0, a.stream, a.p, a.out, a.in_kind,
+                   a.units, a.aidx, a.act, a.K);
     };
     const bool nst = a.p.nstep > 1;
     if (a.p.reqm_one) {
@@ -36,8 +36,8 @@ void launch_duo(const StepArgs& a) {
   const size_t lds = nst ? (size_t)epb * a.p.nstep * (a.p.D + 1) * sizeof(double) : 0;
   auto go = [&](auto kern) {
     if (lds) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(DUO_BLOCK), lds, a.stream, a.p, a.out, a.in_kind,
-                       a.units, a.aidx, a.act, a.K);
+    launch_timed(a.ev0, a.ev1, kern, dim3(grid), dim3(DUO_BLOCK), (uint32_t)lds, a.stream, a.p, a.out,
+                 a.in_kind, a.units, a.aidx, a.act, a.K);
   };
   const bool disc = a.in_kind == IN_DISCRETE;
   if (nst) {  // n-step buffers (generator sources; no ablation build)
@@ -78,11 +78,35 @@ void launch_trio(const StepArgs& a) {
   const int epb = (small ? 64 : TRIO_W) / S;
   const int grid = (a.p.N + epb - 1) / epb;
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(small ? 192 : TRIO_BLOCK), 0, a.stream, a.p, a.out, a.in_kind,
-                       a.units, a.aidx, a.act, a.K);
+    launch_timed(a.ev0, a.ev1, kern, dim3(grid), dim3(small ? 192 : TRIO_BLOCK), 0, a.stream, a.p, a.out,
+                 a.in_kind, a.units, a.aidx, a.act, a.K);
   };
   const bool disc = a.in_kind == IN_DISCRETE;
   const uint32_t om = traj_mask(a.out);
+  if (a.p.nstep > 1) {  // NST: the finish role's NStepBuffer rings in dynamic LDS (no window, D = 1)
+    const size_t lds = (size_t)epb * 2 * a.p.nstep * sizeof(double);
+    auto goN = [&](auto kern) {
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      launch_timed(a.ev0, a.ev1, kern, dim3(grid), dim3(small ? 192 : TRIO_BLOCK), (uint32_t)lds, a.stream,
+                   a.p, a.out, a.in_kind, a.units, a.aidx, a.act, a.K);
+    };
+    if (small) {
+      if (disc) {
+        if (a.p.reqm_one) goN(k_step_trio<S, true, true, 0, false, 64, true>);
+        else goN(k_step_trio<S, false, true, 0, false, 64, true>);
+      } else {
+        if (a.p.reqm_one) goN(k_step_trio<S, true, false, 0, false, 64, true>);
+        else goN(k_step_trio<S, false, false, 0, false, 64, true>);
+      }
+    } else if (disc) {
+      if (a.p.reqm_one) goN(k_step_trio<S, true, true, 0, false, TRIO_W, true>);
+      else goN(k_step_trio<S, false, true, 0, false, TRIO_W, true>);
+    } else {
+      if (a.p.reqm_one) goN(k_step_trio<S, true, false, 0, false, TRIO_W, true>);
+      else goN(k_step_trio<S, false, false, 0, false, TRIO_W, true>);
+    }
+    return;
+  }
   if (small) {  // runtime output mask, window or not
     if (a.p.W > 0) {
       if (disc) {

@@ -96,7 +96,11 @@ struct TrioShared {
 // iteration's reset tick and W - 1 more) during which L does not step and F
 // pushes one refill row per tick -- the rows, order and history marks of
 // k_step_duo / k_step.
-template <int S, bool RQ1, bool DISC, uint32_t OMC = 0, bool WIN = false, int TW = TRIO_W>
+// NST: n-step aggregation (nstep > 1, scalar reward D = 1) in the finish
+// role: the env's NStepBuffer ring and one pop's summands in dynamic LDS
+// (launch_trio sizes it: envs per block x 2n doubles), the discounts staged
+// in LDS, so a pop is n LDS reads issued together, not n dependent loads.
+template <int S, bool RQ1, bool DISC, uint32_t OMC = 0, bool WIN = false, int TW = TRIO_W, bool NST = false>
 __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out, int in_kind_rt,
                                                           const double* __restrict__ units_in,
                                                           const int32_t* __restrict__ aidx_in,
@@ -111,6 +115,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
   __shared__ EnvRecs<S> recs[EPB];
   __shared__ mgn_asset_source s_src[S];
   __shared__ double s_tgt[MGN_MAX_ASSETS + 1];
+  __shared__ double s_disc[NST ? MGN_MAX_NSTEP : 1];                     // NST: gamma^k
+  extern __shared__ __attribute__((aligned(16))) double s_nst[];          // NST: (EPB, 2n)
   const int role = threadIdx.x / TRIO_W;  // 0 generator, 1 ledger, 2 finish
   const int l = threadIdx.x % TRIO_W;
   const int el = l / S;
@@ -143,6 +149,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
   double ep_ret = 0., ep_len = 0., n_done = 0.;  // F
   double shA = 0., shB = 0.;                     // F
   int32_t rhead = 0, rlen = 0;                   // F (WIN): the window ring
+  int32_t nlen = 0, nhead = 0;                   // F (NST): NStepBuffer fill count / oldest index
 #ifdef MGN_TRIO_ABL_PRO  // diagnostic timing build: no state loads (outputs wrong)
   if (false) {
 #else
@@ -179,6 +186,13 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
       shA = p.sA[li];
       shB = p.sB[li];
     }
+    if constexpr (NST) {
+      nlen = p.nlen[envc];
+      nhead = p.nhead[envc];
+      // the env's ring into LDS (every lane of the env copies a share)
+      double* ring = s_nst + (size_t)el * 2 * p.nstep;
+      for (int i = ls; i < p.nstep; i += S) ring[i] = p.nring[(size_t)envc * p.nstep + i];
+    }
   }
   {
     const double* g = reinterpret_cast<const double*>(p.src);
@@ -187,6 +201,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     for (int i = threadIdx.x; i < n; i += TRIO_BLOCK) d[i] = g[i];
     if (p.target)
       for (int i = threadIdx.x; i <= p.A; i += TRIO_BLOCK) s_tgt[i] = p.target[i];
+    if (NST)
+      for (int i = threadIdx.x; i < p.nstep; i += TRIO_BLOCK) s_disc[i] = p.disc[i];
     p.src = s_src;
     if (p.target) p.target = s_tgt;
   }
@@ -225,6 +241,26 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     int jn = 0;
 #endif
     int gpend = 0;  // WIN: refill ticks still to come after the reset tick
+    // Draw-ahead, two stages: in the iteration of tick t the generator lanes
+    // also turn the Philox block of counter t + 1 (drawn an iteration
+    // earlier) into that tick's variates (Box-Muller) and draw the Philox
+    // block of counter t + 2 -- three independent dependency chains in one
+    // iteration instead of one chain of block -> Box-Muller -> tick.  A draw
+    // is a pure function of (seed, env, asset, counter), so a rollback or
+    // reset that changes the counter only sends the tick back to drawing
+    // itself.  Lanes whose kind draws nothing skip it.
+    const uint64_t genv = (uint64_t)(p.env_offset + env);
+    bool draws = false;
+    if (s.valid[0]) {
+      const int kd = s.kind[0];
+      draws = kd == MGN_SRC_TRENDOU || kd == MGN_SRC_OU || kd == MGN_SRC_SIMPLETREND || kd == MGN_SRC_TRENDYOU ||
+              kd == MGN_SRC_GAUSSIAN || kd == MGN_SRC_OUPAIR ||
+              ((kd == MGN_SRC_SINE || kd == MGN_SRC_SAWTOOTH || kd == MGN_SRC_TRIANGLE) && s_src[ls].p[5] != 0.0);
+    }
+    Draw nd = {0.0, 0.0, 0u};  // variates of counter nd_ts
+    uint64_t nd_ts = ~0ull;
+    u4 nx = {0u, 0u, 0u, 0u};  // Philox block (slot 0) of counter nx_ts
+    uint64_t nx_ts = ~0ull;
     for (int j = 0;; ++j) {
       const int cur = j & 1, prv = cur ^ 1;
       MGN_T(T0);
@@ -262,9 +298,22 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
           svTfl = s.tfl[0];
           svTs = ts;
 #ifndef MGN_TRIO_ABL_G  // diagnostic timing build: no tick (prices frozen)
-          gen_tick<M, false, false>(s, p, env, ts);
+          gen_tick<M, false, false>(s, p, env, ts, nd_ts == ts, nd);
 #endif
           ts = ts + 1;
+#if !defined(MGN_ABL_DRAW) && !defined(MGN_TRIO_NO_DRAWAHEAD)
+          if (draws && k + 1 < K) {
+            // variates of counter ts (the next tick) from the block drawn last
+            // iteration, and the block of counter ts + 1
+            const u4 xb = (nx_ts == ts) ? nx : block(p.seed, genv, (uint32_t)s.asset[0], 0u, ts);
+            if (k + 2 < K) {
+              nx = block(p.seed, genv, (uint32_t)s.asset[0], 0u, ts + 1);
+              nx_ts = ts + 1;
+            }
+            nd = draw_from(xb);
+            nd_ts = ts;
+          }
+#endif
           // State.price and timestamp of step k (overwritten if rolled back)
           if (MGN_TRIO_GST) {
             const size_t oN = (size_t)k * p.N;
@@ -615,7 +664,125 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
         cos_term = p.cos_temp * (dot / (np_ * g.cos_qn));
       }
       double shaped_s = 0., rin_s = 0., shaped_v = 0.;
-      if (D == 1) {
+      int pops = 1;
+      if (NST) {
+        // NStepBuffer.add + pop_nstep_sarsd (nstep_buffer.py:315-356, driven as
+        // replay_buffer.py:68-80) for the env's scalar column: append, pop once
+        // when full, every entry on done; the row of step k (n entries, zero
+        // after the pops) is stored here
+        double arr[M];
+        arr[0] = ar;
+        rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(arr) : reward;
+        const int n = p.nstep;
+        double* ring = s_nst + (size_t)el * 2 * n;
+        double* scr = ring + n;
+        const double v = (p.shaper == MGN_SHAPER_PPC) ? rin_s + cos_term : rin_s;
+        const int L1 = nlen + 1;
+        pops = done ? L1 : (L1 >= n ? 1 : 0);
+        MGN_G double* row = (om & O_SHP) ? ov.shaped + kidx(k, sN, (size_t)env) * (size_t)n : nullptr;
+        if (!done && L1 >= n) {
+          // the common case, one pop of a full buffer: term kk on lane kk mod S
+          // (nstep_column's operands), then every lane of the env sums the terms
+          // in kk order from LDS (the reads issue together)
+          int tail = nhead + nlen;
+          tail -= (tail >= n) ? n : 0;
+          if (ls == 0) ring[tail] = v;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          const PopPre c = pop_pre(p.shaper, g.shA, g.shB);
+          for (int kk = ls; kk < L1; kk += S) {
+            int idx = nhead + kk;
+            idx -= (idx >= n) ? n : 0;
+#ifdef MGN_NST_ABL_TERM  // diagnostic timing build (outputs wrong): no summand arithmetic
+            scr[kk] = ring[idx];
+#else
+            scr[kk] = pop_term(p.shaper, ring[idx], g.shA, g.shB, c, s_disc[kk]);
+#endif
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          double acc = 0.0;
+#ifdef MGN_NST_ABL_SUM  // diagnostic timing build (outputs wrong): no ordered sum
+          acc = scr[0];
+          for (int k0 = L1; k0 < L1; k0 += 8) {
+#else
+          for (int k0 = 0; k0 < L1; k0 += 8) {
+#endif
+            double t[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t[u] = (k0 + u < L1) ? scr[k0 + u] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+              if (k0 + u < L1) acc += t[u];
+          }
+          double res = acc;
+          if (p.shaper == MGN_SHAPER_DSR || p.shaper == MGN_SHAPER_DDR) {
+            res = clip1(acc / L1);
+            const double r0 = ring[nhead];
+            g.shA += p.eta * (r0 - g.shA);
+            if (p.shaper == MGN_SHAPER_DSR) {
+              g.shB += p.eta * (r0 * r0 - g.shB);
+            } else {
+              double m = r0 < 0. ? r0 : 0.;
+              if (r0 != r0) m = r0;
+              g.shB += p.eta * (m * m - g.shB);
+            }
+          }
+          if (row) {
+            if (ls == 0) ost(row, res);
+#ifndef MGN_NST_ABL_ROW  // diagnostic timing build (outputs wrong): no zero entries
+            for (int jj = 1 + ls; jj < n; jj += S) ost(row + jj, 0.);
+#endif
+          }
+        } else {
+          // filling (no pop) or a done flush (every entry popped, A / B
+          // updated between pops): nstep_column's statements on the env's
+          // lane 0 over the LDS ring (DSR / DDR / PPC / none: the trio is not
+          // selected for the naive shapers), the shaper state then broadcast
+          if (ls == 0) {
+            int len = L1, head = nhead, pj = 0;
+            int tail = nhead + nlen;
+            tail -= (tail >= n) ? n : 0;
+            ring[tail] = v;
+            while (len >= n || (done && len > 0)) {
+              const PopPre c = pop_pre(p.shaper, g.shA, g.shB);
+              double acc = 0.0;
+              for (int kk = 0, idx = head; kk < len; ++kk, idx = (idx + 1 == n) ? 0 : idx + 1)
+                acc += pop_term(p.shaper, ring[idx], g.shA, g.shB, c, s_disc[kk]);
+              double res = acc;
+              if (p.shaper == MGN_SHAPER_DSR || p.shaper == MGN_SHAPER_DDR) {
+                res = clip1(acc / len);
+                const double r0 = ring[head];
+                g.shA += p.eta * (r0 - g.shA);
+                if (p.shaper == MGN_SHAPER_DSR) {
+                  g.shB += p.eta * (r0 * r0 - g.shB);
+                } else {
+                  double m = r0 < 0. ? r0 : 0.;
+                  if (r0 != r0) m = r0;
+                  g.shB += p.eta * (m * m - g.shB);
+                }
+              }
+              if (row) ost(row + pj, res);
+              head = (head + 1 == n) ? 0 : head + 1;
+              len -= 1;
+              pj += 1;
+              if (!done && len < n) break;
+            }
+            if (row)
+              for (int j = pj; j < n; ++j) ost(row + j, 0.);
+          }
+          g.shA = seg_bcast<S, 0>(g.shA);
+          g.shB = seg_bcast<S, 0>(g.shB);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        nhead += pops;
+        while (nhead >= n) nhead -= n;
+        nlen = L1 - pops;
+      } else if (D == 1) {
         double arr[M];
         arr[0] = ar;
         rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(arr) : reward;
@@ -658,11 +825,11 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
         if (om & O_MC) ost(ov.margin_call + ie, (uint8_t)((flags & TR_MCALL) ? 1 : 0));
         if (om & O_DEND) ost(ov.data_end + ie, (uint8_t)0);
         if (om & O_REW) ost(ov.reward + ie, reward);
-        if (om & O_NSH) ost(ov.n_shaped + ie, (uint8_t)1);
+        if (om & O_NSH) ost(ov.n_shaped + ie, (uint8_t)pops);
         if (!MGN_TRIO_GST && (om & O_TS)) ost(ov.timestamp + ie, (uint64_t)sh.ts[prv][el]);
         if (D == 1) {
           if (om & O_AREW) ost(ov.agent_reward + ie, rin_s);
-          if (om & O_SHP) ost(ov.shaped + ie, shaped_s);
+          if (!NST && (om & O_SHP)) ost(ov.shaped + ie, shaped_s);
         }
       }
 #endif
@@ -722,6 +889,14 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
   return;
 #endif
   if (!live) return;
+  if constexpr (NST) {
+    const double* ring = s_nst + (size_t)el * 2 * p.nstep;
+    for (int i = ls; i < p.nstep; i += S) p.nring[(size_t)env * p.nstep + i] = ring[i];
+    if (ls == 0) {
+      p.nlen[env] = nlen;
+      p.nhead[env] = nhead;
+    }
+  }
   if (ls == 0) {
     if (WIN) {
       p.rhead[env] = rhead;

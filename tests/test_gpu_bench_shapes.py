@@ -9,10 +9,10 @@
     set) bit-exact against the oracle, `done` observed in every launch.
   * C5 at its bench shape: 8192 envs x 16 replay assets (bench.c5_paths, the
     HDFSourceSingle file the bench writes, cache 10000, env stride 997), W = 64,
-    DDR, two 64-step mgn_rollout_hist launches with every step's window
-    (mgn_window_hist) and every output against the oracle's
-    StackerDiscrete.current_data after each step; auto-resets inside both
-    launches refill the window.
+    DDR, 64-step mgn_rollout_hist launches (until two launches with episode
+    ends have run) with every output and the step windows (mgn_window_hist)
+    against the oracle's StackerDiscrete.current_data after each step; the
+    windows the auto-resets refill are all checked.
 """
 import os
 import sys
@@ -61,11 +61,11 @@ def test_c3_full_grid_forced_resets(gpu):
                 assert np.array_equal(o[k], ref[k]), f"K=20 {k}"
             assert np.array_equal(o["timestamp"].astype(np.uint64), ref["timestamp"])
             close(o["reward"], ref["reward"], "K=20 reward")
-            close(o["shaped"], ref["shaped"], "K=20 shaped")
+            close(o["shaped"], ref["shaped"], "K=20 shaped", rtol=1e-10)
         else:
             o = _host(g.rollout(acts[k0:k0 + K]))
             ref = orc.rollout(a[k0:k0 + K], threads=THREADS)
-            out_check(o, ref, f"C3 forced K={K}")
+            out_check(o, ref, f"C3 forced K={K}", shaped_rtol=1e-10)
         ends = int(o["done"].sum())
         assert ends > N // 10, f"K={K}: {ends} episode ends"  # rollbacks all over the grid
         k0 += K
@@ -98,12 +98,18 @@ def test_c5_bench_shape_windows(gpu, tmp_path):
     first, second, _, _ = O.hdf_bounds(ts, 0, 0)
     orc = O.OracleBatch(dict(kw, n_envs=N, n_feats=A, auto_reset=1), [(O.SRC_REPLAY, [])] * A)
     assert orc.set_replay(price, price, ts, first, second, 10_000, 997) == g._tape["ts"].shape[0]
-    acts = g.generate_actions(2 * K, seed=0x6D6164)
+    # C5's first episodes end after a few hundred steps (the 2 % cost drains
+    # equity below 0.1 initCash): launches run until two launches with episode
+    # ends have been checked; every output of every step is checked, and every
+    # step's window in the first launch and from the first launch with resets on
+    MAXL = 16
+    acts = g.generate_actions(MAXL * K, seed=0x6D6164)
     a = acts.cpu().numpy()
-    dones = []
-    for launch in range(2):  # the second launch starts from the first's ring
+    dones, checked = [], 0
+    for launch in range(MAXL):  # each launch starts from the previous one's ring
         out, (wp, wo, wt) = g.rollout_window(acts[launch * K:(launch + 1) * K], per_step=True)
         torch.cuda.synchronize()
+        windows = launch == 0 or any(dones)
         d = 0
         for k in range(K):
             r = orc.rollout(a[launch * K + k:launch * K + k + 1], threads=THREADS)
@@ -113,13 +119,17 @@ def test_c5_bench_shape_windows(gpu, tmp_path):
             for f in ("risk", "done", "margin_call", "data_end"):
                 assert np.array_equal(out[f][k].cpu().numpy(), r[f][0]), f"{tag} {f}"
             close(out["reward"][k].cpu().numpy(), r["reward"][0], f"{tag} reward")
-            close(out["shaped"][k].cpu().numpy(), r["shaped"][0], f"{tag} shaped")
+            close(out["shaped"][k].cpu().numpy(), r["shaped"][0], f"{tag} shaped", rtol=1e-10)
             d += int(r["done"].sum())
-            rpr, rpo, rts = orc.window()
-            assert_bits(wp[k].cpu().numpy(), rpr, f"{tag} window price")
-            assert_bits(wo[k].cpu().numpy(), rpo, f"{tag} window portfolio")
-            assert np.array_equal(wt[k].cpu().numpy().astype(np.uint64), rts), f"{tag} window ts"
+            if windows or d:
+                rpr, rpo, rts = orc.window()
+                assert_bits(wp[k].cpu().numpy(), rpr, f"{tag} window price")
+                assert_bits(wo[k].cpu().numpy(), rpo, f"{tag} window portfolio")
+                assert np.array_equal(wt[k].cpu().numpy().astype(np.uint64), rts), f"{tag} window ts"
         dones.append(d)
         del out, wp, wo, wt
-    assert min(dones) > 0, dones
+        checked += 1 if d and any(dones[:-1]) else 0
+        if checked >= 1 and sum(1 for x in dones if x) >= 2:
+            break
+    assert sum(1 for x in dones if x) >= 2, dones
     state_check(g, orc, "C5 end")

@@ -66,7 +66,7 @@ def gen_state_check(g, orc, tag=""):
     assert np.array_equal(d, orc.field(O.F_DIR).astype(np.int64)), tag
 
 
-def out_check(o, ref, tag="", D=1):
+def out_check(o, ref, tag="", D=1, shaped_rtol=None):
     assert_bits(o["obs_price"], ref["obs_price"], f"{tag} obs_price")
     assert_bits(o["obs_port"], ref["obs_port"], f"{tag} obs_port")
     assert_bits(o["tprice"], ref["tprice"], f"{tag} tprice")
@@ -78,7 +78,12 @@ def out_check(o, ref, tag="", D=1):
     assert np.array_equal(np.asarray(o["timestamp"]).astype(np.uint64), ref["timestamp"]), f"{tag} ts"
     close(o["reward"], ref["reward"], f"{tag} reward")
     close(o["agent_reward"], ref["agent_reward"], f"{tag} agent_reward")
-    close(o["shaped"], ref["shaped"], f"{tag} shaped")
+    # shaped: DDR / DSR of the device-log reward; near-cancelling numerators
+    # amplify the log's last-bit differences (north-star bar: 1e-6)
+    if shaped_rtol is None:
+        close(o["shaped"], ref["shaped"], f"{tag} shaped")
+    else:
+        close(o["shaped"], ref["shaped"], f"{tag} shaped", rtol=shaped_rtol)
 
 
 @pytest.mark.parametrize("name,sources", [
@@ -298,6 +303,9 @@ def test_nstep_rollout(gpu, shaper, mode, n):
     (3, dict(reward_shaper="DSR", reward_mode="agent_per_asset")),
     (4, dict(reward_shaper="PPC", cosine_temp=0.05, window=8, norm_type="log")),
     (2, dict(reward_shaper="sortino_shaperA", sortino_exp=2, reward_mode="agent_sum", window=5)),
+    (4, dict(reward_shaper="DSR", nstep_return=5, discount=0.9)),
+    (8, dict(reward_shaper="PPC", cosine_temp=0.05, nstep_return=3, reward_mode="agent_sum")),
+    (2, dict(reward_shaper=None, nstep_return=7, discount=0.95)),
 ])
 def test_schedules_bit_identical(gpu, A, kw):
     """The two-role kernel (k_step_duo: generator waves + ledger waves), the
@@ -313,7 +321,11 @@ def test_schedules_bit_identical(gpu, A, kw):
     rng = np.random.default_rng(A)
     units = rng.normal(0, 3e3, (N, A))
     res = []
-    trio_ok = A <= 8 and kw.get("nstep_return", 1) == 1
+    # trio_eligible (mgn_api.hip): 2..8 assets; n-step only for a scalar reward
+    # without a window and a non-naive shaper (DSR / DDR / PPC / none)
+    nst = kw.get("nstep_return", 1) > 1
+    trio_ok = 2 <= A <= 8 and (not nst or (kw.get("reward_mode") != "agent_per_asset" and not kw.get("window")
+                                          and kw.get("reward_shaper") in (None, "DSR", "DDR", "PPC")))
     for sched in (L.SCHED_SINGLE, L.SCHED_DUO) + ((L.SCHED_TRIO,) if trio_ok else ()):
         g = BatchedEnv(spec, N, **base, **kw)
         L.check(g.lib.mgn_set_schedule(g.h, sched), g.h)

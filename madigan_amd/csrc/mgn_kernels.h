@@ -333,11 +333,8 @@ __device__ __noinline__ double sinedyn_tick(const double* q, double* ax, bool tr
 // RP: the kernel may serve a replay tape (k_step); AUX: multi-component kinds
 // (views.aux).  The two-role kernel compiles neither (their calls would cost
 // the hot generator registers) and is not selected for such handles.
-// use_pre: slot m's slot-0 draws of this tick were computed ahead into pre
-// (draw0 of the same counter: the same bits); else they are drawn here
 template <int M, bool RP = true, bool AUX = true>
-__device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, uint64_t tick,
-                                         bool use_pre = false, Draw pre = Draw{0.0, 0.0, 0u}) {
+__device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, uint64_t tick) {
   if (RP && p.replay) {
     // HDFSourceSingle::getData (DataSource.cpp:391-398) on the tape: the
     // row iterCache / loadData would serve, then advance (wrap = the
@@ -374,8 +371,7 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
                        kind == MGN_SRC_TRENDYOU || kind == MGN_SRC_GAUSSIAN || kind == MGN_SRC_OUPAIR ||
                        (sine_fam && q[5] != 0.0);
     Draw d = {0.0, 0.0, 0u};
-    if (use_pre) d = pre;
-    else if (need0) d = draw0(p.seed, genv, (uint32_t)a, tick);
+    if (need0) d = draw0(p.seed, genv, (uint32_t)a, tick);
     if (kind == MGN_SRC_TRENDOU) {
       double y = s.P[m];
       if (s.tfl[m] & 1) {

@@ -12,3 +12,11 @@ extern "C" int mgn_diag_wall(unsigned long long* h) {
   return hipMemcpyFromSymbol(h, HIP_SYMBOL(mgn::g_duo_wall), 2048 * 32 * sizeof(unsigned long long)) != hipSuccess;
 }
 #endif
+#ifdef MGN_ITERSTAMP
+extern "C" int mgn_diag_iter(unsigned long long* h) {
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(mgn::g_iter), 256 * 64 * sizeof(unsigned long long)) != hipSuccess)
+    return 1;
+  static unsigned long long z[256 * 64] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(mgn::g_iter), z, sizeof(z)) != hipSuccess;
+}
+#endif

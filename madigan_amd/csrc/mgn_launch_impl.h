@@ -84,7 +84,7 @@ void launch_trio(const StepArgs& a) {
   const bool disc = a.in_kind == IN_DISCRETE;
   const uint32_t om = traj_mask(a.out);
   if (a.p.nstep > 1) {  // NST: the finish role's NStepBuffer rings in dynamic LDS (no window, D = 1)
-    const size_t lds = (size_t)epb * 2 * a.p.nstep * sizeof(double);
+    const size_t lds = (size_t)epb * 2 * nst_pad(a.p.nstep) * sizeof(double);
     auto goN = [&](auto kern) {
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       launch_timed(a.ev0, a.ev1, kern, dim3(grid), dim3(small ? 192 : TRIO_BLOCK), (uint32_t)lds, a.stream,

@@ -40,6 +40,21 @@
 
 namespace mgn {
 
+#ifdef MGN_ITERSTAMP
+// diagnostic build: s_memtime stamps of the first 256 blocks, 64 slots each --
+// [0] entry, [1] after the prologue barrier, [2 + j] generator lane 0 after
+// iteration j's barrier (j < 40), [44] generator / [45] ledger / [46] finish
+// lane 0 after its epilogue stores (with their completion wait)
+__device__ unsigned long long g_iter[256 * 64];
+#define MGN_IT(slot, lane0)                                             \
+  if (threadIdx.x == (lane0) && blockIdx.x < 256 && (slot) < 64)        \
+    g_iter[blockIdx.x * 64 + (slot)] = __builtin_amdgcn_s_memtime()
+#define MGN_IT_DRAIN() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#else
+#define MGN_IT(slot, lane0)
+#define MGN_IT_DRAIN()
+#endif
+
 constexpr int TRIO_BLOCK = 768;
 constexpr int TRIO_W = 256;  // lanes per role
 // TW = 64 (one wave per role, 192-thread workgroups): small batches, whose
@@ -63,11 +78,18 @@ constexpr int TRIO_W = 256;  // lanes per role
 #ifndef MGN_TRIO_PF
 #define MGN_TRIO_PF 1
 #endif
+#ifndef MGN_TRIO_EARLY_WB  // G / L write their state back right after their last step
+#define MGN_TRIO_EARLY_WB 1
+#endif
 
 // TR_REFILL (WIN): the iteration's tick was an auto-reset refill tick
 // (initialize_history's env.step(), preprocessor.py:191-194): F pushes its
 // window row, nothing else
 enum { TR_STEP = 1, TR_ANYMC = 2, TR_MCALL = 4, TR_REFILL = 8 };
+
+// NST: per env, the ring and the pop's summands in slots of nst_pad(n)
+// doubles (n rounded up to 8: whole rounds of 8 lanes, 64-B aligned)
+__host__ __device__ constexpr int nst_pad(int n) { return (n + 7) & ~7; }
 
 template <int S, int TW = TRIO_W>
 struct TrioShared {
@@ -98,13 +120,14 @@ struct TrioShared {
 // k_step_duo / k_step.
 // NST: n-step aggregation (nstep > 1, scalar reward D = 1) in the finish
 // role: the env's NStepBuffer ring and one pop's summands in dynamic LDS
-// (launch_trio sizes it: envs per block x 2n doubles), the discounts staged
+// (launch_trio sizes it: envs per block x 2 nst_pad(n) doubles), the discounts staged
 // in LDS, so a pop is n LDS reads issued together, not n dependent loads.
 template <int S, bool RQ1, bool DISC, uint32_t OMC = 0, bool WIN = false, int TW = TRIO_W, bool NST = false>
 __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out, int in_kind_rt,
                                                           const double* __restrict__ units_in,
                                                           const int32_t* __restrict__ aidx_in,
                                                           const int8_t* __restrict__ act_in, int K) {
+  MGN_IT(0, 0);
   warm_kernargs<(int)(sizeof(KParams) + sizeof(mgn_traj) + 48)>();
   const int in_kind = DISC ? IN_DISCRETE : in_kind_rt;
   constexpr int M = 1;
@@ -116,7 +139,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
   __shared__ mgn_asset_source s_src[S];
   __shared__ double s_tgt[MGN_MAX_ASSETS + 1];
   __shared__ double s_disc[NST ? MGN_MAX_NSTEP : 1];                     // NST: gamma^k
-  extern __shared__ __attribute__((aligned(16))) double s_nst[];          // NST: (EPB, 2n)
+  extern __shared__ __attribute__((aligned(16))) double s_nst[];          // NST: (EPB, 2 nst_pad(n))
   const int role = threadIdx.x / TRIO_W;  // 0 generator, 1 ledger, 2 finish
   const int l = threadIdx.x % TRIO_W;
   const int el = l / S;
@@ -190,7 +213,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
       nlen = p.nlen[envc];
       nhead = p.nhead[envc];
       // the env's ring into LDS (every lane of the env copies a share)
-      double* ring = s_nst + (size_t)el * 2 * p.nstep;
+      double* ring = s_nst + (size_t)el * 2 * nst_pad(p.nstep);
       for (int i = ls; i < p.nstep; i += S) ring[i] = p.nring[(size_t)envc * p.nstep + i];
     }
   }
@@ -219,6 +242,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
   if (threadIdx.x < 8) s_duo_sub[threadIdx.x] = 0;
 #endif
   __syncthreads();
+  MGN_IT(1, 0);
   s.kind[0] = s.valid[0] ? s_src[ls].kind : -1;
 
   if (role == 0) {
@@ -241,26 +265,29 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     int jn = 0;
 #endif
     int gpend = 0;  // WIN: refill ticks still to come after the reset tick
-    // Draw-ahead, two stages: in the iteration of tick t the generator lanes
-    // also turn the Philox block of counter t + 1 (drawn an iteration
-    // earlier) into that tick's variates (Box-Muller) and draw the Philox
-    // block of counter t + 2 -- three independent dependency chains in one
-    // iteration instead of one chain of block -> Box-Muller -> tick.  A draw
-    // is a pure function of (seed, env, asset, counter), so a rollback or
-    // reset that changes the counter only sends the tick back to drawing
-    // itself.  Lanes whose kind draws nothing skip it.
-    const uint64_t genv = (uint64_t)(p.env_offset + env);
-    bool draws = false;
-    if (s.valid[0]) {
-      const int kd = s.kind[0];
-      draws = kd == MGN_SRC_TRENDOU || kd == MGN_SRC_OU || kd == MGN_SRC_SIMPLETREND || kd == MGN_SRC_TRENDYOU ||
-              kd == MGN_SRC_GAUSSIAN || kd == MGN_SRC_OUPAIR ||
-              ((kd == MGN_SRC_SINE || kd == MGN_SRC_SAWTOOTH || kd == MGN_SRC_TRIANGLE) && s_src[ls].p[5] != 0.0);
-    }
-    Draw nd = {0.0, 0.0, 0u};  // variates of counter nd_ts
-    uint64_t nd_ts = ~0ull;
-    u4 nx = {0u, 0u, 0u, 0u};  // Philox block (slot 0) of counter nx_ts
-    uint64_t nx_ts = ~0ull;
+    // the source state write-back: issued right after the launch's last tick
+    // (beside the pipeline's last finish iteration) and again at exit only if
+    // a rollback or reset changed the state after it; fields a kind never
+    // writes are not stored (their value in HBM is the one loaded)
+    const int kd = s.kind[0];
+    const bool w_sx = kd == MGN_SRC_SINE || kd == MGN_SRC_SAWTOOTH || kd == MGN_SRC_TRIANGLE || kd == MGN_SRC_TRENDYOU;
+    const bool w_oum = kd == MGN_SRC_TRENDOU || kd == MGN_SRC_TRENDYOU || kd == MGN_SRC_OUPAIR;
+    const bool w_trend = kd == MGN_SRC_TRENDOU || kd == MGN_SRC_SIMPLETREND || kd == MGN_SRC_TRENDYOU;
+    bool g_dirty = true;
+    auto g_store = [&]() {
+      if (s.valid[0]) {
+        const size_t i = (size_t)env * A + s.asset[0];
+        p.P[i] = s.P[0];
+        if (w_sx) p.sx[i] = s.sx[0];
+        if (w_oum) p.oum[i] = s.oum[0];
+        if (w_trend) {
+          p.dy[i] = s.dy[0];
+          p.tlen[i] = s.tlen[0];
+          p.tfl[i] = s.tfl[0];
+        }
+      }
+      if (ls == 0) p.ts[env] = ts;
+    };
     for (int j = 0;; ++j) {
       const int cur = j & 1, prv = cur ^ 1;
       MGN_T(T0);
@@ -273,7 +300,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
           gen_tick<M, false, false>(s, p, env, ts);
           ts = ts + 1;
           gpend -= 1;
+          g_dirty = true;
         } else if (rst) {
+          g_dirty = true;
           if (prev_step) {  // roll the speculative tick back
             s.P[0] = svP;
             s.sx[0] = svSx;
@@ -298,22 +327,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
           svTfl = s.tfl[0];
           svTs = ts;
 #ifndef MGN_TRIO_ABL_G  // diagnostic timing build: no tick (prices frozen)
-          gen_tick<M, false, false>(s, p, env, ts, nd_ts == ts, nd);
+          gen_tick<M, false, false>(s, p, env, ts);
 #endif
           ts = ts + 1;
-#if !defined(MGN_ABL_DRAW) && !defined(MGN_TRIO_NO_DRAWAHEAD)
-          if (draws && k + 1 < K) {
-            // variates of counter ts (the next tick) from the block drawn last
-            // iteration, and the block of counter ts + 1
-            const u4 xb = (nx_ts == ts) ? nx : block(p.seed, genv, (uint32_t)s.asset[0], 0u, ts);
-            if (k + 2 < K) {
-              nx = block(p.seed, genv, (uint32_t)s.asset[0], 0u, ts + 1);
-              nx_ts = ts + 1;
-            }
-            nd = draw_from(xb);
-            nd_ts = ts;
-          }
-#endif
           // State.price and timestamp of step k (overwritten if rolled back)
           if (MGN_TRIO_GST) {
             const size_t oN = (size_t)k * p.N;
@@ -321,6 +337,10 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
             if (ls == 0 && (om & O_TS)) ost(ov.timestamp + (oN + env), (uint64_t)ts);
           }
           k += 1;
+          if (MGN_TRIO_EARLY_WB && k == K) {  // the launch's last tick: write the state back now
+            g_store();
+            g_dirty = false;
+          }
         }
       }
       sh.price[cur][l] = s.P[0];
@@ -328,6 +348,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
       MGN_T(T1);
       __syncthreads();
       MGN_T(T2);
+      MGN_IT(2 + (j < 40 ? j : 40), 0);
 #ifdef MGN_STAMPS
       acc0 += T1 - T0;
       acc1 += T2 - T1;
@@ -346,17 +367,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
 #ifdef MGN_TRIO_ABL_EPI  // diagnostic timing build: no state write-back
     return;
 #endif
-    if (!live) return;
-    if (s.valid[0]) {
-      const size_t i = (size_t)env * A + s.asset[0];
-      p.P[i] = s.P[0];
-      p.sx[i] = s.sx[0];
-      p.oum[i] = s.oum[0];
-      p.dy[i] = s.dy[0];
-      p.tlen[i] = s.tlen[0];
-      p.tfl[i] = s.tfl[0];
-    }
-    if (ls == 0) p.ts[env] = ts;
+    if (live && g_dirty) g_store();
+    MGN_IT_DRAIN();
+    MGN_IT(44, 0);
     return;
   }
 
@@ -376,6 +389,18 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     drain_vmem();
     int k = 0;
     int lpend = 0;  // WIN: refill ticks still to come after the reset tick
+    // the ledger write-back: right after the launch's last step, again at
+    // exit only if a rollback (fresh Broker) changed it afterwards
+    bool l_dirty = true;
+    auto l_store = [&]() {
+      if (s.valid[0]) {
+        const size_t i = (size_t)env * A + s.asset[0];
+        p.L[i] = s.L[0];
+        p.mep[i] = s.mep[0];
+        p.Bm[i] = s.Bm[0];
+      }
+      if (ls == 0) p.cash[env] = cash;
+    };
     __builtin_amdgcn_s_setprio(MGN_TRIO_PL);  // the orders are the critical path
 #ifdef MGN_STAMPS
     unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0;
@@ -397,6 +422,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
         // iteration j-1 is void; a fresh Broker (Env.h:181-187) waits for the
         // reset tick's prices
         if (prev_step) k -= 1;
+        l_dirty = true;
         s.L[0] = 0.;
         s.mep[0] = 0.;
         s.Bm[0] = 0.;
@@ -485,6 +511,10 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
         }
         flags = TR_STEP | (any_mc ? TR_ANYMC : 0) | (mcall ? TR_MCALL : 0);
         k += 1;
+        if (MGN_TRIO_EARLY_WB && k == K && live) {  // the launch's last step: write the ledger back now
+          l_store();
+          l_dirty = false;
+        }
       }
       if (WIN && refill) {
         // the refill row's portfolio (the fresh Broker's): F evaluates it
@@ -517,14 +547,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
 #ifdef MGN_TRIO_ABL_EPI  // diagnostic timing build: no state write-back
     return;
 #endif
-    if (!live) return;
-    if (s.valid[0]) {
-      const size_t i = (size_t)env * A + s.asset[0];
-      p.L[i] = s.L[0];
-      p.mep[i] = s.mep[0];
-      p.Bm[i] = s.Bm[0];
-    }
-    if (ls == 0) p.cash[env] = cash;
+    if (live && l_dirty) l_store();
+    MGN_IT_DRAIN();
+    MGN_IT(45, TRIO_W);
     return;
   }
 
@@ -674,31 +699,52 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
         arr[0] = ar;
         rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(arr) : reward;
         const int n = p.nstep;
-        double* ring = s_nst + (size_t)el * 2 * n;
-        double* scr = ring + n;
+        double* ring = s_nst + (size_t)el * 2 * nst_pad(n);  // ring, then the pop's summands
+        double* scr = ring + nst_pad(n);
         const double v = (p.shaper == MGN_SHAPER_PPC) ? rin_s + cos_term : rin_s;
         const int L1 = nlen + 1;
         pops = done ? L1 : (L1 >= n ? 1 : 0);
         MGN_G double* row = (om & O_SHP) ? ov.shaped + kidx(k, sN, (size_t)env) * (size_t)n : nullptr;
-        if (!done && L1 >= n) {
-          // the common case, one pop of a full buffer: term kk on lane kk mod S
-          // (nstep_column's operands), then every lane of the env sums the terms
-          // in kk order from LDS (the reads issue together)
-          int tail = nhead + nlen;
-          tail -= (tail >= n) ? n : 0;
-          if (ls == 0) ring[tail] = v;
+        // append v; then the pops (one when the buffer is full, every entry
+        // on done), each by all the env's lanes: summand kk on lane kk mod S
+        // (nstep_column's operands) into LDS, slots [len, R S) +0.0 (the
+        // ordered sum is unchanged: acc starts at +0.0 and is never -0.0),
+        // then every lane sums them in kk order (S per chunk, the next
+        // chunk's reads issued before this chunk's adds); the shaper state
+        // steps between pops as nstep_column's does
+        int tail = nhead + nlen;
+        tail -= (tail >= n) ? n : 0;
+        if (ls == 0) ring[tail] = v;
+        int len = L1, head = nhead;
+        for (int pj = 0; pj < pops; ++pj) {
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           const PopPre c = pop_pre(p.shaper, g.shA, g.shB);
-          for (int kk = ls; kk < L1; kk += S) {
-            int idx = nhead + kk;
-            idx -= (idx >= n) ? n : 0;
+          const int R = (len + S - 1) / S;
+          for (int j = 0; j < R; j += 2) {
+            double rr[2], dd[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const int kk = ls + (j + u) * S;
+              int idx = head + kk;
+              idx -= (idx >= n) ? n : 0;
+              const bool ok = kk < len && j + u < R;
+              rr[u] = ring[ok ? idx : 0];
+              dd[u] = s_disc[ok ? kk : 0];
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const int kk = ls + (j + u) * S;
+              if (j + u < R) {
 #ifdef MGN_NST_ABL_TERM  // diagnostic timing build (outputs wrong): no summand arithmetic
-            scr[kk] = ring[idx];
+                const double t = rr[u];
 #else
-            scr[kk] = pop_term(p.shaper, ring[idx], g.shA, g.shB, c, s_disc[kk]);
+                const double t = pop_term(p.shaper, rr[u], g.shA, g.shB, c, dd[u]);
 #endif
+                scr[kk] = (kk < len) ? t : 0.0;
+              }
+            }
           }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
@@ -706,21 +752,29 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
           double acc = 0.0;
 #ifdef MGN_NST_ABL_SUM  // diagnostic timing build (outputs wrong): no ordered sum
           acc = scr[0];
-          for (int k0 = L1; k0 < L1; k0 += 8) {
 #else
-          for (int k0 = 0; k0 < L1; k0 += 8) {
-#endif
-            double t[8];
+          const d2* sc = reinterpret_cast<const d2*>(scr);
+          d2 cur[S / 2];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) t[u] = (k0 + u < L1) ? scr[k0 + u] : 0.0;
+          for (int u = 0; u < S / 2; ++u) cur[u] = sc[u];
+          for (int j = 0; j < R; ++j) {
+            d2 nxt[S / 2];
+            const int jn = (j + 1 < R) ? j + 1 : j;
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-              if (k0 + u < L1) acc += t[u];
+            for (int u = 0; u < S / 2; ++u) nxt[u] = sc[jn * (S / 2) + u];
+#pragma unroll
+            for (int u = 0; u < S / 2; ++u) {
+              acc += cur[u].x;
+              acc += cur[u].y;
+            }
+#pragma unroll
+            for (int u = 0; u < S / 2; ++u) cur[u] = nxt[u];
           }
+#endif
           double res = acc;
           if (p.shaper == MGN_SHAPER_DSR || p.shaper == MGN_SHAPER_DDR) {
-            res = clip1(acc / L1);
-            const double r0 = ring[nhead];
+            res = clip1(acc / len);
+            const double r0 = ring[head];
             g.shA += p.eta * (r0 - g.shA);
             if (p.shaper == MGN_SHAPER_DSR) {
               g.shB += p.eta * (r0 * r0 - g.shB);
@@ -730,55 +784,14 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
               g.shB += p.eta * (m * m - g.shB);
             }
           }
-          if (row) {
-            if (ls == 0) ost(row, res);
-#ifndef MGN_NST_ABL_ROW  // diagnostic timing build (outputs wrong): no zero entries
-            for (int jj = 1 + ls; jj < n; jj += S) ost(row + jj, 0.);
-#endif
-          }
-        } else {
-          // filling (no pop) or a done flush (every entry popped, A / B
-          // updated between pops): nstep_column's statements on the env's
-          // lane 0 over the LDS ring (DSR / DDR / PPC / none: the trio is not
-          // selected for the naive shapers), the shaper state then broadcast
-          if (ls == 0) {
-            int len = L1, head = nhead, pj = 0;
-            int tail = nhead + nlen;
-            tail -= (tail >= n) ? n : 0;
-            ring[tail] = v;
-            while (len >= n || (done && len > 0)) {
-              const PopPre c = pop_pre(p.shaper, g.shA, g.shB);
-              double acc = 0.0;
-              for (int kk = 0, idx = head; kk < len; ++kk, idx = (idx + 1 == n) ? 0 : idx + 1)
-                acc += pop_term(p.shaper, ring[idx], g.shA, g.shB, c, s_disc[kk]);
-              double res = acc;
-              if (p.shaper == MGN_SHAPER_DSR || p.shaper == MGN_SHAPER_DDR) {
-                res = clip1(acc / len);
-                const double r0 = ring[head];
-                g.shA += p.eta * (r0 - g.shA);
-                if (p.shaper == MGN_SHAPER_DSR) {
-                  g.shB += p.eta * (r0 * r0 - g.shB);
-                } else {
-                  double m = r0 < 0. ? r0 : 0.;
-                  if (r0 != r0) m = r0;
-                  g.shB += p.eta * (m * m - g.shB);
-                }
-              }
-              if (row) ost(row + pj, res);
-              head = (head + 1 == n) ? 0 : head + 1;
-              len -= 1;
-              pj += 1;
-              if (!done && len < n) break;
-            }
-            if (row)
-              for (int j = pj; j < n; ++j) ost(row + j, 0.);
-          }
-          g.shA = seg_bcast<S, 0>(g.shA);
-          g.shB = seg_bcast<S, 0>(g.shB);
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          if (row && ls == 0) ost(row + pj, res);
+          head = (head + 1 == n) ? 0 : head + 1;
+          len -= 1;
         }
+#ifndef MGN_NST_ABL_ROW  // diagnostic timing build (outputs wrong): no zero entries
+        if (row)
+          for (int jj = pops + ls; jj < n; jj += S) ost(row + jj, 0.);
+#endif
         nhead += pops;
         while (nhead >= n) nhead -= n;
         nlen = L1 - pops;
@@ -890,7 +903,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
 #endif
   if (!live) return;
   if constexpr (NST) {
-    const double* ring = s_nst + (size_t)el * 2 * p.nstep;
+    const double* ring = s_nst + (size_t)el * 2 * nst_pad(p.nstep);
     for (int i = ls; i < p.nstep; i += S) p.nring[(size_t)env * p.nstep + i] = ring[i];
     if (ls == 0) {
       p.nlen[env] = nlen;
@@ -913,6 +926,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     p.sA[(size_t)env * A + s.asset[0]] = g.shA;
     p.sB[(size_t)env * A + s.asset[0]] = g.shB;
   }
+  MGN_IT_DRAIN();
+  MGN_IT(46, 2 * TRIO_W);
 }
 
 }  // namespace mgn

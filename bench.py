@@ -492,6 +492,15 @@ def main():
                 "fused_note": "what the fused kernel must move (state held in registers across "
                               "the launch's steps; PMC traffic matches this figure)",
                 "compute_issue": valu_issue(workload, avg_launch_s)}
+        if traffic:
+            # the bytes the kernel really moves (PMC, per launch) over the same
+            # launch time: `achieved`/`frac` stay on the algorithmic bytes the
+            # roofline contract prices, this is the HBM the launch used
+            roof["measured_traffic_GBs"] = traffic / avg_launch_s / 1e9
+            roof["measured_traffic_frac"] = roof["measured_traffic_GBs"] / PEAK_HBM_GBS
+            roof["measured_traffic_note"] = ("PMC (2*FETCH_SIZE + WRITE_SIZE) * 1024 B per launch / "
+                                             "avg_launch_us; below `achieved` because the fused "
+                                             "kernel keeps the state in registers across steps")
         if probe:
             roof["attainable_copy_GBs"] = probe
             roof["frac_of_attainable"] = achieved_gbs / probe
@@ -671,6 +680,7 @@ def windowed(args, world, rank, dev):
                          "bytes_per_env_step": gb / (N * Kf),
                          "avg_launch_us": gather_us},
             "step_launch_avg_us": step_us,
+            "step_launch_traffic": load_pmc_traffic(f"{wl}_step_{N}x{A}_fuse{Kf}")[0],
             "step_launch_note": "the K-step step kernel" + (
                 " (the previous launch's k_hist_gather runs beside it on a second stream)"
                 if args.win_overlap else ""),

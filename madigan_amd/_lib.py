@@ -217,6 +217,27 @@ def load(path: str = ""):
     return lib
 
 
+_pycall = None
+
+
+def pycall():
+    """The CPython binding of mgn_rollout (`_mgn_pycall`, csrc/mgn_pycall.c,
+    linked against the in-tree libmadigan_hip.so), or None when the loaded
+    library is another build (MADIGAN_LIB_PATH) or the binding is not built:
+    the launcher then calls through ctypes."""
+    global _pycall
+    if _pycall is None:
+        lib = load()
+        mod = False
+        if os.path.realpath(lib._name) == os.path.realpath(LIB_PATH):
+            try:
+                from . import _mgn_pycall as mod
+            except ImportError:
+                mod = False
+        _pycall = mod
+    return _pycall or None
+
+
 def check(status: int, handle=None) -> None:
     if status == OK:
         return

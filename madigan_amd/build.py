@@ -69,6 +69,34 @@ def build_hdf(force: bool = False, verbose: bool = False) -> str:
     return HDF_OUT
 
 
+PYCALL_SRC = os.path.join(CSRC, "mgn_pycall.c")
+
+
+def pycall_out() -> str:
+    import sysconfig
+    return os.path.join(HERE, "_mgn_pycall" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_pycall(force: bool = False, verbose: bool = False) -> str:
+    """_mgn_pycall: the CPython binding of mgn_rollout (host C, linked against
+    the in-tree libmadigan_hip.so, found next to it through $ORIGIN)."""
+    import sysconfig
+    out = pycall_out()
+    deps_ = [PYCALL_SRC, OUT, os.path.join(ROOT, "include", "madigan_amd.h")]
+    if not force and os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps_):
+        return out
+    cmd = [shutil.which("gcc") or "gcc", "-O2", "-fPIC", "-shared", "-Wall",
+           f"-I{sysconfig.get_paths()['include']}", f"-I{os.path.join(ROOT, 'include')}",
+           "-o", out + ".tmp", PYCALL_SRC, f"-L{HERE}", "-l:libmadigan_hip.so", "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"gcc failed on {PYCALL_SRC}:\n{r.stderr}")
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def deps():
     return sources() + glob.glob(os.path.join(CSRC, "*.h")) + [
         os.path.join(ROOT, "include", "madigan_amd.h")]
@@ -84,6 +112,7 @@ def needs_build() -> bool:
 def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
     build_hdf(force=force, verbose=verbose)
     if not force and not needs_build():
+        build_pycall(verbose=verbose)
         return OUT
     os.makedirs(OBJ, exist_ok=True)
     cc = hipcc()
@@ -108,6 +137,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(OUT + ".tmp", OUT)
+    build_pycall(force=True, verbose=verbose)
     return OUT
 
 

@@ -339,7 +339,7 @@ bool trio_eligible(const mgn_env* e) {
   // (its output indices are k x a 32-bit stride: N (A + 1), N F and N n fit 32 bits)
   const uint64_t row = (uint64_t)(e->A + 1 > e->F ? e->A + 1 : e->F);
   const bool nst_ok = e->cfg.nstep == 1 || (e->D == 1 && e->W == 0 && e->cfg.shaper < MGN_SHAPER_SHARPE);
-  return e->apad >= 2 && e->apad <= 8 && !e->cfg.aux && !e->replay && nst_ok &&
+  return e->apad >= 2 && e->apad <= 16 && !e->cfg.aux && !e->replay && nst_ok &&
          (uint64_t)e->N * row < (1ull << 32) && (uint64_t)e->N * (uint64_t)e->cfg.nstep < (1ull << 32);
 }
 // automatic: where the single-role kernel would run one lane per asset (small
@@ -355,7 +355,7 @@ void choose_sched(mgn_env* e) {
     e->trio = trio_eligible(e);
     e->duo = !e->trio && duo_eligible(e);
   } else {
-    e->trio = trio_eligible(e) && e->m == 1;
+    e->trio = trio_eligible(e) && e->m == 1 && e->apad <= 8;
     e->duo = !e->trio && duo_eligible(e) && e->m == 1;
   }
 }
@@ -384,7 +384,7 @@ void launch_step(const mgn_env* e, const mgn_traj& out, int in_kind, const doubl
                  const int32_t* aidx, const int8_t* act, int K, hipEvent_t ev0, hipEvent_t ev1) {
   mgn::StepArgs a{kparams(e), out, in_kind, units, aidx, act, K, e->stream, ev0, ev1};
   if (e->trio) {
-    const int idx = e->apad <= 2 ? 1 : e->apad <= 4 ? 2 : 3;
+    const int idx = e->apad <= 2 ? 1 : e->apad <= 4 ? 2 : e->apad <= 8 ? 3 : 4;
     kTrio[idx](a);
     return;
   }

@@ -187,7 +187,7 @@ void dispatch_m(int m, const Arg& a) {
     if constexpr (A >= 2 && A <= 16) launch_duo<A>(a);                                       \
   }                                                                                          \
   void launch_trio_a##A(const StepArgs& a) {                                                 \
-    if constexpr (A >= 2 && A <= 8) launch_trio<A>(a);                                       \
+    if constexpr (A >= 2 && A <= 16) launch_trio<A>(a);                                       \
   }                                                                                          \
   void launch_step_a##A(int m, const StepArgs& a) { dispatch_m<StepL, A>(m, a); }            \
   void launch_init_a##A(int m, const InitArgs& a) { dispatch_m<InitL, A>(m, a); }            \

@@ -505,6 +505,14 @@ class BatchedEnv:
         host work is the ctypes call).  The caller keeps ``out`` alive."""
         K = int(k_steps)
         t = self._traj_for(out, K)
+        pc = L.pycall()
+        if pc is not None:  # the CPython binding: no ctypes conversion per call
+            f, hv, tv = pc.rollout, int(self.h), C.addressof(t)
+
+            def launch(actions_ptr: int) -> int:
+                return f(hv, actions_ptr, K, tv)
+            launch._keep = t  # the mgn_traj the address points at
+            return launch
         ref = C.byref(t)
         fn, h = self.lib.mgn_rollout, self.h
 

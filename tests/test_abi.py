@@ -130,3 +130,18 @@ def test_no_cpu_fallback():
         BatchedEnv(ou_spec([10.], [.1], [.04]), 4)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         Env("OU", 1_000_000)
+
+
+def test_pycall_binding_links_the_in_tree_library():
+    """The CPython binding of mgn_rollout (csrc/mgn_pycall.c) is built next to
+    libmadigan_hip.so, resolves it through $ORIGIN and rejects a null handle
+    before any HIP call (no GPU needed)."""
+    import os
+    from madigan_amd import _lib as L
+    pc = L.pycall()
+    assert pc is not None, "_mgn_pycall is not built (python -m madigan_amd.build)"
+    assert os.path.dirname(pc.__file__) == os.path.dirname(L.LIB_PATH)
+    with pytest.raises(ValueError):
+        pc.rollout(0, 0, 1, 0)
+    with pytest.raises(TypeError):
+        pc.rollout(0, 0)

@@ -321,10 +321,10 @@ def test_schedules_bit_identical(gpu, A, kw):
     rng = np.random.default_rng(A)
     units = rng.normal(0, 3e3, (N, A))
     res = []
-    # trio_eligible (mgn_api.hip): 2..8 assets; n-step only for a scalar reward
+    # trio_eligible (mgn_api.hip): 2..16 assets; n-step only for a scalar reward
     # without a window and a non-naive shaper (DSR / DDR / PPC / none)
     nst = kw.get("nstep_return", 1) > 1
-    trio_ok = 2 <= A <= 8 and (not nst or (kw.get("reward_mode") != "agent_per_asset" and not kw.get("window")
+    trio_ok = 2 <= A <= 16 and (not nst or (kw.get("reward_mode") != "agent_per_asset" and not kw.get("window")
                                           and kw.get("reward_shaper") in (None, "DSR", "DDR", "PPC")))
     for sched in (L.SCHED_SINGLE, L.SCHED_DUO) + ((L.SCHED_TRIO,) if trio_ok else ()):
         g = BatchedEnv(spec, N, **base, **kw)

@@ -1,65 +1,82 @@
-"""Diagnostic: host-side cost around one 20-step C3 launch (the driver's
-bench shape): wall time of [launch; synchronize] with and without the
-library's kernel events, with one or two synchronizes, against the kernel
-time itself (events) and an idle synchronize."""
+"""Host overhead of the driver's timed region (diagnostic): one 20-step launch
+at C3 (8192 x 8) bracketed by torch.cuda.synchronize(), repeated; the median
+wall time by launcher (ctypes / the CPython binding) and kernel-timing mode
+(0 none, 1 marker events, 2 events recorded by the launch).  Run it once with
+the default environment and once with HSA_ENABLE_INTERRUPT=0 to see the
+completion-signal wait.
+
+    python tools/host_overhead.py [--reps 300]
+"""
+import argparse
 import ctypes as C
 import json
 import os
 import sys
 import time
 
-import numpy as np
-import torch
-
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import bench  # noqa: E402
-from madigan_amd import _lib as L  # noqa: E402
-
-env, _, _ = bench.workload_env("C3", 8192, 8, 0, torch.device("cuda:0"))
-lib, h = env.lib, env.h
-K = int(os.environ.get("K", 20))
-acts = env.generate_actions(K * 40, seed=5)
-traj = env.alloc_traj(K, fields=["reward", "shaped", "done", "obs_price", "obs_port", "timestamp",
-                                 "tprice", "tunits", "tcost", "risk", "margin_call"])
-fn = env.rollout_launcher(traj, K)
-base, per = acts.data_ptr(), env.N * env.A
-res = {}
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
-def trial(name, timing, syncs, reps=30):
-    ts = []
-    L.check(lib.mgn_set_timing(h, 1 if timing else 0), h)
-    for r in range(reps):
-        torch.cuda.synchronize()
-        time.sleep(0.002)
-        t0 = time.perf_counter()
-        fn(base + (r % 40) * K * per)
-        for _ in range(syncs):
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=300)
+    ap.add_argument("--k", type=int, default=20)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    import bench
+    from madigan_amd import _lib as L
+    dev = torch.device("cuda:0")
+    env, _, _ = bench.workload_env("C3", 8192, 8, 0, dev)
+    K = a.k
+    acts = env.generate_actions(K * 4, seed=0x6D6164)
+    traj = env.alloc_traj(K, fields=["reward", "shaped", "done", "obs_price", "obs_port", "timestamp",
+                                     "tprice", "tunits", "tcost", "risk", "margin_call"])
+    lib, h = env.lib, env.h
+    t = env._traj_for(traj, K)
+    ref = C.byref(t)
+    fn = lib.mgn_rollout
+    pc = L.pycall()
+    ptr = acts.data_ptr()
+
+    def via_ctypes():
+        return fn(h, ptr, K, ref)
+
+    def via_pycall():
+        return pc.rollout(int(h), ptr, K, C.addressof(t))
+
+    res = {"HSA_ENABLE_INTERRUPT": os.environ.get("HSA_ENABLE_INTERRUPT", "(default)")}
+    for name, call in (("ctypes", via_ctypes), ("pycall", via_pycall)):
+        if call is via_pycall and pc is None:
+            continue
+        for mode in (0, 1, 2):
+            L.check(lib.mgn_set_timing(h, mode), h)
+            for _ in range(20):
+                call()
             torch.cuda.synchronize()
-        ts.append(time.perf_counter() - t0)
-    if timing:
-        tm = (C.c_double * 4)()
-        L.check(lib.mgn_get_timing(h, tm), h)
-        res[name + "_kernel_us"] = tm[0] / tm[1] * 1e3
-    res[name + "_wall_us"] = float(np.median(ts[3:])) * 1e6
+            wall, host = [], []
+            for _ in range(a.reps):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                rc = call()
+                t1 = time.perf_counter()
+                torch.cuda.synchronize()
+                t2 = time.perf_counter()
+                L.check(rc, h)
+                wall.append((t2 - t0) * 1e6)
+                host.append((t1 - t0) * 1e6)
+            tm = (C.c_double * 4)()
+            L.check(lib.mgn_get_timing(h, tm), h)
+            kus = tm[0] / max(tm[1], 1) * 1e3 if mode else None
+            res[f"{name}_mode{mode}"] = {"wall_us_median": float(np.median(wall)),
+                                         "wall_us_p10": float(np.percentile(wall, 10)),
+                                         "launch_call_us_median": float(np.median(host)),
+                                         "kernel_us": kus}
+            print(name, mode, json.dumps(res[f"{name}_mode{mode}"]), flush=True)
+    L.check(lib.mgn_set_timing(h, 0), h)
+    print(json.dumps(res))
 
 
-trial("events_2sync", True, 2)
-trial("events_1sync", True, 1)
-trial("noevents_1sync", False, 1)
-trial("noevents_2sync", False, 2)
-ts = []
-for r in range(30):
-    t0 = time.perf_counter()
-    torch.cuda.synchronize()
-    ts.append(time.perf_counter() - t0)
-res["idle_sync_us"] = float(np.median(ts)) * 1e6
-ts = []
-for r in range(30):
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    fn(base)
-    ts.append(time.perf_counter() - t0)
-    torch.cuda.synchronize()
-res["launch_call_us"] = float(np.median(ts)) * 1e6
-print(json.dumps(res))
+if __name__ == "__main__":
+    main()

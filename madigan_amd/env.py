@@ -507,7 +507,7 @@ class BatchedEnv:
         t = self._traj_for(out, K)
         pc = L.pycall()
         if pc is not None:  # the CPython binding: no ctypes conversion per call
-            f, hv, tv = pc.rollout, int(self.h), C.addressof(t)
+            f, hv, tv = pc.rollout, self.h.value, C.addressof(t)
 
             def launch(actions_ptr: int) -> int:
                 return f(hv, actions_ptr, K, tv)

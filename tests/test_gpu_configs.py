@@ -268,3 +268,35 @@ def test_stats_allgather_rccl_single_rank(gpu):
                                               C.c_void_p(out.data_ptr())), g.h)
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("binding", ["pycall", "ctypes"])
+def test_rollout_launcher_matches_rollout(gpu, binding, monkeypatch):
+    """BatchedEnv.rollout_launcher (bench.py's timed loop) through the CPython
+    binding and through ctypes: the same launches as rollout() into the same
+    output buffers, bit-exact against the oracle (C3 shape, 1- and 20-step)."""
+    from madigan_amd import _lib as L
+    if binding == "ctypes":
+        monkeypatch.setattr(L, "pycall", lambda: None)
+    else:
+        assert L.pycall() is not None, "_mgn_pycall not built"
+    N, A = 8192, 8
+    g, orc = make_pair(trendou_sources(A, TRENDOU_P), N, seed=0x6D6164 + 5, **C3_KW)
+    acts = g.generate_actions(1 + 20, seed=0x6D6164)
+    a = acts.cpu().numpy()
+    k0 = 0
+    for K in (1, 20):
+        out = g.alloc_traj(K, fields=list(STD_FIELDS))
+        launch = g.rollout_launcher(out, K)
+        assert launch(acts[k0:k0 + K].data_ptr()) == 0
+        ref = orc.rollout(a[k0:k0 + K], threads=THREADS)
+        o = _host(out)
+        for f in ("obs_price", "obs_port", "tprice", "tunits", "tcost"):
+            assert_bits(o[f], ref[f], f"launcher {binding} K={K} {f}")
+        for f in ("risk", "done", "margin_call"):
+            assert np.array_equal(o[f], ref[f]), f"launcher {binding} K={K} {f}"
+        assert np.array_equal(o["timestamp"].astype(np.uint64), ref["timestamp"])
+        close(o["reward"], ref["reward"], f"launcher {binding} K={K} reward")
+        close(o["shaped"], ref["shaped"], f"launcher {binding} K={K} shaped")
+        k0 += K
+    state_check(g, orc, f"launcher {binding}")

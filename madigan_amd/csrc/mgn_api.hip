@@ -383,6 +383,11 @@ int choose_m(int n_envs, int apad) {
 void launch_step(const mgn_env* e, const mgn_traj& out, int in_kind, const double* units,
                  const int32_t* aidx, const int8_t* act, int K, hipEvent_t ev0, hipEvent_t ev1) {
   mgn::StepArgs a{kparams(e), out, in_kind, units, aidx, act, K, e->stream, ev0, ev1};
+#ifndef MGN_NO_GK  // diagnostic A/B builds: the generic generator role everywhere
+  a.gkind = e->kinds[0];
+  for (int i = 1; i < e->A; ++i)
+    if (e->kinds[i] != a.gkind) a.gkind = -1;
+#endif
   if (e->trio) {
     const int idx = e->apad <= 2 ? 1 : e->apad <= 4 ? 2 : e->apad <= 8 ? 3 : 4;
     kTrio[idx](a);

@@ -332,8 +332,10 @@ __device__ __noinline__ double sinedyn_tick(const double* q, double* ax, bool tr
 // 1457-1493; Composite concatenation :439-451) ; tick = timestamp before ++.
 // RP: the kernel may serve a replay tape (k_step); AUX: multi-component kinds
 // (views.aux).  The two-role kernel compiles neither (their calls would cost
-// the hot generator registers) and is not selected for such handles.
-template <int M, bool RP = true, bool AUX = true>
+// the hot generator registers) and is not selected for such handles.  GK >= 0:
+// every asset of the handle is of kind GK (the launcher checks), so the
+// per-lane kind dispatch folds away at compile time.
+template <int M, bool RP = true, bool AUX = true, int GK = -1>
 __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, uint64_t tick) {
   if (RP && p.replay) {
     // HDFSourceSingle::getData (DataSource.cpp:391-398) on the tape: the
@@ -361,7 +363,7 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
     if (!s.valid[m]) continue;
     const int a = s.asset[m];
     const double* q = p.src[a].p;
-    const int kind = s.kind[m];
+    const int kind = GK >= 0 ? GK : s.kind[m];
     // the slot-0 variates, drawn once for every kind that reads them: a
     // Composite source's lanes (Synth / OU / TrendOU in one wave) then run one
     // Philox + Box-Muller instead of one per kind branch (same bits: the draw
@@ -527,13 +529,13 @@ __device__ __forceinline__ void put_feats(const Lane<M>& s, const KParams& p, in
 
 // source reset (DataSource.h:466, :232; DataSource.cpp:1495-1502; the replay
 // source carries on, DataSource.cpp:200-206)
-template <int M, bool AUX = true>
+template <int M, bool AUX = true, int GK = -1>
 __device__ __forceinline__ void src_reset(Lane<M>& s, const KParams& p, int env, uint64_t tick) {
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     if (!s.valid[m]) continue;
     const double* q = p.src[s.asset[m]].p;
-    const int kind = s.kind[m];
+    const int kind = GK >= 0 ? GK : s.kind[m];
     if (kind == MGN_SRC_TRENDOU) {
       s.tfl[m] &= ~1;
       s.P[m] = q[5];

@@ -24,6 +24,9 @@ struct StepArgs {
   // itself (hipExtLaunchKernel: the kernel's own begin / end, no marker
   // packets around it); null otherwise
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // the source kind shared by every asset of the handle, else -1 (selects the
+  // kind-specialized generator role where one is instantiated)
+  int gkind = -1;
 };
 // hipLaunchKernelGGL, or the event-recording launch when the step's events are set
 template <typename Kern, typename... Args>

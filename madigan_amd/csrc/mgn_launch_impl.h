@@ -132,11 +132,23 @@ void launch_trio(const StepArgs& a) {
       else go(k_step_trio<S, false, false, 0, true>);
     }
   } else if (disc && om == O_STD) {  // the agent loop's output set
-    if (a.p.reqm_one) go(k_step_trio<S, true, true, O_STD>);
-    else go(k_step_trio<S, false, true, O_STD>);
+    if (a.gkind == MGN_SRC_TRENDOU) {
+      if (a.p.reqm_one) go(k_step_trio<S, true, true, O_STD, false, TRIO_W, false, MGN_SRC_TRENDOU>);
+      else go(k_step_trio<S, false, true, O_STD, false, TRIO_W, false, MGN_SRC_TRENDOU>);
+    } else if (a.p.reqm_one) {
+      go(k_step_trio<S, true, true, O_STD>);
+    } else {
+      go(k_step_trio<S, false, true, O_STD>);
+    }
   } else if (disc && om == O_ALL) {
-    if (a.p.reqm_one) go(k_step_trio<S, true, true, O_ALL>);
-    else go(k_step_trio<S, false, true, O_ALL>);
+    if (a.gkind == MGN_SRC_TRENDOU) {
+      if (a.p.reqm_one) go(k_step_trio<S, true, true, O_ALL, false, TRIO_W, false, MGN_SRC_TRENDOU>);
+      else go(k_step_trio<S, false, true, O_ALL, false, TRIO_W, false, MGN_SRC_TRENDOU>);
+    } else if (a.p.reqm_one) {
+      go(k_step_trio<S, true, true, O_ALL>);
+    } else {
+      go(k_step_trio<S, false, true, O_ALL>);
+    }
   } else if (disc) {
     if (a.p.reqm_one) go(k_step_trio<S, true, true>);
     else go(k_step_trio<S, false, true>);

@@ -121,7 +121,10 @@ struct TrioShared {
 // role: the env's NStepBuffer ring and one pop's summands in dynamic LDS
 // (launch_trio sizes it: envs per block x 2 nst_pad(n) doubles), the discounts staged
 // in LDS, so a pop is n LDS reads issued together, not n dependent loads.
-template <int S, bool RQ1, bool DISC, uint32_t OMC = 0, bool WIN = false, int TW = TRIO_W, bool NST = false>
+// GK >= 0: every asset's source is of kind GK (the generator role's per-lane
+// kind dispatch folds away: TrendOU at C3)
+template <int S, bool RQ1, bool DISC, uint32_t OMC = 0, bool WIN = false, int TW = TRIO_W, bool NST = false,
+          int GK = -1>
 __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out, int in_kind_rt,
                                                           const double* __restrict__ units_in,
                                                           const int32_t* __restrict__ aidx_in,
@@ -268,7 +271,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     // not stored (their value in HBM is the one loaded).  (Storing right after
     // the launch's last tick, beside the final finish iteration, measured
     // ~0.7 us slower per 20-step launch.)
-    const int kd = s.kind[0];
+    const int kd = GK >= 0 ? GK : s.kind[0];
     const bool w_sx = kd == MGN_SRC_SINE || kd == MGN_SRC_SAWTOOTH || kd == MGN_SRC_TRIANGLE || kd == MGN_SRC_TRENDYOU;
     const bool w_oum = kd == MGN_SRC_TRENDOU || kd == MGN_SRC_TRENDYOU || kd == MGN_SRC_OUPAIR;
     const bool w_trend = kd == MGN_SRC_TRENDOU || kd == MGN_SRC_SIMPLETREND || kd == MGN_SRC_TRENDYOU;
@@ -295,7 +298,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
         const bool prev_step = (sh.rFlags[prv][el] & TR_STEP) != 0;
         if (WIN && !rst && gpend > 0) {
           // a refill tick (not speculative: the reset is confirmed)
-          gen_tick<M, false, false>(s, p, env, ts);
+          gen_tick<M, false, false, GK>(s, p, env, ts);
           ts = ts + 1;
           gpend -= 1;
         } else if (rst) {
@@ -310,8 +313,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
             k -= 1;
           }
           // Env::reset -> dataSource->reset + getData (Env.h:181-187)
-          src_reset<M, false>(s, p, env, ts);
-          gen_tick<M, false, false>(s, p, env, ts);
+          src_reset<M, false, GK>(s, p, env, ts);
+          gen_tick<M, false, false, GK>(s, p, env, ts);
           ts = ts + 1;
           if (WIN) gpend = p.W - 1;
         } else if (k < K) {
@@ -323,7 +326,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
           svTfl = s.tfl[0];
           svTs = ts;
 #ifndef MGN_TRIO_ABL_G  // diagnostic timing build: no tick (prices frozen)
-          gen_tick<M, false, false>(s, p, env, ts);
+          gen_tick<M, false, false, GK>(s, p, env, ts);
 #endif
           ts = ts + 1;
           // State.price and timestamp of step k (overwritten if rolled back)

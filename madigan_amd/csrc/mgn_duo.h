@@ -741,7 +741,7 @@ __device__ __forceinline__ void duo_replay_tick(Lane<1>& s, const KParams& p, ui
 // aggregation (nstep > 1) on the generator side, each env's (n, D) ring and
 // an n-entry pop scratch in dynamic LDS (launch_duo sizes it: envs per block
 // x n x (D + 1) doubles).
-template <int S, bool RQ1, bool ABL, bool DISC, bool RP, bool NST>
+template <int S, bool RQ1, bool ABL, bool DISC, bool RP, bool NST, int GK = -1>
 __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out, int in_kind_rt,
                                                         const double* __restrict__ units_in,
                                                         const int32_t* __restrict__ aidx_in,
@@ -939,8 +939,8 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
             // the replay source carries on through a reset (DataSource.cpp:200-206)
             duo_replay_tick(s, p, ts, rp, rnx);
           } else {
-            if (sh.reset[el]) src_reset<M, false>(s, p, env, ts);  // Env::reset -> dataSource->reset (Env.h:183)
-            if (!(ABL && (p.ablate & 2))) gen_tick<M, false, false>(s, p, env, ts);
+            if (sh.reset[el]) src_reset<M, false, GK>(s, p, env, ts);  // Env::reset -> dataSource->reset (Env.h:183)
+            if (!(ABL && (p.ablate & 2))) gen_tick<M, false, false, GK>(s, p, env, ts);
             ts = ts + 1;
           }
           sh.price[l] = s.P[0];

@@ -40,8 +40,12 @@ void launch_duo(const StepArgs& a) {
                  a.in_kind, a.units, a.aidx, a.act, a.K);
   };
   const bool disc = a.in_kind == IN_DISCRETE;
+  const bool tou = a.gkind == MGN_SRC_TRENDOU;  // every asset TrendOU: the kind-specialized generator waves
   if (nst) {  // n-step buffers (generator sources; no ablation build)
-    if (disc) {
+    if (disc && tou) {
+      if (a.p.reqm_one) go(k_step_duo<S, true, false, true, false, true, MGN_SRC_TRENDOU>);
+      else go(k_step_duo<S, false, false, true, false, true, MGN_SRC_TRENDOU>);
+    } else if (disc) {
       if (a.p.reqm_one) go(k_step_duo<S, true, false, true, false, true>);
       else go(k_step_duo<S, false, false, true, false, true>);
     } else {
@@ -61,6 +65,9 @@ void launch_duo(const StepArgs& a) {
     if (a.p.reqm_one) go(k_step_duo<S, true, true, true, false, false>);
     else go(k_step_duo<S, false, true, true, false, false>);
 #endif
+  } else if (disc && tou) {
+    if (a.p.reqm_one) go(k_step_duo<S, true, false, true, false, false, MGN_SRC_TRENDOU>);
+    else go(k_step_duo<S, false, false, true, false, false, MGN_SRC_TRENDOU>);
   } else if (disc) {
     if (a.p.reqm_one) go(k_step_duo<S, true, false, true, false, false>);
     else go(k_step_duo<S, false, false, true, false, false>);
@@ -98,6 +105,9 @@ void launch_trio(const StepArgs& a) {
         if (a.p.reqm_one) goN(k_step_trio<S, true, false, 0, false, 64, true>);
         else goN(k_step_trio<S, false, false, 0, false, 64, true>);
       }
+    } else if (disc && a.gkind == MGN_SRC_TRENDOU) {
+      if (a.p.reqm_one) goN(k_step_trio<S, true, true, 0, false, TRIO_W, true, MGN_SRC_TRENDOU>);
+      else goN(k_step_trio<S, false, true, 0, false, TRIO_W, true, MGN_SRC_TRENDOU>);
     } else if (disc) {
       if (a.p.reqm_one) goN(k_step_trio<S, true, true, 0, false, TRIO_W, true>);
       else goN(k_step_trio<S, false, true, 0, false, TRIO_W, true>);
@@ -109,7 +119,10 @@ void launch_trio(const StepArgs& a) {
   }
   if (small) {  // runtime output mask, window or not
     if (a.p.W > 0) {
-      if (disc) {
+      if (disc && a.gkind == MGN_SRC_OU) {  // C2: OU windows
+        if (a.p.reqm_one) go(k_step_trio<S, true, true, 0, true, 64, false, MGN_SRC_OU>);
+        else go(k_step_trio<S, false, true, 0, true, 64, false, MGN_SRC_OU>);
+      } else if (disc) {
         if (a.p.reqm_one) go(k_step_trio<S, true, true, 0, true, 64>);
         else go(k_step_trio<S, false, true, 0, true, 64>);
       } else {

@@ -1058,17 +1058,17 @@ __device__ __forceinline__ double dsr_one(double r, double A, double B) {
   // ((B - A^2)^2)^(3/4) = |B - A^2|^(3/2), evaluated as a*sqrt(a): within 2 ulp of
   // libm pow (outputs are compared at rtol 1e-12; they never feed back into state)
   const double a = fabs(t);
-  return (B * dA - (A * dB) / 2) / (a * sqrt(a) + 1.1920928955078125e-07);
+  return rt_div(B * dA - (A * dB) / 2, a * rt_sqrt(a) + 1.1920928955078125e-07);
 }
 __device__ __forceinline__ double ddr_one(double r, double A, double B) {
   // r > 0: (r - A/2) / (sqrt(B) + eps); else (B(r - A/2) - A r^2/2) / (B^(3/2) + eps),
   // B^(3/2) as B*sqrt(B); one division with the branch's operands selected
-  const double sB = sqrt(B);
+  const double sB = rt_sqrt(B);
   const double h = r - A / 2;
   const bool pos = r > 0.;
   const double num = pos ? h : (B * h - (A * (r * r)) / 2);
   const double den = (pos ? sB : B * sB) + 1.1920928955078125e-07;
-  return num / den;
+  return rt_div(num, den);
 }
 // ddr_one with its reward-independent operands (A/2 and the two
 // denominators) evaluated ahead of the reward: the same operations on the
@@ -1077,26 +1077,26 @@ struct DdrPre {
   double hA, dpos, dneg;
 };
 __device__ __forceinline__ DdrPre ddr_pre(double A, double B) {
-  const double sB = sqrt(B);
+  const double sB = rt_sqrt(B);
   return DdrPre{A / 2, sB + 1.1920928955078125e-07, B * sB + 1.1920928955078125e-07};
 }
 __device__ __forceinline__ double ddr_one_pre(double r, double A, double B, const DdrPre& q) {
   const double h = r - q.hA;
   const bool pos = r > 0.;
   const double num = pos ? h : (B * h - (A * (r * r)) / 2);
-  return num / (pos ? q.dpos : q.dneg);
+  return rt_div(num, pos ? q.dpos : q.dneg);
 }
 __device__ __forceinline__ double clip1(double v) { return v < -1. ? -1. : (v > 1. ? 1. : v); }
 // dsr_one with its reward-independent denominator evaluated once per pop (the
 // same operations on the same operands)
 __device__ __forceinline__ double dsr_den(double A, double B) {
   const double a = fabs(B - A * A);
-  return a * sqrt(a) + 1.1920928955078125e-07;
+  return a * rt_sqrt(a) + 1.1920928955078125e-07;
 }
 __device__ __forceinline__ double dsr_one_den(double r, double A, double B, double den) {
   const double dA = r - A;
   const double dB = r * r - B;
-  return (B * dA - (A * dB) / 2) / den;
+  return rt_div(B * dA - (A * dB) / 2, den);
 }
 // the summand of one NStepBuffer entry at discount slot k (nstep_buffer.py:62-91,
 // :128-162; PPC / none: the stored value)

@@ -163,6 +163,39 @@ __device__ __noinline__ double det_sin(double x) {
 
 constexpr double TWO_M32 = 2.3283064365386962890625e-10;
 
+// Arithmetic of the reward shaping (DSR / DDR quotients and square roots, and
+// the quotient inside log_ratio, whose residual term absorbs its last bits):
+// outputs compared at a relative tolerance (rtol 1e-6, tests
+// 1e-12) whose error stays relative to the output itself, and which never
+// feed the ledger, the prices, done or State.  a / b as a times the
+// reciprocal of b refined by two Newton steps (<= 2 ulp; 6 VALU instead of
+// the IEEE sequence's 11), sqrt x from v_rsq_f64 with one Goldschmidt
+// refinement (<= 1 ulp; 8 VALU instead of 17).  Operands outside the normal
+// class (zero, denormal, inf, NaN, negative square-root arguments) take the
+// IEEE operation.  The reward ratio curEq / prevEq stays IEEE: a small log
+// reward would carry its last-bit error at a large relative size.  Every step
+// kernel uses these helpers, so the schedules stay bit-identical.
+#ifndef MGN_FAST_RT
+#define MGN_FAST_RT 1
+#endif
+constexpr int kNormalClass = (1 << 3) | (1 << 8);  // v_cmp_class: -normal | +normal
+__device__ __forceinline__ double rt_div(double a, double b) {
+  if (!MGN_FAST_RT || !__builtin_amdgcn_class(b, kNormalClass)) return a / b;
+  double r = __builtin_amdgcn_rcp(b);
+  r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
+  r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
+  return a * r;
+}
+__device__ __forceinline__ double rt_sqrt(double x) {
+  if (!MGN_FAST_RT || !__builtin_amdgcn_class(x, 1 << 8)) return sqrt(x);
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = __builtin_fma(-g, h, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  return __builtin_fma(__builtin_fma(-g, g, x), h, g);
+}
+
 // Variates of one (env, asset, tick) from its slot-0 block x0..x3:
 //   u1 = ((x1:x0 >> 11) + 1) 2^-53 in (0,1],  u2 = x2 2^-32 in [0,1)
 //   z  = sqrt(-2 log u1) cos(2 pi u2)            (Box-Muller)
@@ -217,7 +250,7 @@ __device__ __forceinline__ double log_ratio(double x) {
   if (fabs(d) <= 0.03125) {
     const double u = x + 1.0;
     const double e = x - (u - 1.0);  // x + 1 == u + e exactly
-    const double sh = d / u;
+    const double sh = rt_div(d, u);
     const double r = __fma_rn(-sh, u, d);  // d - sh * u exactly
     const double sl = (r - sh * e) * 0.5;  // 1/u ~ 1/2 to 2 %: s_lo needs few bits
     const double s2 = sh * sh;

@@ -81,6 +81,19 @@ constexpr int TRIO_W = 256;  // lanes per role
 #endif
 
 
+// the loop's exit test after iteration j's barrier: iterations 0..K always
+// run (the K steps, one iteration behind for the finish role), so the shared
+// `more` flag -- an LDS read on every role's path out of the barrier -- is
+// consulted only from iteration K on (MGN_TRIO_MORESKIP; rollbacks and refill
+// ticks raise it)
+#ifndef MGN_TRIO_MORESKIP
+#define MGN_TRIO_MORESKIP 1
+#endif
+__device__ __forceinline__ bool trio_exit(int j, int K, const int32_t& more) {
+  if (MGN_TRIO_MORESKIP && j < K) return false;
+  return !__builtin_amdgcn_readfirstlane(more);
+}
+
 // TR_REFILL (WIN): the iteration's tick was an auto-reset refill tick
 // (initialize_history's env.step(), preprocessor.py:191-194): F pushes its
 // window row, nothing else
@@ -268,9 +281,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
 #endif
     int gpend = 0;  // WIN: refill ticks still to come after the reset tick
     // the source state write-back at exit; fields a kind never writes are
-    // not stored (their value in HBM is the one loaded).  (Storing right after
-    // the launch's last tick, beside the final finish iteration, measured
-    // ~0.7 us slower per 20-step launch.)
+    // not stored (their value in HBM is the one loaded).  (Storing it in the
+    // first idle iteration, under the finish role's last iteration, measured
+    // 1-2.5 % slower per step: profiles/r03k_early_store_fast_rt_ab.txt.)
     const int kd = GK >= 0 ? GK : s.kind[0];
     const bool w_sx = kd == MGN_SRC_SINE || kd == MGN_SRC_SAWTOOTH || kd == MGN_SRC_TRIANGLE || kd == MGN_SRC_TRENDYOU;
     const bool w_oum = kd == MGN_SRC_TRENDOU || kd == MGN_SRC_TRENDYOU || kd == MGN_SRC_OUPAIR;
@@ -349,7 +362,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
       acc1 += T2 - T1;
       jn = j;
 #endif
-      if (!__builtin_amdgcn_readfirstlane(sh.more[j % 3])) break;
+      if (trio_exit(j, K, sh.more[j % 3])) break;
     }
 #ifdef MGN_STAMPS
     if (threadIdx.x == 0) {
@@ -523,7 +536,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
       acc0 += T1 - T0;
       acc1 += T2 - T1;
 #endif
-      if (!__builtin_amdgcn_readfirstlane(sh.more[j % 3])) break;
+      if (trio_exit(j, K, sh.more[j % 3])) break;
     }
 #ifdef MGN_STAMPS
     if (l == 0) {
@@ -878,7 +891,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     acc0 += T1 - T0;
     acc1 += T2 - T1;
 #endif
-    if (!__builtin_amdgcn_readfirstlane(sh.more[j % 3])) break;
+    if (trio_exit(j, K, sh.more[j % 3])) break;
   }
 #ifdef MGN_STAMPS
   if (l == 0) {

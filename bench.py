@@ -659,6 +659,32 @@ def windowed(args, world, rank, dev):
     L.check(lib.mgn_set_timing(h, 0), h)
     step_us = tm[0] / max(tm[1], 1) * 1e3
     gather_us = tm[2] / max(tm[3], 1) * 1e3
+    # the zero-copy form (element-wise normalisers, preprocessor.py:183-189):
+    # the same launches with the windows read in place from the launch
+    # history (mgn_window_hist_view) instead of materialised -- measured after
+    # the timed region, reported beside the line, never as its value
+    view = None
+    if env.cfg.norm_type in (L.NORM_NONE, L.NORM_LOG):
+        hv = L.HistView()
+
+        def run_view(l0, l1):
+            rc = 0
+            for l in range(l0, l1):
+                rc |= lib.mgn_rollout_hist(h, C.c_void_p(base + l * Kf * per), Kf, tstruct)
+                rc |= lib.mgn_window_hist_view(h, C.byref(hv))
+            L.check(rc, h)
+        n_view = n_time  # the timed launches' actions again
+        run_view(n_warm, n_warm + 1)
+        torch.cuda.synchronize()
+        tv = time.perf_counter()
+        run_view(n_warm, n_warm + n_view)
+        torch.cuda.synchronize()
+        view_s = time.perf_counter() - tv
+        view = {"value": N * n_view * Kf / view_s, "unit": "env-steps/s",
+                "ms_per_step": view_s * 1e3 / (n_view * Kf), "launches": n_view,
+                "note": "mgn_rollout_hist + mgn_window_hist_view: each step's window is the history "
+                        "row range [hend - hlen, hend), read in place by the consumer (no k_hist_gather); "
+                        "measured after the timed region on this rank"}
     gb = gather_bytes(env, Kf)
     achieved = gb / (gather_us * 1e-6) / 1e9
     value = world * N * args.steps / elapsed
@@ -687,6 +713,8 @@ def windowed(args, world, rank, dev):
             "episodes_completed": int(gathered[:, 3].sum().item()),
             "allgather_path": allgather_path,
         }
+        if view is not None:
+            res["view_mode"] = view
         if wl == "C5":
             tape_bytes = sum(t.numel() * t.element_size() for t in env._tape.values())
             res["replay_staging"] = {"tape_rows": int(env._tape["ts"].shape[0]),

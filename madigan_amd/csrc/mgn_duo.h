@@ -741,6 +741,13 @@ __device__ __forceinline__ void duo_replay_tick(Lane<1>& s, const KParams& p, ui
 // aggregation (nstep > 1) on the generator side, each env's (n, D) ring and
 // an n-entry pop scratch in dynamic LDS (launch_duo sizes it: envs per block
 // x n x (D + 1) doubles).
+// the exit test after barrier B of iteration j: the ledger runs at most one
+// step per iteration, so every iteration j < K - 1 is followed by another and
+// the shared `more` flag (an LDS round trip on both roles' paths) is read only
+// from iteration K - 1 on
+#ifndef MGN_DUO_MORESKIP
+#define MGN_DUO_MORESKIP 1
+#endif
 template <int S, bool RQ1, bool ABL, bool DISC, bool RP, bool NST, int GK = -1>
 __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out, int in_kind_rt,
                                                         const double* __restrict__ units_in,
@@ -971,7 +978,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       acc[0] += T1 - T0; acc[1] += T2 - T1; acc[2] += T3 - T2; acc[3] += T4 - T3;
 #endif
       // a wave-uniform (scalar) exit test: the fin pass skips a barrier
-      if (!__builtin_amdgcn_readfirstlane(sh.more[j % 3])) {
+      if ((!MGN_DUO_MORESKIP || j + 1 >= K) && !__builtin_amdgcn_readfirstlane(sh.more[j % 3])) {
         fin = true;
         MGN_WALL(4);
       }
@@ -1225,7 +1232,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
     if (j == 0) MGN_WALL(6);
     if (j == 2) MGN_WALL(7);
 #endif
-    if (!sh.more[j % 3]) break;
+    if ((!MGN_DUO_MORESKIP || j + 1 >= K) && !__builtin_amdgcn_readfirstlane(sh.more[j % 3])) break;
   }
   MGN_WALL(3);
   MGN_WALLV(14, rmax);

@@ -25,7 +25,10 @@ def main():
     out_dir = os.path.join(ROOT, "tools", "_var", name)
     os.makedirs(out_dir, exist_ok=True)
     cc = B.hipcc()
-    redo = {"mgn_api.hip", "mgn_launch_a8.hip"}
+    # the translation units rebuilt with the extra flags (MGN_VARIANT_UNITS,
+    # comma-separated APADs: default the A = 8 kernels)
+    units = os.environ.get("MGN_VARIANT_UNITS", "8").split(",")
+    redo = {"mgn_api.hip"} | {f"mgn_launch_a{u}.hip" for u in units}
 
     def one(src):
         base = os.path.basename(src)

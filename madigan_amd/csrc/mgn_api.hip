@@ -355,7 +355,10 @@ void choose_sched(mgn_env* e) {
     e->trio = trio_eligible(e);
     e->duo = !e->trio && duo_eligible(e);
   } else {
-    e->trio = trio_eligible(e) && e->m == 1 && e->apad <= 8;
+    // 16 assets: the three-role kernel where measured faster (one-step
+    // rewards, no window: 5.3 vs 6.3 us/step at 8192 x 16 TrendOU)
+    e->trio = trio_eligible(e) && e->m == 1 &&
+              (e->apad <= 8 || (e->apad <= 16 && e->W == 0 && e->cfg.nstep == 1));
     e->duo = !e->trio && duo_eligible(e) && e->m == 1;
   }
 }

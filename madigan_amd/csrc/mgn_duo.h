@@ -536,15 +536,22 @@ __device__ __forceinline__ Q4 q4add(const Q4& x, const Q4& y) {
 }
 template <int N>
 constexpr int ilog2() { return N <= 1 ? 0 : 1 + ilog2<N / 2>(); }
-template <int S, int LO, int N, bool RP>
+// FENCE (the three-role kernel at S = 16): a scheduling fence between the
+// halves of every subtree of >= 8 leaves keeps the scheduler from hoisting the
+// right half's leaf loads above the left half's sums -- all 64 leaf doubles
+// live at once spilled its ledger waves (168 VGPRs + 37 spilled -> 134, none;
+// 16 TrendOU assets 7.7 -> 5.3 us/step).  The two-role kernel, at two waves
+// per SIMD either way, runs slower fenced (6.3 -> 6.8) and is not.
+template <int S, int LO, int N, bool RP, bool FENCE = false>
 __device__ __forceinline__ Q4 tree4(const EnvRecs<S>& er, uint32_t post, Q4 (&sib)[6]) {
   if constexpr (N == 1) {
     const d2* rv = reinterpret_cast<const d2*>(&er.r[LO]) + (((post >> LO) & 1u) ? 2 : 0);
     const d2 a = rv[0], b = rv[1];
     return Q4{a.x, a.y, b.x, b.y};
   } else {
-    const Q4 l = tree4<S, LO, N / 2, false>(er, post, sib);
-    const Q4 r = tree4<S, LO + N / 2, N / 2, RP>(er, post, sib);
+    const Q4 l = tree4<S, LO, N / 2, false, FENCE>(er, post, sib);
+    if constexpr (FENCE && N >= 8) __builtin_amdgcn_sched_barrier(0);
+    const Q4 r = tree4<S, LO + N / 2, N / 2, RP, FENCE>(er, post, sib);
     if constexpr (RP) sib[ilog2<N>() - 1] = l;
     return q4add(l, r);
   }
@@ -582,6 +589,11 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
     double c = cash0, c_own = cash0;
 #pragma unroll
     for (int i = 0; i < S; ++i) {
+      // the three-role kernel at S = 16: records read four at a time (a
+      // scheduling fence per group, as tree4's FENCE)
+      if constexpr (LOWREG && S >= 16) {
+        if (i > 0 && i % 4 == 0) __builtin_amdgcn_sched_barrier(0);
+      }
       if (i == ls) c_own = c;
       const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
       const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
@@ -593,7 +605,7 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
     // orders after the order, the others before
     double r0, r1, r2, r3;
     if constexpr (STREAM) {
-      const Q4 rt = tree4<S, 0, S, true>(er, go_bits & ((1u << ls) - 1u), sib);
+      const Q4 rt = tree4<S, 0, S, true, LOWREG && S >= 16>(er, go_bits & ((1u << ls) - 1u), sib);
       r0 = rt.a;
       r1 = rt.b;
       r2 = rt.c;

@@ -30,8 +30,8 @@
 // oracle).
 // Stores: L stores the BrokerResponse arrays of its step, G the tick's
 // State.price and timestamp, F everything that needs equity.
-// Scope: M = 1, APAD = S in {2, 4, 8, 16} (16: explicit schedule only, slower
-// than k_step_duo there), generator sources; n = 1 with or without a window
+// Scope: M = 1, APAD = S in {2, 4, 8, 16} (16: the ledger's broker trees read
+// behind scheduling fences, tree4's FENCE), generator sources; n = 1 with or without a window
 // (WIN: the finish role pushes the ring / launch-history row of every step it
 // confirms, and the refill rows after an auto-reset), or n-step (NST, no
 // window); k_step_duo / k_step run the rest.

@@ -300,3 +300,23 @@ def test_rollout_launcher_matches_rollout(gpu, binding, monkeypatch):
         close(o["shaped"], ref["shaped"], f"launcher {binding} K={K} shaped")
         k0 += K
     state_check(g, orc, f"launcher {binding}")
+
+
+def test_sixteen_assets_auto_schedule_vs_oracle(gpu):
+    """16 TrendOU assets at the automatic schedule (the three-role kernel since
+    round 3: its ledger's broker trees behind scheduling fences), 20- and
+    64-step launches against the oracle: every output and the final state."""
+    from madigan_amd import _lib as L
+    N, A = 2048, 16
+    g, orc = make_pair(trendou_sources(A, TRENDOU_P), N, seed=0x6D6164 + 7, **C3_KW)
+    assert g.lib.mgn_get_schedule(g.h) == L.SCHED_TRIO
+    acts = g.generate_actions(20 + 64, seed=0x6D6164)
+    a = acts.cpu().numpy()
+    k0 = 0
+    for K in (20, 64):
+        out = _host(g.rollout(acts[k0:k0 + K]))
+        ref = orc.rollout(a[k0:k0 + K], threads=THREADS)
+        out_check(out, ref, f"A16 K={K}")
+        k0 += K
+        state_check(g, orc, f"A16 after K={K}")
+    gen_state_check(g, orc, "A16")

@@ -331,7 +331,8 @@ bool duo_eligible(const mgn_env* e) {
   }
   return true;
 }
-// the three-role kernel: 2..8 assets, generator sources; one-step rewards
+// the three-role kernel: 2..16 assets, generator sources (replay tapes at 16
+// assets on the 256-lane layout); one-step rewards
 // (windows included: the confirmed steps' rows are pushed by its finish role)
 // or n-step aggregation of a scalar reward without a window (the finish
 // role's rings in dynamic LDS)
@@ -339,7 +340,9 @@ bool trio_eligible(const mgn_env* e) {
   // (its output indices are k x a 32-bit stride: N (A + 1), N F and N n fit 32 bits)
   const uint64_t row = (uint64_t)(e->A + 1 > e->F ? e->A + 1 : e->F);
   const bool nst_ok = e->cfg.nstep == 1 || (e->D == 1 && e->W == 0 && e->cfg.shaper < MGN_SHAPER_SHARPE);
-  return e->apad >= 2 && e->apad <= 16 && !e->cfg.aux && !e->replay && nst_ok &&
+  // replay tapes: 16 assets at the 256-lane layout (N * 16 >= 256 * 256), n = 1
+  const bool rp_ok = !e->replay || (e->apad == 16 && e->cfg.nstep == 1 && (uint64_t)e->N * 16 >= 65536);
+  return e->apad >= 2 && e->apad <= 16 && !e->cfg.aux && rp_ok && nst_ok &&
          (uint64_t)e->N * row < (1ull << 32) && (uint64_t)e->N * (uint64_t)e->cfg.nstep < (1ull << 32);
 }
 // automatic: where the single-role kernel would run one lane per asset (small
@@ -355,10 +358,11 @@ void choose_sched(mgn_env* e) {
     e->trio = trio_eligible(e);
     e->duo = !e->trio && duo_eligible(e);
   } else {
-    // 16 assets: the three-role kernel where measured faster (one-step
-    // rewards, no window: 5.3 vs 6.3 us/step at 8192 x 16 TrendOU)
+    // 16 assets: the three-role kernel where measured faster -- generator
+    // sources with one-step rewards and no window (5.2 vs 6.3 us/step at
+    // 8192 x 16 TrendOU) and replay tapes (C5: 405 vs 485 us per 64-step launch)
     e->trio = trio_eligible(e) && e->m == 1 &&
-              (e->apad <= 8 || (e->apad <= 16 && e->W == 0 && e->cfg.nstep == 1));
+              (e->apad <= 8 || (e->apad <= 16 && ((e->W == 0 && e->cfg.nstep == 1) || e->replay)));
     e->duo = !e->trio && duo_eligible(e) && e->m == 1;
   }
 }

@@ -90,6 +90,26 @@ void launch_trio(const StepArgs& a) {
   };
   const bool disc = a.in_kind == IN_DISCRETE;
   const uint32_t om = traj_mask(a.out);
+  if (a.p.replay) {  // RP: replay tapes at 16 assets, the 256-lane layout (trio_eligible)
+    if constexpr (S == 16) {
+      if (a.p.W > 0) {
+        if (disc) {
+          if (a.p.reqm_one) go(k_step_trio<S, true, true, 0, true, TRIO_W, false, -1, true>);
+          else go(k_step_trio<S, false, true, 0, true, TRIO_W, false, -1, true>);
+        } else {
+          if (a.p.reqm_one) go(k_step_trio<S, true, false, 0, true, TRIO_W, false, -1, true>);
+          else go(k_step_trio<S, false, false, 0, true, TRIO_W, false, -1, true>);
+        }
+      } else if (disc) {
+        if (a.p.reqm_one) go(k_step_trio<S, true, true, 0, false, TRIO_W, false, -1, true>);
+        else go(k_step_trio<S, false, true, 0, false, TRIO_W, false, -1, true>);
+      } else {
+        if (a.p.reqm_one) go(k_step_trio<S, true, false, 0, false, TRIO_W, false, -1, true>);
+        else go(k_step_trio<S, false, false, 0, false, TRIO_W, false, -1, true>);
+      }
+    }
+    return;
+  }
   if (a.p.nstep > 1) {  // NST: the finish role's NStepBuffer rings in dynamic LDS (no window, D = 1)
     const size_t lds = (size_t)epb * 2 * nst_pad(a.p.nstep) * sizeof(double);
     auto goN = [&](auto kern) {

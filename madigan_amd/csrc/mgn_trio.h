@@ -120,6 +120,11 @@ struct TrioShared {
   int32_t reset[2][EPB];
   uint64_t ts[2][EPB];  // timestamp after the tick (G -> F when F stores it)
   int32_t more[3];
+  // RP (replay tape): the tick's tape row and dataEnd flag per env, the
+  // lane's feature column value (F <= S) -- G -> F for State.price / windows
+  int64_t row[2][EPB];
+  uint32_t dend[2][EPB];
+  double feat[2][TRIO_W];
 };
 
 // OMC: the output set when known at compile time (O_ALL, O_STD), else 0.
@@ -135,9 +140,16 @@ struct TrioShared {
 // (launch_trio sizes it: envs per block x 2 nst_pad(n) doubles), the discounts staged
 // in LDS, so a pop is n LDS reads issued together, not n dependent loads.
 // GK >= 0: every asset's source is of kind GK (the generator role's per-lane
-// kind dispatch folds away: TrendOU at C3)
+// kind dispatch folds away: TrendOU at C3).
+// RP: every asset from the replay tape (HDFSourceSingle, DataSource.cpp:
+// 391-398): G reads the tape one row ahead instead of ticking (duo_replay_tick)
+// and publishes the row, its dataEnd flag and the lane's feature value; F
+// writes State.price and the window rows from the tape's feature row.  The
+// replay source carries on through a reset (DataSource.cpp:200-206), so the
+// reset's getData reads the row the voided speculative tick read: a rollback
+// keeps the tick's state as the reset tick's.
 template <int S, bool RQ1, bool DISC, uint32_t OMC = 0, bool WIN = false, int TW = TRIO_W, bool NST = false,
-          int GK = -1>
+          int GK = -1, bool RP = false>
 __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out, int in_kind_rt,
                                                           const double* __restrict__ units_in,
                                                           const int32_t* __restrict__ aidx_in,
@@ -169,7 +181,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
   s.rcur = 0;
   s.row = 0;
   s.pf_ok = false;
-  s.fcol = -1;
+  s.fcol = (RP && p.F <= S) ? ls : -1;  // RP: one feature column per lane
   const size_t li = (size_t)envc * A + (s.valid[0] ? ls : 0);
 #ifdef MGN_TRIO_ABL_PRO
   s.P[0] = 5.0;
@@ -201,6 +213,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
       s.tfl[0] = p.tfl[li];
     }
     ts = p.ts[envc];
+    if (RP) s.rcur = p.rcur[envc];
   } else if (role == 1) {
     if (s.valid[0]) {
       s.L[0] = p.L[li];
@@ -280,6 +293,17 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     int jn = 0;
 #endif
     int gpend = 0;  // WIN: refill ticks still to come after the reset tick
+    RpCur rp{0., 0, 0u};  // RP: the current State's tape row, feature, dataEnd
+    RpNext rnx{0., 0., 0, 0u};
+    // one tick: the tape row (RP; its timestamp) or the generator and ++ts
+    auto tick = [&]() {
+      if constexpr (RP) {
+        duo_replay_tick(s, p, ts, rp, rnx);
+      } else {
+        gen_tick<M, false, false, GK>(s, p, env, ts);
+        ts = ts + 1;
+      }
+    };
     // the source state write-back at exit; fields a kind never writes are
     // not stored (their value in HBM is the one loaded).  (Storing it in the
     // first idle iteration, under the finish role's last iteration, measured
@@ -311,9 +335,15 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
         const bool prev_step = (sh.rFlags[prv][el] & TR_STEP) != 0;
         if (WIN && !rst && gpend > 0) {
           // a refill tick (not speculative: the reset is confirmed)
-          gen_tick<M, false, false, GK>(s, p, env, ts);
-          ts = ts + 1;
+          tick();
           gpend -= 1;
+        } else if (RP && rst) {
+          // the replay source carries on: the reset's getData reads the row the
+          // voided speculative tick read, whose state stands; after a step that
+          // was not speculated (none ran in the previous iteration) it reads the next
+          if (prev_step) k -= 1;
+          else tick();
+          if (WIN) gpend = p.W - 1;
         } else if (rst) {
           if (prev_step) {  // roll the speculative tick back
             s.P[0] = svP;
@@ -331,17 +361,20 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
           ts = ts + 1;
           if (WIN) gpend = p.W - 1;
         } else if (k < K) {
-          svP = s.P[0];
-          svSx = s.sx[0];
-          svOum = s.oum[0];
-          svDy = s.dy[0];
-          svTlen = s.tlen[0];
-          svTfl = s.tfl[0];
-          svTs = ts;
+          if (!RP) {
+            svP = s.P[0];
+            svSx = s.sx[0];
+            svOum = s.oum[0];
+            svDy = s.dy[0];
+            svTlen = s.tlen[0];
+            svTfl = s.tfl[0];
+            svTs = ts;
+          }
 #ifndef MGN_TRIO_ABL_G  // diagnostic timing build: no tick (prices frozen)
-          gen_tick<M, false, false, GK>(s, p, env, ts);
-#endif
+          tick();
+#else
           ts = ts + 1;
+#endif
           // State.price and timestamp of step k (overwritten if rolled back)
           if (MGN_TRIO_GST) {
             const size_t oN = (size_t)k * p.N;
@@ -353,6 +386,13 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
       }
       sh.price[cur][l] = s.P[0];
       if (!MGN_TRIO_GST && ls == 0) sh.ts[cur][el] = ts;
+      if constexpr (RP) {
+        if (ls == 0) {
+          sh.row[cur][el] = rp.row;
+          sh.dend[cur][el] = rp.dend;
+        }
+        sh.feat[cur][l] = rp.curF;
+      }
       MGN_T(T1);
       __syncthreads();
       MGN_T(T2);
@@ -375,7 +415,10 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
 #ifdef MGN_TRIO_ABL_EPI  // diagnostic timing build: no state write-back
     return;
 #endif
-    if (live) g_store();
+    if (live) {
+      g_store();
+      if (RP && ls == 0) p.rcur[env] = s.rcur;
+    }
     MGN_IT_DRAIN();
     MGN_IT(44, 0);
     return;
@@ -598,20 +641,39 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
   // log-normalised (as the ring stores them) prices, ledgerNormedFull and the
   // timestamp into ring slot head + 1 and history row hcnt (ring_push's
   // values; duo_store's order)
-  const auto push_row = [&](double P, double portA, double port0, uint64_t tsv, int kmark) {
+  // State.price of the State G published at parity q into dst[0, F): the
+  // lane's asset price, or (RP) the tape row's features (duo_feats' split:
+  // one column per lane when F <= S, else read back per column); lg:
+  // StackerDiscrete's log
+  const auto put_price = [&](MGN_G double* dst, double P, bool lg, int q) {
+    if constexpr (RP) {
+      if (s.fcol >= 0) {
+        if (s.fcol < p.F) {
+          const double v = sh.feat[q][l];
+          ost(dst + s.fcol, lg ? log_norm(v) : v);
+        }
+      } else {
+        const int64_t row = sh.row[q][el];
+        for (int f = ls; f < p.F; f += S) {
+          const double v = p.rp_feat[(size_t)row * p.F + f];
+          ost(dst + f, lg ? log_norm(v) : v);
+        }
+      }
+    } else if (s.valid[0]) {
+      ost(dst + s.asset[0], lg ? log_norm(P) : P);
+    }
+  };
+  const auto push_row = [&](double P, double portA, double port0, uint64_t tsv, int kmark, int q) {
     rhead = (rhead + 1) % p.W;
     if (rlen < p.W) rlen += 1;
     const int R = p.F + A + 1;
     MGN_G double* row = gs.ring + ((size_t)env * p.W + rhead) * R;
     MGN_G double* hrow = p.hist ? gs.hist + ((size_t)env * p.hrows + hcnt) * R : nullptr;
+    put_price(row, P, p.ring_log != 0, q);
+    if (hrow) put_price(hrow, P, p.ring_log != 0, q);
     if (s.valid[0]) {
-      const double fv = p.ring_log ? log_norm(P) : P;
-      ost(row + s.asset[0], fv);
       ost(row + (p.F + 1 + s.asset[0]), portA);
-      if (hrow) {
-        ost(hrow + s.asset[0], fv);
-        ost(hrow + (p.F + 1 + s.asset[0]), portA);
-      }
+      if (hrow) ost(hrow + (p.F + 1 + s.asset[0]), portA);
     }
     if (ls == 0) {
       ost(row + p.F, port0);
@@ -823,13 +885,14 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
           if (om & O_TC) ost(ov.tcost + i, sh.rTc[prv][l]);
           if (om & O_RISK) ost(ov.risk + i, (uint8_t)sh.rRk[prv][l]);
         }
-        if (!MGN_TRIO_GST && (om & O_OPR)) ost(ov.obs_price + kidx(k, sNF, bP), P);
+        if (!RP && !MGN_TRIO_GST && (om & O_OPR)) ost(ov.obs_price + kidx(k, sNF, bP), P);
         if (om & O_OPT) ost(ov.obs_port + (kidx(k, sNA1, bO) + 1 + f.asset[0]), portA);
         if (D != 1) {
           if (om & O_AREW) ost(ov.agent_reward + i, ar);
           if (om & O_SHP) ost(ov.shaped + i, shaped_v);
         }
       }
+      if (RP && live && (om & O_OPR)) put_price(ov.obs_price + kidx(k, sNF, (size_t)env * p.F), P, false, prv);
 #endif
 #ifndef MGN_ABL_NOSTORE_ENV
       if (ls == 0) {
@@ -837,7 +900,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
         if (om & O_OPT) ost(ov.obs_port + kidx(k, sNA1, bO), port0);
         if (om & O_DONE) ost(ov.done + ie, (uint8_t)(done ? 1 : 0));
         if (om & O_MC) ost(ov.margin_call + ie, (uint8_t)((flags & TR_MCALL) ? 1 : 0));
-        if (om & O_DEND) ost(ov.data_end + ie, (uint8_t)0);
+        if (om & O_DEND) ost(ov.data_end + ie, (uint8_t)(RP ? sh.dend[prv][el] : 0u));
         if (om & O_REW) ost(ov.reward + ie, reward);
         if (om & O_NSH) ost(ov.n_shaped + ie, (uint8_t)pops);
         if (!MGN_TRIO_GST && (om & O_TS)) ost(ov.timestamp + ie, (uint64_t)sh.ts[prv][el]);
@@ -848,7 +911,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
       }
 #endif
       if (WIN) {
-        push_row(P, portA, port0, (uint64_t)sh.ts[prv][el], k);
+        push_row(P, portA, port0, (uint64_t)sh.ts[prv][el], k, prv);
         if (done && p.auto_reset) {  // a reset empties the window before its refill ticks
           rlen = 0;
           rhead = p.W - 1;
@@ -880,7 +943,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
       double tlp[M];
       tlp[0] = Lf * Pf;
       const double eq = (cashf + canon<M, S>(tlp)) - bf;
-      push_row(Pf, (Lf * Pf) / eq, (cashf - bf) / eq, (uint64_t)sh.ts[prv][el], klast);
+      push_row(Pf, (Lf * Pf) / eq, (cashf - bf) / eq, (uint64_t)sh.ts[prv][el], klast, prv);
     }
     if (ls == 0) sh.reset[cur][el] = rst_out;
     if (rst_out) sh.more[j % 3] = 1;  // the reset tick runs next iteration

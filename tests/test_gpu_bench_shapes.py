@@ -76,7 +76,8 @@ def test_c3_full_grid_forced_resets(gpu):
         close(st[:, j], orc.scalar(name), name)
 
 
-def test_c5_bench_shape_windows(gpu, tmp_path):
+@pytest.mark.parametrize("sched", ["auto", "duo"])
+def test_c5_bench_shape_windows(gpu, tmp_path, sched):
     import torch
     if ROOT not in sys.path:
         sys.path.insert(0, ROOT)
@@ -95,6 +96,10 @@ def test_c5_bench_shape_windows(gpu, tmp_path):
               auto_reset=True, init_cash=1_000_000.0, window=W, adaptation_rate=0.001,
               reward_shaper="DDR", seed=0x6D6164 + 5)
     g = BatchedEnv(spec_from_config(cfg), N, device=gpu, replay_stride=997, **kw)
+    from madigan_amd import _lib as L
+    if sched == "duo":  # the two-role kernel (explicit); auto: the three-role kernel
+        L.check(g.lib.mgn_set_schedule(g.h, L.SCHED_DUO), g.h)
+    assert g.lib.mgn_get_schedule(g.h) == (L.SCHED_DUO if sched == "duo" else L.SCHED_TRIO)
     first, second, _, _ = O.hdf_bounds(ts, 0, 0)
     orc = O.OracleBatch(dict(kw, n_envs=N, n_feats=A, auto_reset=1), [(O.SRC_REPLAY, [])] * A)
     assert orc.set_replay(price, price, ts, first, second, 10_000, 997) == g._tape["ts"].shape[0]

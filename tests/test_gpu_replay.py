@@ -197,3 +197,50 @@ def test_replay_window_history(gpu, tmp_path, A, F, window, norm):
             assert_bits(wo[k].cpu().numpy(), rpo, f"window portfolio {half}/{k}")
             assert np.array_equal(wt[k].cpu().numpy().astype(np.uint64), rts)
     assert dones > 0 or A == 1
+
+
+@pytest.mark.parametrize("F,window", [(16, 0), (20, 0), (16, 8)])
+def test_replay_trio_equals_duo_sixteen_assets(gpu, F, window):
+    """The three-role kernel on a replay tape (16 assets, the 256-lane layout:
+    4096 envs) against the two-role kernel from the same construction: every
+    output, the window and the final state bit for bit, through auto-resets
+    (a leveraged, costly broker), 20- and 1-step launches; F > 16 features
+    take the read-back-per-column path."""
+    import torch
+    from madigan_amd import BatchedEnv, replay_spec
+    from madigan_amd import _lib as L
+    rng = np.random.default_rng(21 + F)
+    P, A, N = 503, 16, 4096
+    price = 5.0 * np.exp(np.cumsum(rng.normal(0, 0.03, (P, A)), axis=0))
+    feats = rng.normal(0, 1, (P, F))
+    tape = dict(price=torch.tensor(price, device=gpu), feats=torch.tensor(feats, device=gpu),
+                ts=torch.arange(P, dtype=torch.int64, device=gpu) * 60 + 7,
+                data_end=torch.zeros(P, dtype=torch.uint8, device=gpu))
+    tape["data_end"][-1] = 1
+    kw = dict(required_margin=0.1, maintenance_margin=0.5, transaction_cost_rel=0.02, unit_size=0.9,
+              auto_reset=True, replay_stride=29, replay_tape=tape, seed=3, reward_shaper="DDR",
+              window=window, init_cash=1e5)
+    res = []
+    for sched in (L.SCHED_DUO, L.SCHED_TRIO):
+        g = BatchedEnv(replay_spec(A, F), N, device=gpu, **kw)
+        L.check(g.lib.mgn_set_schedule(g.h, sched), g.h)
+        assert g.lib.mgn_get_schedule(g.h) == sched
+        acts = g.generate_actions(41, seed=8)
+        outs = [g.rollout(acts[:20]), g.rollout(acts[20:21]), g.rollout(acts[21:])]
+        host = [{k: v.cpu().numpy() for k, v in o.items()} for o in outs]
+        win = [t.cpu().numpy() for t in g.window()] if window else []
+        state = [t.cpu().numpy() for t in (g.ledger, g.cash, g.prices, g.timestamp, g.replay_cursor,
+                                           g.episode_stats, g.shaper_a, g.shaper_b)]
+        res.append((host, win, state))
+    (h0, w0, s0), (h1, w1, s1) = res
+    assert sum(int(h["done"].sum()) for h in h0) > 0, "no episode ended"
+    def same(x, y, what):
+        if x.dtype == np.float64:
+            assert_bits(y, x, what)
+        else:
+            np.testing.assert_array_equal(y, x, err_msg=what)
+    for a, b in zip(h0, h1):
+        for k in a:
+            same(a[k], b[k], f"trio vs duo {k}")
+    for i, (a, b) in enumerate(zip(w0 + s0, w1 + s1)):
+        same(a, b, f"trio vs duo window/state {i}")

@@ -10,7 +10,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 export TMPDIR=/tmp
-O=gpurun_out/r03final2
+O=gpurun_out/r03final4
 mkdir -p $O
 PT="python -u -m pytest -v --timeout 180 --timeout-method thread -p no:cacheprovider"
 timeout -k 10 900 $PT -m gpu tests > $O/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -30 $O/pytest_gpu.log; exit 1; }

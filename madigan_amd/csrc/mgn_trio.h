@@ -115,6 +115,7 @@ struct TrioShared {
   // per env: cash and the three price-independent sums after the orders,
   // equity before the step, the step index and TR_* flags
   double rCash[2][EPB], rMl[2][EPB], rSh[2][EPB], rB[2][EPB], rPrevEq[2][EPB];
+  double rLpA[2][EPB];  // the sum L*P after the orders at the step's pre-tick prices (F: marginCall)
   int32_t rK[2][EPB], rFlags[2][EPB];
   // F -> G, L: the step F evaluated ended its episode and the env resets
   int32_t reset[2][EPB];
@@ -434,6 +435,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     p.mainM = in_vgpr(p.mainM);
     p.unit_size = in_vgpr(p.unit_size);
     const uint32_t act_step = (uint32_t)p.N * (uint32_t)A;
+    const bool need_ar = (p.reward_mode != MGN_REWARD_ENV_LOG) || (om & O_AREW);  // as the finish role's
     // sums of the ledger (canonical trees): ml, sh, b change only with the
     // orders, lp with the prices; `fresh` = recompute all four (start, reset)
     Sums sa = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
@@ -507,6 +509,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
         rk[0] = MGN_GREEN;
         uc[0] = 0.;
         const size_t oN = (size_t)k * p.N, oNA = (size_t)k * p.N * A;
+        const double prevVal = s.L[0] * s.P[0];
         if (in_kind == IN_DISCRETE) {  // dqn.py:160-179
           const double bp = (cash + s0.sh) + (s0.lp - s0.ml);
           const double avM = RQ1 ? bp : bp / p.reqM;
@@ -523,16 +526,14 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
           const double u = gunits[oN + env];
           uc[0] = (s.valid[0] && s.asset[0] == ai) ? u : 0.;
         }
-        const double prevVal = s.L[0] * s.P[0];
         Sums after = s0;
-        int any_mc = 0, mcall = 0;
+        int any_mc = 0;
 #ifdef MGN_TRIO_ABL_L  // diagnostic timing build: no Broker orders
         if (false) {
 #else
         if (in_kind != IN_NONE) {
 #endif
           broker_spec<S, RQ1, true>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, after, any_mc);
-          mcall = margin_call(after, cash, p.mainM) ? 1 : 0;  // Broker.cpp:156-157
         }
         sa = after;
         // BrokerResponse of step k (overwritten if rolled back)
@@ -547,7 +548,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
         sh.rTp[cur][l] = tp[0];
         sh.rTu[cur][l] = tu[0];
         sh.rTc[cur][l] = tc[0];
-        sh.rPv[cur][l] = prevVal;
+        if (need_ar) sh.rPv[cur][l] = prevVal;  // the agent reward's L * P before the orders
         sh.rRk[cur][l] = rk[0];
         if (ls == 0) {
           sh.rCash[cur][el] = cash;
@@ -555,9 +556,12 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
           sh.rSh[cur][el] = after.sh;
           sh.rB[cur][el] = after.b;
           sh.rPrevEq[cur][el] = prevEq;
+          sh.rLpA[cur][el] = after.lp;
           sh.rK[cur][el] = k;
         }
-        flags = TR_STEP | (any_mc ? TR_ANYMC : 0) | (mcall ? TR_MCALL : 0);
+        // the Broker's post-order margin check (Broker.cpp:156-157) is the
+        // finish role's (marginCall output), off this role's chain
+        flags = TR_STEP | (any_mc ? TR_ANYMC : 0) | (in_kind != IN_NONE ? TR_MCALL : 0);
         k += 1;
       }
       if (WIN && refill) {
@@ -899,7 +903,12 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
         const size_t ie = kidx(k, sN, (size_t)env);
         if (om & O_OPT) ost(ov.obs_port + kidx(k, sNA1, bO), port0);
         if (om & O_DONE) ost(ov.done + ie, (uint8_t)(done ? 1 : 0));
-        if (om & O_MC) ost(ov.margin_call + ie, (uint8_t)((flags & TR_MCALL) ? 1 : 0));
+        if (om & O_MC) {
+          // TR_MCALL: orders ran (in_kind != NONE); the check on the sums after them
+          const Sums qa{sh.rLpA[prv][el], q.ml, q.sh, q.b};
+          const bool mcall = (flags & TR_MCALL) && margin_call(qa, cashv, p.mainM);
+          ost(ov.margin_call + ie, (uint8_t)(mcall ? 1 : 0));
+        }
         if (om & O_DEND) ost(ov.data_end + ie, (uint8_t)(RP ? sh.dend[prv][el] : 0u));
         if (om & O_REW) ost(ov.reward + ie, reward);
         if (om & O_NSH) ost(ov.n_shaped + ie, (uint8_t)pops);

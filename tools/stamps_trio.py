@@ -23,7 +23,9 @@ from madigan_amd import _lib as L  # noqa: E402
 def main():
     N = int(os.environ.get("N", 8192))
     fuse = int(os.environ.get("FUSE", 64))
-    env, _, _ = bench.workload_env("C3", N, 8, 0, "cuda:0")
+    nst = int(os.environ.get("NSTEP", 1))
+    extra = dict(nstep_return=nst, discount=0.99) if nst > 1 else {}
+    env, _, _ = bench.workload_env("C3", N, 8, 0, "cuda:0", **extra)
     assert int(env.lib.mgn_get_schedule(env.h)) == L.SCHED_TRIO
     fn = env.lib.mgn_diag_stamps
     fn.argtypes = [C.POINTER(C.c_ulonglong)]

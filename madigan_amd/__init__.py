@@ -7,6 +7,7 @@ libmadigan_hip.so); this package is the host side mirroring the reference's
 Python surface (madigan/environments, madigan/utils/preprocessor.py).
 """
 from . import _lib
+from . import reward_normalization
 from .config import ConfigError, SourceSpec, replay_spec, spec_from_config
 from .env import (Asset, BatchedEnv, BrokerResponse, DataSourceTick, Env, EnvInfo, RiskInfo, State,
                   get_env_info, make_batched_env, make_env)

@@ -81,6 +81,12 @@ constexpr int TRIO_W = 256;  // lanes per role
 #endif
 
 
+// NST: rounds of a pop's summands evaluated together (the terms' chains
+// interleave; rounds past the buffer's are computed and dropped)
+#ifndef MGN_NST_U
+#define MGN_NST_U 3
+#endif
+
 // the loop's exit test after iteration j's barrier: iterations 0..K always
 // run (the K steps, one iteration behind for the finish role), so the shared
 // `more` flag -- an LDS read on every role's path out of the barrier -- is
@@ -789,10 +795,13 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           const PopPre c = pop_pre(p.shaper, g.shA, g.shB);
           const int R = (len + S - 1) / S;
-          for (int j = 0; j < R; j += 2) {
-            double rr[2], dd[2];
+          // MGN_NST_U rounds of summands per pass, every one evaluated (on
+          // clamped operands) so their chains interleave; only the stores
+          // of rounds past R are skipped
+          for (int j = 0; j < R; j += MGN_NST_U) {
+            double rr[MGN_NST_U], dd[MGN_NST_U];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
+            for (int u = 0; u < MGN_NST_U; ++u) {
               const int kk = ls + (j + u) * S;
               int idx = head + kk;
               idx -= (idx >= n) ? n : 0;
@@ -801,16 +810,14 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
               dd[u] = s_disc[ok ? kk : 0];
             }
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
+            for (int u = 0; u < MGN_NST_U; ++u) {
               const int kk = ls + (j + u) * S;
-              if (j + u < R) {
 #ifdef MGN_NST_ABL_TERM  // diagnostic timing build (outputs wrong): no summand arithmetic
-                const double t = rr[u];
+              const double t = rr[u];
 #else
-                const double t = pop_term(p.shaper, rr[u], g.shA, g.shB, c, dd[u]);
+              const double t = pop_term(p.shaper, rr[u], g.shA, g.shB, c, dd[u]);
 #endif
-                scr[kk] = (kk < len) ? t : 0.0;
-              }
+              if (j + u < R) scr[kk] = (kk < len) ? t : 0.0;
             }
           }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -18,7 +18,6 @@ env step): numpy, no device work.
 """
 from __future__ import annotations
 
-import math
 from typing import Optional
 
 import numpy as np
@@ -308,4 +307,3 @@ class SharpeEWMA(RewardShaper):
 
 _CLASSES = {c.__name__: c for c in (SharpeFixedWindow, SortinoFixedWindowA, SortinoFixedWindowB,
                                      SortinoFixedWindowC, SharpeEWMA)}
-_ = math  # the reference's module imports math (unused there too)

@@ -424,12 +424,13 @@ def main():
     L.check(rc, h)
     # the sharded path's one collective, issued at log intervals
     # in a training loop, not per step: after the timed steps, timed on its own
-    ta = time.perf_counter()
     from madigan_amd import distributed as D
+    ta = time.perf_counter()
     gathered = D.allgather_env_stats(env, n_total=world * N)
     allgather_path = D.last_allgather_path
     torch.cuda.synchronize()
-    allgather_us = (time.perf_counter() - ta) * 1e6
+    # reported only when a collective ran ("local": one rank, no exchange)
+    allgather_us = (time.perf_counter() - ta) * 1e6 if allgather_path != "local" else None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         if args.dist_backend == "gloo":

@@ -341,9 +341,13 @@ int mgn_get_layout(const mgn_env *env);
  * in a generator wave that shares the SIMD; 2..16 assets, generator sources
  * or a replay tape, n-step rings that fit LDS); MGN_SCHED_TRIO = k_step_trio
  * (generator, ledger and finish waves pipelined one step apart, `done`
- * speculated; 2..8 assets, generator sources, nstep 1);
- * MGN_SCHED_AUTO (default) = TRIO, else DUO where eligible and the layout is
- * one asset per lane.  Results are bit-identical; only speed changes. */
+ * speculated; 2..16 assets, generator sources with n = 1 with or without a
+ * window, or a scalar n-step reward without a window whose rings fit the
+ * workgroup's LDS, and replay tapes at 16 assets for N >= 4096);
+ * MGN_SCHED_AUTO (default) = TRIO where eligible and measured faster (up to
+ * 8 assets; 16 assets without window and n = 1, or replay), else DUO where
+ * eligible and the layout is one asset per lane, else SINGLE.  Results are
+ * bit-identical; only speed changes. */
 enum { MGN_SCHED_AUTO = 0, MGN_SCHED_SINGLE = 1, MGN_SCHED_DUO = 2, MGN_SCHED_TRIO = 3 };
 int mgn_set_schedule(mgn_env *env, int32_t schedule);
 int mgn_get_schedule(const mgn_env *env);
@@ -384,7 +388,10 @@ int mgn_window_hist_view(mgn_env *env, mgn_hist_view *out);
  *   MGN_OP_CHECK_ORDER   Portfolio::checkRisk(assetIdx, units)
  *                        (Portfolio.cpp:254-279) into out->risk (N); no change
  * out: tprice / tunits / tcost / risk / margin_call device pointers (null =
- * not written); margin_call = Portfolio::checkRisk() after the operation. */
+ * not written); margin_call = Portfolio::checkRisk() after the operation.
+ * An asset index outside [0, n_assets) leaves that env untouched (response
+ * zero, risk code 0xFF, margin_call 0); the Python layer raises IndexError
+ * before calling, as the reference's std::out_of_range. */
 enum { MGN_OP_BROKER_UNITS = 0, MGN_OP_BROKER_SINGLE = 1, MGN_OP_BROKER_CLOSE = 2,
        MGN_OP_PORT_TXN = 3, MGN_OP_PORT_CLOSE = 4, MGN_OP_CHECK_ORDER = 5 };
 int mgn_ledger_op(mgn_env *env, int32_t op, const int32_t *asset_idx_dev, const double *units_dev,

@@ -420,8 +420,13 @@ def build_config(spec: SourceSpec, *, n_envs: int, init_cash: float = 1_000_000.
                  unit_size: float = 0.05, seed: int = 0, env_offset: int = 0,
                  nstep_return: int = 1, discount: float = 0.99, sortino_exp=None):
     A = spec.n_assets
-    if A < 1 or A > L.MAX_ASSETS:
-        raise ValueError(f"n_assets must be in [1, {L.MAX_ASSETS}], got {A}")
+    if A < 1:
+        raise ValueError(f"n_assets must be >= 1, got {A}")
+    if A > L.MAX_ASSETS:
+        # a limit of this build (the reference's Eigen vectors are dynamic):
+        # raised as the reference raises an unsupported config (ConfigError ->
+        # RuntimeError, DataTypes.h:36-46)
+        raise ConfigError(f"n_assets must be in [1, {L.MAX_ASSETS}] (MGN_MAX_ASSETS), got {A}")
     c = L.Config()
     c.n_envs = int(n_envs)
     c.n_assets = A
@@ -449,7 +454,7 @@ def build_config(spec: SourceSpec, *, n_envs: int, init_cash: float = 1_000_000.
     c.action_atoms = int(action_atoms)
     c.unit_size = float(unit_size)
     if not 1 <= int(nstep_return) <= L.MAX_NSTEP:
-        raise ConfigError(f"nstep_return must be in [1, {L.MAX_NSTEP}], got {nstep_return}")
+        raise ConfigError(f"nstep_return must be in [1, {L.MAX_NSTEP}] (MGN_MAX_NSTEP), got {nstep_return}")
     c.nstep = int(nstep_return)  # config.py:126 (Agent/Model spec)
     c.discount = float(discount)  # config.py:154
     c.n_feats = int(spec.n_feats) if spec.replay else 0

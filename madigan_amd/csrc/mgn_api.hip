@@ -179,9 +179,10 @@ int check_hip(mgn_env* e, hipError_t st, const char* what) {
 int validate(const mgn_config* c, const mgn_asset_source* s, std::string& msg) {
   if (!c || !s) { msg = "null config"; return MGN_ERR_ARG; }
   if (c->n_envs < 1) { msg = "n_envs must be >= 1"; return MGN_ERR_LENGTH; }
-  if (c->n_assets < 1 || c->n_assets > MGN_MAX_ASSETS) {
-    msg = "n_assets must be in [1, 64]";
-    return MGN_ERR_LENGTH;
+  if (c->n_assets < 1) { msg = "n_assets must be >= 1"; return MGN_ERR_LENGTH; }
+  if (c->n_assets > MGN_MAX_ASSETS) {  // this build's cap: an unsupported config
+    msg = "n_assets must be in [1, 64] (MGN_MAX_ASSETS)";
+    return MGN_ERR_CONFIG;
   }
   if (c->window < 0) { msg = "window must be >= 0"; return MGN_ERR_CONFIG; }
   if (c->shaper < 0 || c->shaper > MGN_SHAPER_SORTINO_B) { msg = "unknown reward shaper"; return MGN_ERR_CONFIG; }
@@ -342,8 +343,19 @@ bool trio_eligible(const mgn_env* e) {
   const bool nst_ok = e->cfg.nstep == 1 || (e->D == 1 && e->W == 0 && e->cfg.shaper < MGN_SHAPER_SHARPE);
   // replay tapes: 16 assets at the 256-lane layout (N * 16 >= 256 * 256), n = 1
   const bool rp_ok = !e->replay || (e->apad == 16 && e->cfg.nstep == 1 && (uint64_t)e->N * 16 >= 65536);
-  return e->apad >= 2 && e->apad <= 16 && !e->cfg.aux && rp_ok && nst_ok &&
-         (uint64_t)e->N * row < (1ull << 32) && (uint64_t)e->N * (uint64_t)e->cfg.nstep < (1ull << 32);
+  if (!(e->apad >= 2 && e->apad <= 16 && !e->cfg.aux && rp_ok && nst_ok &&
+        (uint64_t)e->N * row < (1ull << 32) && (uint64_t)e->N * (uint64_t)e->cfg.nstep < (1ull << 32)))
+    return false;
+  // n-step: the static arrays plus the envs' rings in dynamic LDS within a
+  // workgroup's 160 KiB (2 assets at n = 64 would need more: the two-role /
+  // single-role kernels run those)
+  if (e->cfg.nstep > 1) {
+    static size_t (*const lds_of[5])(long long, int) = {nullptr, mgn::trio_nst_lds_a2, mgn::trio_nst_lds_a4,
+                                                        mgn::trio_nst_lds_a8, mgn::trio_nst_lds_a16};
+    const int idx = e->apad <= 2 ? 1 : e->apad <= 4 ? 2 : e->apad <= 8 ? 3 : 4;
+    if (lds_of[idx](e->N, e->cfg.nstep) > mgn::kTrioLdsMax) return false;
+  }
+  return true;
 }
 // automatic: where the single-role kernel would run one lane per asset (small
 // batches: one wave per SIMD), give every asset a second (and a third) lane
@@ -1054,7 +1066,7 @@ int mgn_set_schedule(mgn_env* e, int32_t schedule) {
                 "the two-role kernel needs 2..16 assets, no multi-component source, n-step rings within LDS");
   if (schedule == MGN_SCHED_TRIO && !trio_eligible(e))
     return fail(e, MGN_ERR_CONFIG,
-                "the three-role kernel needs 2..8 assets, generator sources, nstep 1 or a scalar n-step reward without a window");
+                "the three-role kernel needs 2..16 assets, generator sources (or a replay tape at 16 assets), nstep 1 or a scalar n-step reward without a window whose rings fit LDS");
   e->sched = schedule;
   auto_layout(e);
   return MGN_OK;

@@ -668,6 +668,19 @@ __global__ __launch_bounds__(BLOCK) void k_ledger_op(KParams p, LedgerOp o) {
     P[i] = p.P[b + i];
   }
   double cash = p.cash[env];
+  if (o.op != MGN_OP_BROKER_UNITS && (o.aidx[env] < 0 || o.aidx[env] >= A)) {
+    // an asset index out of range (the Python layer raises IndexError first,
+    // as the reference's std::out_of_range): the env is left untouched, its
+    // response zero with risk code 0xFF
+    if (o.op != MGN_OP_PORT_TXN && o.op != MGN_OP_PORT_CLOSE) {
+      if (o.o_tp) o.o_tp[env] = 0.;
+      if (o.o_tu) o.o_tu[env] = 0.;
+      if (o.o_tc) o.o_tc[env] = 0.;
+      if (o.o_risk) o.o_risk[env] = (uint8_t)0xFF;
+    }
+    if (o.o_mc) o.o_mc[env] = 0;
+    return;
+  }
   if (o.op == MGN_OP_BROKER_UNITS) {
     // Broker::handleTransaction(port, units), Broker.cpp:144-158
     for (int i = 0; i < A; ++i) {

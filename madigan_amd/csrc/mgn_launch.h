@@ -47,12 +47,16 @@ struct ValArgs {
   hipStream_t stream;
 };
 
+// a workgroup's LDS on gfx950 (the three-role kernel's n-step eligibility)
+constexpr size_t kTrioLdsMax = 160 * 1024;
+
 // smallest assets-per-lane with at most 16 lanes per env (DPP-only reductions)
 constexpr int min_m(int apad) { return apad > 16 ? apad / 16 : 1; }
 
 #define MGN_DECLARE_APAD(A)                          \
   void launch_duo_a##A(const StepArgs& a);           \
   void launch_trio_a##A(const StepArgs& a);          \
+  size_t trio_nst_lds_a##A(long long n_envs, int nstep); \
   void launch_step_a##A(int m, const StepArgs& a);   \
   void launch_init_a##A(int m, const InitArgs& a);   \
   void launch_val_a##A(int m, const ValArgs& a);

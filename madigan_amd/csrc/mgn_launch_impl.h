@@ -35,7 +35,10 @@ void launch_duo(const StepArgs& a) {
   // NST: the envs' n-step rings in dynamic LDS (duo_nst_lds_bytes)
   const size_t lds = nst ? (size_t)epb * a.p.nstep * (a.p.D + 1) * sizeof(double) : 0;
   auto go = [&](auto kern) {
-    if (lds) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    // a refused size is the caller's hipGetLastError (HIP records every call's status)
+    if (lds && hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+                   hipSuccess)
+      return;
     launch_timed(a.ev0, a.ev1, kern, dim3(grid), dim3(DUO_BLOCK), (uint32_t)lds, a.stream, a.p, a.out,
                  a.in_kind, a.units, a.aidx, a.act, a.K);
   };
@@ -111,9 +114,13 @@ void launch_trio(const StepArgs& a) {
     return;
   }
   if (a.p.nstep > 1) {  // NST: the finish role's NStepBuffer rings in dynamic LDS (no window, D = 1)
-    const size_t lds = (size_t)epb * 2 * nst_pad(a.p.nstep) * sizeof(double);
+    const size_t lds = trio_nst_dyn_lds(S, small ? 64 : TRIO_W, a.p.nstep);
     auto goN = [&](auto kern) {
-      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      // a refused size is the caller's hipGetLastError (HIP records every
+      // call's status); trio_eligible keeps static + dynamic LDS within 160 KiB
+      if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+          hipSuccess)
+        return;
       launch_timed(a.ev0, a.ev1, kern, dim3(grid), dim3(small ? 192 : TRIO_BLOCK), (uint32_t)lds, a.stream,
                    a.p, a.out, a.in_kind, a.units, a.aidx, a.act, a.K);
     };
@@ -233,6 +240,14 @@ void dispatch_m(int m, const Arg& a) {
   }                                                                                          \
   void launch_trio_a##A(const StepArgs& a) {                                                 \
     if constexpr (A >= 2 && A <= 16) launch_trio<A>(a);                                       \
+  }                                                                                          \
+  size_t trio_nst_lds_a##A(long long n_envs, int nstep) {                                    \
+    if constexpr (A >= 2 && A <= 16) {                                                       \
+      const bool small = n_envs * A < 256LL * TRIO_W;                                        \
+      return (small ? trio_static_lds<A, 64, true>() : trio_static_lds<A, TRIO_W, true>()) +   \
+             trio_nst_dyn_lds(A, small ? 64 : TRIO_W, nstep);                                \
+    }                                                                                        \
+    return ~(size_t)0;                                                                       \
   }                                                                                          \
   void launch_step_a##A(int m, const StepArgs& a) { dispatch_m<StepL, A>(m, a); }            \
   void launch_init_a##A(int m, const InitArgs& a) { dispatch_m<InitL, A>(m, a); }            \

@@ -105,9 +105,14 @@ __device__ __forceinline__ bool trio_exit(int j, int K, const int32_t& more) {
 // window row, nothing else
 enum { TR_STEP = 1, TR_ANYMC = 2, TR_MCALL = 4, TR_REFILL = 8 };
 
-// NST: per env, the ring and the pop's summands in slots of nst_pad(n)
-// doubles (n rounded up to 8: whole rounds of 8 lanes, 64-B aligned)
-__host__ __device__ constexpr int nst_pad(int n) { return (n + 7) & ~7; }
+// NST: per env, the ring and the pop's summands in slots of nst_pad(n, S)
+// doubles: n rounded up to a multiple of max(8, S) -- a pop writes whole
+// rounds of S summands (R S slots, R = ceil(len / S)) and the ordered sum
+// reads R S / 2 pairs, so at S = 16 a multiple of 8 would run into the next
+// env's ring; 64-B aligned
+__host__ __device__ constexpr int nst_pad(int n, int S) {
+  return (n + (S > 8 ? S : 8) - 1) / (S > 8 ? S : 8) * (S > 8 ? S : 8);
+}
 
 template <int S, int TW = TRIO_W>
 struct TrioShared {
@@ -134,6 +139,19 @@ struct TrioShared {
   double feat[2][TRIO_W];
 };
 
+// LDS of k_step_trio<S, ..., TW, NST>: its static arrays (an upper bound of
+// the compiler's layout) plus, for NST, the rings in dynamic LDS; the
+// launcher's eligibility test keeps the sum within a workgroup's 160 KiB
+// (kTrioLdsMax, mgn_launch.h)
+template <int S, int TW, bool NST>
+constexpr size_t trio_static_lds() {
+  return sizeof(TrioShared<S, TW>) + (size_t)(TW / S) * sizeof(EnvRecs<S>) + S * sizeof(mgn_asset_source) +
+         (MGN_MAX_ASSETS + 1) * sizeof(double) + (NST ? MGN_MAX_NSTEP : 1) * sizeof(double) + 256;
+}
+inline size_t trio_nst_dyn_lds(int S, int TW, int nstep) {
+  return (size_t)(TW / S) * 2 * nst_pad(nstep, S) * sizeof(double);
+}
+
 // OMC: the output set when known at compile time (O_ALL, O_STD), else 0.
 // WIN: the handle keeps a window (StackerDiscrete ring, and the launch
 // history under mgn_rollout_hist).  The window rows are pushed by F, which
@@ -144,7 +162,7 @@ struct TrioShared {
 // k_step_duo / k_step.
 // NST: n-step aggregation (nstep > 1, scalar reward D = 1) in the finish
 // role: the env's NStepBuffer ring and one pop's summands in dynamic LDS
-// (launch_trio sizes it: envs per block x 2 nst_pad(n) doubles), the discounts staged
+// (launch_trio sizes it: envs per block x 2 nst_pad(n, S) doubles), the discounts staged
 // in LDS, so a pop is n LDS reads issued together, not n dependent loads.
 // GK >= 0: every asset's source is of kind GK (the generator role's per-lane
 // kind dispatch folds away: TrendOU at C3).
@@ -173,7 +191,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
   __shared__ mgn_asset_source s_src[S];
   __shared__ double s_tgt[MGN_MAX_ASSETS + 1];
   __shared__ double s_disc[NST ? MGN_MAX_NSTEP : 1];                     // NST: gamma^k
-  extern __shared__ __attribute__((aligned(16))) double s_nst[];          // NST: (EPB, 2 nst_pad(n))
+  extern __shared__ __attribute__((aligned(16))) double s_nst[];          // NST: (EPB, 2 nst_pad(n, S))
   const int role = threadIdx.x / TRIO_W;  // 0 generator, 1 ledger, 2 finish
   const int l = threadIdx.x % TRIO_W;
   const int el = l / S;
@@ -248,7 +266,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
       nlen = p.nlen[envc];
       nhead = p.nhead[envc];
       // the env's ring into LDS (every lane of the env copies a share)
-      double* ring = s_nst + (size_t)el * 2 * nst_pad(p.nstep);
+      double* ring = s_nst + (size_t)el * 2 * nst_pad(p.nstep, S);
       for (int i = ls; i < p.nstep; i += S) ring[i] = p.nring[(size_t)envc * p.nstep + i];
     }
   }
@@ -772,8 +790,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
         arr[0] = ar;
         rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(arr) : reward;
         const int n = p.nstep;
-        double* ring = s_nst + (size_t)el * 2 * nst_pad(n);  // ring, then the pop's summands
-        double* scr = ring + nst_pad(n);
+        double* ring = s_nst + (size_t)el * 2 * nst_pad(n, S);  // ring, then the pop's summands
+        double* scr = ring + nst_pad(n, S);
         const double v = (p.shaper == MGN_SHAPER_PPC) ? rin_s + cos_term : rin_s;
         const int L1 = nlen + 1;
         pops = done ? L1 : (L1 >= n ? 1 : 0);
@@ -983,7 +1001,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
 #endif
   if (!live) return;
   if constexpr (NST) {
-    const double* ring = s_nst + (size_t)el * 2 * nst_pad(p.nstep);
+    const double* ring = s_nst + (size_t)el * 2 * nst_pad(p.nstep, S);
     for (int i = ls; i < p.nstep; i += S) p.nring[(size_t)env * p.nstep + i] = ring[i];
     if (ls == 0) {
       p.nlen[env] = nlen;

@@ -300,6 +300,11 @@ class SharpeEWMA(RewardShaper):
         if r.shape != (self.N,):
             raise ValueError(f"reward must be ({self.N},), got {r.shape}")
         self._update(r)
+        # the .pyx divides by sqrt(ewssq) with Cython's checked division: a
+        # zero variance (a constant reward stream) raises ZeroDivisionError
+        # there, never a nan / inf into the caller's data
+        if np.any((self.count > 1) & (self.ewssq == 0.)):
+            raise ZeroDivisionError("float division by zero (SharpeEWMA: zero reward variance)")
         with np.errstate(divide="ignore", invalid="ignore"):
             out = np.where(self.count <= 1, 0., r / np.sqrt(self.ewssq))
         return float(out[0]) if self.scalar else out

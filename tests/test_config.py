@@ -121,3 +121,20 @@ def test_naive_shaper_config():
         build_config(spec, n_envs=2, reward_shaper="sortino_shaperA")
     c, _ = build_config(spec, n_envs=2, reward_shaper="sortino_shaperA", sortino_exp=3)
     assert c.sortino_exp == 3.0 and c.shaper == L.SHAPER_SORTINO_A
+
+
+def test_build_caps_raise_runtime_error():
+    """This build's fixed caps (include/madigan_amd.h MGN_MAX_ASSETS = 64,
+    MGN_MAX_NSTEP = 64; the reference's Eigen vectors and NStepBuffer are
+    unbounded, DataTypes.h:28-29, nstep_buffer.py:315-330) are refused as the
+    reference refuses an unsupported config: ConfigError, a RuntimeError
+    (DataTypes.h:36-46), before any device call."""
+    wide = ou_spec([10.] * (L.MAX_ASSETS + 1), [.15] * (L.MAX_ASSETS + 1), [.04] * (L.MAX_ASSETS + 1))
+    with pytest.raises(RuntimeError, match="MGN_MAX_ASSETS"):
+        build_config(wide, n_envs=4)
+    full = ou_spec([10.] * L.MAX_ASSETS, [.15] * L.MAX_ASSETS, [.04] * L.MAX_ASSETS)
+    assert build_config(full, n_envs=4)[0].n_assets == L.MAX_ASSETS
+    with pytest.raises(RuntimeError, match="MGN_MAX_NSTEP"):
+        build_config(spec_from_config(OU), n_envs=4, reward_shaper="DDR", nstep_return=L.MAX_NSTEP + 1)
+    assert build_config(spec_from_config(OU), n_envs=4, reward_shaper="DDR",
+                        nstep_return=L.MAX_NSTEP)[0].nstep == L.MAX_NSTEP

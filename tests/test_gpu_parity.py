@@ -292,6 +292,31 @@ def test_nstep_rollout(gpu, shaper, mode, n):
     close(gb, orc.scalar("shaperB"), "B")
 
 
+def test_nstep64_two_assets_auto_schedule(gpu):
+    """2 assets, n = 64, at a batch that takes the 256-lane layout: the
+    three-role kernel's static arrays plus 128 envs' rings (128 KiB) exceed a
+    workgroup's 160 KiB of LDS, so trio_eligible refuses it and the automatic
+    schedule runs another kernel -- the rollout launches and matches the
+    oracle (before the LDS check the three-role kernel was chosen and failed
+    at launch)."""
+    from madigan_amd import _lib as L
+    N, A, K = 40000, 2, 72
+    kw = dict(required_margin=0.02, maintenance_margin=0.25, transaction_cost_rel=0.02,
+              unit_size=0.9, auto_reset=1, init_cash=1e5, reward_shaper="DDR",
+              adaptation_rate=0.01, nstep_return=64, discount=0.97)
+    g, orc = make_pair(trendou_sources(A, [0.2, 2, 6, 0.05, 0.2, 5.0, 0.15, 0.3, 0.2, 0.99]), N, **kw)
+    assert g.lib.mgn_get_schedule(g.h) != L.SCHED_TRIO
+    assert g.lib.mgn_set_schedule(g.h, L.SCHED_TRIO) != 0  # refused, not launched
+    L.check(g.lib.mgn_set_schedule(g.h, L.SCHED_AUTO), g.h)
+    acts = g.generate_actions(K, seed=5)
+    host = {k: v.cpu().numpy() for k, v in g.rollout(acts).items()}
+    ref = orc.rollout(acts.cpu().numpy())
+    assert ref["done"].sum() > 0 and ref["n_shaped"].max() >= 1
+    out_check({**host, "shaped": ref["shaped"]}, ref, "nstep64", 1)
+    assert np.array_equal(host["n_shaped"], ref["n_shaped"]), "n_shaped"
+    np.testing.assert_allclose(host["shaped"], ref["shaped"], rtol=1e-10, atol=1e-14, err_msg="shaped")
+
+
 @pytest.mark.parametrize("A,kw", [
     (8, dict(reward_shaper="DDR")),
     (16, dict(reward_shaper="DDR")),
@@ -306,6 +331,10 @@ def test_nstep_rollout(gpu, shaper, mode, n):
     (4, dict(reward_shaper="DSR", nstep_return=5, discount=0.9)),
     (8, dict(reward_shaper="PPC", cosine_temp=0.05, nstep_return=3, reward_mode="agent_sum")),
     (2, dict(reward_shaper=None, nstep_return=7, discount=0.95)),
+    # 16 assets with n-step rings: the three-role kernel's pop writes whole
+    # rounds of 16 summands (nst_pad rounds n up to a multiple of 16)
+    (16, dict(reward_shaper="DDR", nstep_return=3, discount=0.9)),
+    (16, dict(reward_shaper="DSR", nstep_return=20, discount=0.99)),
 ])
 def test_schedules_bit_identical(gpu, A, kw):
     """The two-role kernel (k_step_duo: generator waves + ledger waves), the

@@ -322,6 +322,8 @@ def main():
     ap.add_argument("--nstep", type=int, default=1,
                     help="C3 diagnostics: n-step aggregation (nstep_return), not the headline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-k-sweep", dest="k_sweep", action="store_false",
+                    help="skip the K = 1 / 16 / 256 launch-length block of the line")
     ap.add_argument("--sweep", action="store_true",
                     help="also time 1/16/64/256 steps per launch (separate launches; keep it off "
                          "when profiling, so the kernel's rocprof average is the headline's)")
@@ -450,26 +452,47 @@ def main():
     value = world * N * args.steps / elapsed
     episodes = int(gathered[:, 3].sum().item())
 
-    # steps fused per launch (K in {1, 16, 256} beside the headline);
-    # outside the timed region, rank 0 only
+    # steps fused per launch (K in {1, 16, 256} beside the headline;
+    # K = 1 is the agent loop's shape, one env.step per policy step,
+    # offpolicy_q.py:143): per launch length the step kernel's own duration
+    # (HIP events recorded by the launch), and the per-step time of launches
+    # issued back to back through the same per-launch binding as the timed
+    # loop; outside the timed region, rank 0 only
     sweep = {}
-    if rank == 0 and args.sweep:
+    if rank == 0 and args.k_sweep:
         stream = torch.cuda.current_stream(dev)
         big = env.alloc_traj(256, fields=list(traj.keys()))
-        for K in (1, 16, 64, 256):
-            reps = max(2, 512 // K)
-            s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        # every launch reads K steps of actions (K, N, A) from sw_base
+        sw_actions = env.generate_actions(256, seed=0x6D6165)
+        sw_base = sw_actions.data_ptr()
+        for K in ((1, 16, 64, 256) if args.sweep else (1, 16, 256)):
+            assert sw_actions.shape[0] >= K
+            reps = max(4, 512 // K)
             fn = env.rollout_launcher({kk: v[:K] for kk, v in big.items()}, K)
-            fn(base)  # warm
+            fn(sw_base)  # warm
+            torch.cuda.synchronize()
+            L.check(lib.mgn_set_timing(h, 2), h)
+            for r in range(reps):
+                fn(sw_base)
+            torch.cuda.synchronize()
+            tk = (C.c_double * 4)()
+            L.check(lib.mgn_get_timing(h, tk), h)
+            L.check(lib.mgn_set_timing(h, 0), h)
+            launch_us = tk[0] / max(int(tk[1]), 1) * 1e3
+            s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s_ev.record(stream)
             for r in range(reps):
-                fn(base)
+                fn(sw_base)
             e_ev.record(stream)
             torch.cuda.synchronize()
             us = s_ev.elapsed_time(e_ev) * 1e3 / (reps * K)
-            sweep[str(K)] = {"us_per_step": us, "env_steps_per_s": N / us * 1e6,
+            sweep[str(K)] = {"kernel_us_per_launch": launch_us, "kernel_us_per_step": launch_us / K,
+                             "kernel_frac_survey_bytes": N * K * bpes / (launch_us * 1e-6) / 1e9 / PEAK_HBM_GBS,
+                             "back_to_back_us_per_step": us, "env_steps_per_s": N / us * 1e6,
                              "achieved_GBs_survey_bytes": N * bpes / us / 1e3,
-                             "fused_bytes_per_env_step": bytes_per_env_step(A, K, env.D)}
+                             "fused_bytes_per_env_step": bytes_per_env_step(A, K, env.D),
+                             "launches": reps}
+        del big, sw_actions
 
     if rank == 0 and args.dump_stats:
         np.save(args.dump_stats, gathered.cpu().numpy())
@@ -502,6 +525,16 @@ def main():
             roof["measured_traffic_note"] = ("PMC (2*FETCH_SIZE + WRITE_SIZE) * 1024 B per launch / "
                                              "avg_launch_us; below `achieved` because the fused "
                                              "kernel keeps the state in registers across steps")
+        # the resource that binds the launch, from the PMC figures: fp64 VALU
+        # issue (SQ_INSTS_VALU) against the HBM the launch really moved
+        # (FETCH_SIZE / WRITE_SIZE); `achieved` / `frac` stay priced on the
+        # algorithmic bytes either way
+        ci = roof["compute_issue"]
+        if ci and traffic:
+            busy = ci["valu_busy_frac_lower_bound"]
+            roof["bound"] = "valu" if busy > roof["measured_traffic_frac"] else "hbm"
+            roof["bound_note"] = (f"PMC: VALU issue >= {busy:.2f} of SIMD cycles vs HBM traffic "
+                                  f"{roof['measured_traffic_frac']:.2f} of 8 TB/s")
         if probe:
             roof["attainable_copy_GBs"] = probe
             roof["frac_of_attainable"] = achieved_gbs / probe
@@ -526,7 +559,12 @@ def main():
             "allgather_path": allgather_path,
         }
         if sweep:
-            res["fusion_sweep"] = sweep
+            res["launch_lengths"] = sweep
+            res["launch_lengths_note"] = (
+                "K steps per launch on the same handle after the timed region: kernel_us_per_launch "
+                "from the launch's own HIP events; back_to_back_us_per_step from events around "
+                "`launches` launches issued by the per-launch binding (host + dispatch included); "
+                "frac on SURVEY 8d bytes (1393 B per C3 env-step) over the kernel time")
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(N, A, args.cpu_budget)
         print(json.dumps(res))

@@ -335,8 +335,11 @@ __device__ __noinline__ double sinedyn_tick(const double* q, double* ax, bool tr
 // the hot generator registers) and is not selected for such handles.  GK >= 0:
 // every asset of the handle is of kind GK (the launcher checks), so the
 // per-lane kind dispatch folds away at compile time.
+// qreg: the lane's parameters in registers (the three-role kernel with a
+// compile-time kind, M = 1), else read from p.src
 template <int M, bool RP = true, bool AUX = true, int GK = -1>
-__device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, uint64_t tick) {
+__device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, uint64_t tick,
+                                         const double* qreg = nullptr) {
   if (RP && p.replay) {
     // HDFSourceSingle::getData (DataSource.cpp:391-398) on the tape: the
     // row iterCache / loadData would serve, then advance (wrap = the
@@ -362,7 +365,7 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
   for (int m = 0; m < M; ++m) {
     if (!s.valid[m]) continue;
     const int a = s.asset[m];
-    const double* q = p.src[a].p;
+    const double* q = qreg ? qreg : p.src[a].p;
     const int kind = GK >= 0 ? GK : s.kind[m];
     // the slot-0 variates, drawn once for every kind that reads them: a
     // Composite source's lanes (Synth / OU / TrendOU in one wave) then run one
@@ -530,11 +533,12 @@ __device__ __forceinline__ void put_feats(const Lane<M>& s, const KParams& p, in
 // source reset (DataSource.h:466, :232; DataSource.cpp:1495-1502; the replay
 // source carries on, DataSource.cpp:200-206)
 template <int M, bool AUX = true, int GK = -1>
-__device__ __forceinline__ void src_reset(Lane<M>& s, const KParams& p, int env, uint64_t tick) {
+__device__ __forceinline__ void src_reset(Lane<M>& s, const KParams& p, int env, uint64_t tick,
+                                          const double* qreg = nullptr) {
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     if (!s.valid[m]) continue;
-    const double* q = p.src[s.asset[m]].p;
+    const double* q = qreg ? qreg : p.src[s.asset[m]].p;
     const int kind = GK >= 0 ? GK : s.kind[m];
     if (kind == MGN_SRC_TRENDOU) {
       s.tfl[m] &= ~1;

@@ -45,7 +45,10 @@ namespace mgn {
 // diagnostic build: s_memtime stamps of the first 256 blocks, 64 slots each --
 // [0] entry, [1] after the prologue barrier, [2 + j] generator lane 0 after
 // iteration j's barrier (j < 40), [44] generator / [45] ledger / [46] finish
-// lane 0 after its epilogue stores (with their completion wait)
+// lane 0 after its epilogue stores (with their completion wait); [47] G lane 0
+// once the kernel arguments arrived, [48] G lane 0 once its iteration-0 tick
+// is published to LDS, [49] L lane 0 once its iteration-0 records are
+// published, [50] F lane 0 once its iteration-1 outputs are issued
 __device__ unsigned long long g_iter[256 * 64];
 #define MGN_IT(slot, lane0)                                             \
   if (threadIdx.x == (lane0) && blockIdx.x < 256 && (slot) < 64)        \
@@ -181,6 +184,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
                                                           const int8_t* __restrict__ act_in, int K) {
   MGN_IT(0, 0);
   warm_kernargs<(int)(sizeof(KParams) + sizeof(mgn_traj) + 48)>();
+  MGN_IT(47, 0);
   const int in_kind = DISC ? IN_DISCRETE : in_kind_rt;
   constexpr int M = 1;
   constexpr int TRIO_W = TW;
@@ -208,10 +212,21 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
   s.pf_ok = false;
   s.fcol = (RP && p.F <= S) ? ls : -1;  // RP: one feature column per lane
   const size_t li = (size_t)envc * A + (s.valid[0] ? ls : 0);
+  // QREG: the handle's one source kind is known at compile time (GK), so the
+  // generator lanes hold their asset's few parameters in registers, loaded
+  // with the state (TrendOU: q[0..8], OU: q[0..2]) -- no LDS staging, and no
+  // prologue barrier: every role starts its first iteration as soon as its
+  // own state arrives (the one-step launch's prologue was two memory round
+  // trips and a barrier before the orders could start)
+  constexpr int NQ = RP ? 0 : GK == MGN_SRC_TRENDOU ? 9 : GK == MGN_SRC_OU ? 3 : 0;
+  constexpr bool QREG = NQ > 0;
+  double qr[QREG ? NQ : 1];
+  const double* const tgt_g = p.target;  // the PPC target in global memory (F's prologue)
 #ifdef MGN_TRIO_ABL_PRO
   s.P[0] = 5.0;
 #else
-  s.P[0] = s.valid[0] ? p.P[li] : 0.;
+  // the finish role takes its prices from the generator's LDS records
+  s.P[0] = (s.valid[0] && role != 2) ? p.P[li] : 0.;
 #endif
   s.L[0] = s.mep[0] = s.Bm[0] = s.sx[0] = s.oum[0] = s.dy[0] = 0.;
   s.tlen[0] = 0;
@@ -230,12 +245,25 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
 #else
   if (role == 0) {
 #endif
+    // only the fields the kind reads (GK): TrendOU no sine phase, OU none
+    constexpr bool r_sx = GK < 0 || GK == MGN_SRC_SINE || GK == MGN_SRC_SAWTOOTH || GK == MGN_SRC_TRIANGLE ||
+                          GK == MGN_SRC_TRENDYOU;
+    constexpr bool r_oum = GK < 0 || GK == MGN_SRC_TRENDOU || GK == MGN_SRC_TRENDYOU || GK == MGN_SRC_OUPAIR;
+    constexpr bool r_trend = GK < 0 || GK == MGN_SRC_TRENDOU || GK == MGN_SRC_SIMPLETREND ||
+                             GK == MGN_SRC_TRENDYOU;
     if (s.valid[0]) {
-      s.sx[0] = p.sx[li];
-      s.oum[0] = p.oum[li];
-      s.dy[0] = p.dy[li];
-      s.tlen[0] = p.tlen[li];
-      s.tfl[0] = p.tfl[li];
+      if (r_sx) s.sx[0] = p.sx[li];
+      if (r_oum) s.oum[0] = p.oum[li];
+      if (r_trend) {
+        s.dy[0] = p.dy[li];
+        s.tlen[0] = p.tlen[li];
+        s.tfl[0] = p.tfl[li];
+      }
+    }
+    if constexpr (QREG) {
+      const double* q = p.src[s.valid[0] ? ls : 0].p;
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) qr[i] = q[i];
     }
     ts = p.ts[envc];
     if (RP) s.rcur = p.rcur[envc];
@@ -271,10 +299,13 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     }
   }
   {
-    const double* g = reinterpret_cast<const double*>(p.src);
-    double* d = reinterpret_cast<double*>(s_src);
-    const int n = p.A * (int)(sizeof(mgn_asset_source) / sizeof(double));
-    for (int i = threadIdx.x; i < n; i += TRIO_BLOCK) d[i] = g[i];
+    if (!QREG) {
+      const double* g = reinterpret_cast<const double*>(p.src);
+      double* d = reinterpret_cast<double*>(s_src);
+      const int n = p.A * (int)(sizeof(mgn_asset_source) / sizeof(double));
+      for (int i = threadIdx.x; i < n; i += TRIO_BLOCK) d[i] = g[i];
+    }
+    // read by the finish role from iteration 1 on (after iteration 0's barrier)
     if (p.target)
       for (int i = threadIdx.x; i <= p.A; i += TRIO_BLOCK) s_tgt[i] = p.target[i];
     if (NST)
@@ -282,10 +313,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     p.src = s_src;
     if (p.target) p.target = s_tgt;
   }
-  if (role == 1 && ls == 0) {  // no step before iteration 0, no reset pending
-    sh.rFlags[1][el] = 0;
-    sh.reset[1][el] = 0;
-  }
+  // iteration 0 reads no record of another role (no step before it, no reset
+  // pending: the j > 0 tests below), and `more` is read from iteration K >= 1
+  // on, after G zeroed its slot one iteration earlier
   if (threadIdx.x == 0) {
     sh.more[0] = 0;
     sh.more[1] = 0;
@@ -294,9 +324,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
 #ifdef MGN_STAMPS
   if (threadIdx.x < 8) s_duo_sub[threadIdx.x] = 0;
 #endif
-  __syncthreads();
+  if (!QREG || K == 0 || !MGN_TRIO_MORESKIP) __syncthreads();
   MGN_IT(1, 0);
-  s.kind[0] = s.valid[0] ? s_src[ls].kind : -1;
+  s.kind[0] = s.valid[0] ? (QREG ? GK : s_src[ls].kind) : -1;
 
   if (role == 0) {
     // ---------------- generator waves: tick of step j, State.price / timestamp
@@ -325,7 +355,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
       if constexpr (RP) {
         duo_replay_tick(s, p, ts, rp, rnx);
       } else {
-        gen_tick<M, false, false, GK>(s, p, env, ts);
+        gen_tick<M, false, false, GK>(s, p, env, ts, QREG ? qr : nullptr);
         ts = ts + 1;
       }
     };
@@ -356,8 +386,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
       MGN_T(T0);
       if (threadIdx.x == 0) sh.more[(j + 1) % 3] = 0;
       if (live) {
-        const bool rst = sh.reset[prv][el] != 0;
-        const bool prev_step = (sh.rFlags[prv][el] & TR_STEP) != 0;
+        const bool rst = j > 0 && sh.reset[prv][el] != 0;
+        const bool prev_step = j > 0 && (sh.rFlags[prv][el] & TR_STEP) != 0;
         if (WIN && !rst && gpend > 0) {
           // a refill tick (not speculative: the reset is confirmed)
           tick();
@@ -381,8 +411,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
             k -= 1;
           }
           // Env::reset -> dataSource->reset + getData (Env.h:181-187)
-          src_reset<M, false, GK>(s, p, env, ts);
-          gen_tick<M, false, false, GK>(s, p, env, ts);
+          src_reset<M, false, GK>(s, p, env, ts, QREG ? qr : nullptr);
+          gen_tick<M, false, false, GK>(s, p, env, ts, QREG ? qr : nullptr);
           ts = ts + 1;
           if (WIN) gpend = p.W - 1;
         } else if (k < K) {
@@ -418,6 +448,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
         }
         sh.feat[cur][l] = rp.curF;
       }
+      if (j == 0) MGN_IT(48, 0);
       MGN_T(T1);
       __syncthreads();
       MGN_T(T2);
@@ -483,8 +514,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     for (int j = 0;; ++j) {
       const int cur = j & 1, prv = cur ^ 1;
       MGN_T(T0);
-      const bool rst = live && sh.reset[prv][el] != 0;
-      const bool prev_step = (sh.rFlags[prv][el] & TR_STEP) != 0;
+      const bool rst = live && j > 0 && sh.reset[prv][el] != 0;
+      const bool prev_step = j > 0 && (sh.rFlags[prv][el] & TR_STEP) != 0;
       // WIN: this iteration's tick refills the window (the reset tick or one
       // of the W - 1 after it): no step
       const bool refill = WIN && live && (rst || lpend > 0);
@@ -600,6 +631,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
       if (ls == 0) sh.rFlags[cur][el] = flags;
       // another iteration: F evaluates this step, or steps remain
       if (live && (stepping || rst || refill || k < K || (WIN && lpend > 0))) sh.more[j % 3] = 1;
+      if (j == 0) MGN_IT(49, TRIO_W);
       MGN_T(T1);
       __syncthreads();
       MGN_T(T2);
@@ -653,9 +685,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
   g.cos_qn = 0.;
   if (p.shaper == MGN_SHAPER_PPC) {
     double qq[M];
-    const double q = s.valid[0] ? s_tgt[1 + s.asset[0]] : 0.;
+    const double q = s.valid[0] ? tgt_g[1 + s.asset[0]] : 0.;
     qq[0] = q * q;
-    g.cos_qn = sqrt(s_tgt[0] * s_tgt[0] + canon<M, S>(qq));
+    g.cos_qn = sqrt(tgt_g[0] * tgt_g[0] + canon<M, S>(qq));
   }
   const bool need_ar = (p.reward_mode != MGN_REWARD_ENV_LOG) || (om & O_AREW);
   // output element strides per step (32-bit: checked on the host) and the
@@ -730,7 +762,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     MGN_T(T0);
     int rst_out = 0;
     // the step L ran in iteration j-1, unless F voided it at iteration j-1
-    const int flags = sh.rFlags[prv][el];
+    const int flags = j > 0 ? sh.rFlags[prv][el] : 0;
 #ifdef MGN_TRIO_ABL_F  // diagnostic timing build: no step finish, no outputs
     if (false) {
 #else
@@ -981,6 +1013,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     }
     if (ls == 0) sh.reset[cur][el] = rst_out;
     if (rst_out) sh.more[j % 3] = 1;  // the reset tick runs next iteration
+    if (j == 1) MGN_IT(50, 2 * TRIO_W);
     MGN_T(T1);
     __syncthreads();
     MGN_T(T2);

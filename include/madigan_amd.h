@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MGN_ABI_VERSION 7
+#define MGN_ABI_VERSION 8
 #define MGN_MAX_ASSETS 64
 #define MGN_MAX_NSTEP 64
 
@@ -203,6 +203,9 @@ typedef struct {
   int64_t *replay_cursor;                            /* (N) next tape row of a replay env */
   double *aux;                                       /* (N,A,MGN_AUX_WIDTH) multi-component
                                                         source state (NULL if unused) */
+  uint64_t *draw_skip;                               /* (N) resets so far: the variates'
+                                                        draw index is timestamp + draw_skip
+                                                        (ABI 8; DESIGN.md, variates v3) */
   mgn_traj out;                                      /* mgn_step outputs */
   int32_t n_envs, n_assets, window, reward_dim, nstep, n_feats;
 } mgn_views;

@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmadigan_hip.so")
 MAX_ASSETS = 64
-ABI_VERSION = 7
+ABI_VERSION = 8
 SRC_PARAMS = 64
 AUX_WIDTH = 24
 MAX_NSTEP = 64
@@ -71,7 +71,7 @@ VIEW_PTR_FIELDS = ("ledger", "mean_entry", "borrowed", "prices", "sine_x", "ou_m
                    "ep_stats", "episode_stats", "ext_prices", "units", "asset_idx", "ring",
                    "ring_ts", "ring_head", "ring_len", "win_price", "win_port", "win_ts",
                    "reset_mask", "nstep_ring", "nstep_len", "nstep_head", "replay_cursor",
-                   "aux")
+                   "aux", "draw_skip")
 
 
 class Views(C.Structure):

@@ -98,7 +98,7 @@ struct mgn_env {
 namespace {
 
 struct Offsets {
-  size_t L, mep, Bm, P, sx, oum, dy, tlen, tfl, cash, ts, sA, sB, ep, epstats, ext, units, aidx,
+  size_t L, mep, Bm, P, sx, oum, dy, tlen, tfl, cash, ts, dskip, sA, sB, ep, epstats, ext, units, aidx,
       ring, ring_ts, rhead, rlen, wprice, wport, wts, mask, reward, areward, shaped, done, obsp,
       obsport, obsts, tprice, tunits, tcost, risk, mcall, nshaped, dend, nring, nlen, nhead, disc,
       src, target, rcur, aux;
@@ -124,6 +124,7 @@ Offsets plan(const mgn_config* c) {
   o.tfl = l.add(N * A);
   o.cash = l.add(N * 8);
   o.ts = l.add(N * 8);
+  o.dskip = l.add(N * 8);
   o.sA = l.add(N * D * 8);
   o.sB = l.add(N * D * 8);
   o.ep = l.add(N * 2 * 8);
@@ -282,7 +283,7 @@ mgn::KParams kparams(const mgn_env* e) {
   const mgn_views& v = e->v;
   p.L = v.ledger; p.mep = v.mean_entry; p.Bm = v.borrowed; p.P = v.prices;
   p.sx = v.sine_x; p.oum = v.ou_mean; p.dy = v.trend_dy; p.tlen = v.trend_len; p.tfl = v.trend_flags;
-  p.cash = v.cash; p.ts = v.timestamp; p.sA = v.shaper_a; p.sB = v.shaper_b;
+  p.cash = v.cash; p.ts = v.timestamp; p.dskip = v.draw_skip; p.sA = v.shaper_a; p.sB = v.shaper_b;
   p.ep = v.ep_stats; p.epstats = v.episode_stats; p.ext = v.ext_prices;
   p.ring = v.ring; p.ring_ts = v.ring_ts; p.rhead = v.ring_head; p.rlen = v.ring_len;
   p.src = e->src_dev; p.src_g = e->src_dev; p.target = e->target_dev;
@@ -527,6 +528,7 @@ int mgn_create(const mgn_config* cfg, const mgn_asset_source* sources, void* str
   v.prices = (double*)(b + o.P); v.sine_x = (double*)(b + o.sx); v.ou_mean = (double*)(b + o.oum);
   v.trend_dy = (double*)(b + o.dy); v.trend_len = (int32_t*)(b + o.tlen); v.trend_flags = (uint8_t*)(b + o.tfl);
   v.cash = (double*)(b + o.cash); v.timestamp = (uint64_t*)(b + o.ts);
+  v.draw_skip = (uint64_t*)(b + o.dskip);
   v.shaper_a = (double*)(b + o.sA); v.shaper_b = (double*)(b + o.sB);
   v.ep_stats = (double*)(b + o.ep); v.episode_stats = (double*)(b + o.epstats);
   v.ext_prices = (double*)(b + o.ext); v.units = (double*)(b + o.units); v.asset_idx = (int32_t*)(b + o.aidx);

@@ -846,6 +846,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       for (int i = ls; i < nD; i += S) nst.ring[i] = p.nring[(size_t)envc * nD + i];
     }
     ts = p.ts[envc];
+    s.dskip = p.dskip[envc];
     ep_ret = p.ep[(size_t)envc * 2];
     ep_len = p.ep[(size_t)envc * 2 + 1];
     n_done = p.epstats[(size_t)envc * 4 + 3];
@@ -956,6 +957,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
         if (live && sh.tick[el]) {
           if constexpr (RP) {
             // the replay source carries on through a reset (DataSource.cpp:200-206)
+            if (sh.reset[el]) s.dskip += 1;  // Env::reset counts (the draw index)
             duo_replay_tick(s, p, ts, rp, rnx);
           } else {
             if (sh.reset[el]) src_reset<M, false, GK>(s, p, env, ts);  // Env::reset -> dataSource->reset (Env.h:183)
@@ -1035,6 +1037,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
     }
     if (ls == 0) {
       p.ts[env] = ts;
+      p.dskip[env] = s.dskip;
       if (RP) p.rcur[env] = s.rcur;
       p.ep[(size_t)env * 2] = g.ep_ret;
       p.ep[(size_t)env * 2 + 1] = g.ep_len;

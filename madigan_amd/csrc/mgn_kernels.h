@@ -49,6 +49,7 @@ struct KParams {
   uint8_t *tfl;
   double *cash;
   uint64_t *ts;
+  uint64_t *dskip;  // (N) resets so far: the variates' draw index is ts + dskip
   double *sA, *sB;
   double *ep;       // (N,2)
   double *epstats;  // (N,4)
@@ -215,6 +216,11 @@ struct Lane {
   double pfP[M], pfF, curF;
   int fcol = -1;       // feature column of this lane (-1: features read per row)
   bool pf_ok = false;  // pfP / pfF hold row rcur
+  // variates (mgn_math.h, v3): the env's resets so far (draw index d =
+  // timestamp + dskip), and per slot the cached odd half of the last pair
+  uint64_t dskip = 0;
+  double zc[M] = {};
+  uint64_t ztag[M] = {};
 };
 
 // ---------------------------------------------------------------------------
@@ -273,7 +279,7 @@ __device__ __noinline__ double sineadder_tick(const double* q, double* ax, uint6
   double sum = 0.;
   for (int c = 0; c < C; ++c) {
     double nz = 0.0;  // component c's noise: the block of counter slot c
-    if (q[2] != 0.0) nz = draw_s(seed, genv, asset, (uint32_t)c, tick).z * q[2] + 0.0;
+    if (q[2] != 0.0) nz = normal_of(block(seed, genv, asset, (uint32_t)c, tick)) * q[2] + 0.0;
     sum += (nz + q[3 + C + c]) + q[3 + 2 * C + c] * det_sin(PI2 * ax[c] * q[3 + c]);
     ax[c] += q[1];
   }
@@ -294,7 +300,7 @@ __device__ __noinline__ double sinedyn_tick(const double* q, double* ax, bool tr
     else sum += a[2] + a[3] * out;
   }
   double nz = 0.0;
-  if (q[2] != 0.0) nz = draw_from(x0).z * q[2] + 0.0;
+  if (q[2] != 0.0) nz = normal_of(x0) * q[2] + 0.0;
   if (!trend) return sum + nz;
   const double* tq = q + 3 + 10 * C;  // T, then per trend {minLen, maxLen, incr, prob}
   const int T = (int)tq[0];
@@ -361,6 +367,7 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
     return;
   }
   const uint64_t genv = (uint64_t)(p.env_offset + env);
+  tick += s.dskip;  // the draw index (mgn_math.h, v3)
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     if (!s.valid[m]) continue;
@@ -376,7 +383,7 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
                        kind == MGN_SRC_TRENDYOU || kind == MGN_SRC_GAUSSIAN || kind == MGN_SRC_OUPAIR ||
                        (sine_fam && q[5] != 0.0);
     Draw d = {0.0, 0.0, 0u};
-    if (need0) d = draw0(p.seed, genv, (uint32_t)a, tick);
+    if (need0) d = draw_d(p.seed, genv, (uint32_t)a, tick, s.zc[m], s.ztag[m]);
     if (kind == MGN_SRC_TRENDOU) {
       double y = s.P[m];
       if (s.tfl[m] & 1) {
@@ -482,7 +489,7 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
       // is keyed by the pair's first asset, counter slot 2)
       const uint32_t a0 = (uint32_t)(a - (q[3] != 0.0 ? 1 : 0));
       double mean = s.oum[m];
-      mean += mean * (draw_s(p.seed, genv, a0, 2, tick).z * q[2] + 0.0);
+      mean += mean * (normal_of(block(p.seed, genv, a0, 2, tick)) * q[2] + 0.0);
       const double z = d.z * q[1] + 0.0;
       double x = s.P[m];
       x += (q[0] * (mean - x)) + mean * z;
@@ -535,6 +542,9 @@ __device__ __forceinline__ void put_feats(const Lane<M>& s, const KParams& p, in
 template <int M, bool AUX = true, int GK = -1>
 __device__ __forceinline__ void src_reset(Lane<M>& s, const KParams& p, int env, uint64_t tick,
                                           const double* qreg = nullptr) {
+  // every Env::reset skips one draw index (mgn_math.h, v3): the reset's
+  // getData draws at timestamp + resets
+  s.dskip += 1;
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     if (!s.valid[m]) continue;
@@ -560,7 +570,7 @@ __device__ __forceinline__ void src_reset(Lane<M>& s, const KParams& p, int env,
       s.oum[m] = 10.;
     } else if (AUX && (kind == MGN_SRC_SINEDYNAMIC || kind == MGN_SRC_SINEDYNTREND)) {  // :794-800, :994-1000
       sd_sample(p.src_g[s.asset[m]].p, p.aux + ((size_t)env * p.A + s.asset[m]) * MGN_AUX_WIDTH, p.seed,
-                (uint64_t)(p.env_offset + env), (uint32_t)s.asset[m], tick);
+                (uint64_t)(p.env_offset + env), (uint32_t)s.asset[m], tick + s.dskip);
     }
   }
 }
@@ -1327,6 +1337,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
   if (p.replay && p.F <= S) s.fcol = ls;  // one feature column per lane: prefetched
   double cash = p.cash[env];
   uint64_t ts = p.ts[env];
+  s.dskip = p.dskip[env];
   double shA[M], shB[M];  // shaper state: slot values for D==A, [0] for D==1
 #pragma unroll
   for (int m = 0; m < M; ++m) {
@@ -1638,6 +1649,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
   if (ls == 0) {
     p.cash[env] = cash;
     p.ts[env] = ts;
+    p.dskip[env] = s.dskip;
     if (p.replay) p.rcur[env] = s.rcur;
     p.ep[(size_t)env * 2] = ep_ret;
     p.ep[(size_t)env * 2 + 1] = ep_len;
@@ -1715,6 +1727,7 @@ __global__ __launch_bounds__(BLOCK) void k_init_reset(KParams p, int mode,
       }
     }
     ts = 0;
+    s.dskip = 0;
     cash = p.init_cash;
     // replay: env g starts at tape row (g * stride) mod rows
     s.rcur = p.replay ? (int64_t)(((uint64_t)(p.env_offset + env) * (uint64_t)p.rp_stride) %
@@ -1736,6 +1749,7 @@ __global__ __launch_bounds__(BLOCK) void k_init_reset(KParams p, int mode,
     load_lane<M>(s, p, env, ls);
     cash = p.cash[env];
     ts = p.ts[env];
+    s.dskip = p.dskip[env];
     if (p.W > 0) {
       head = p.rhead[env];
       len = p.rlen[env];
@@ -1750,6 +1764,7 @@ __global__ __launch_bounds__(BLOCK) void k_init_reset(KParams p, int mode,
   if (ls == 0) {
     p.cash[env] = cash;
     p.ts[env] = ts;
+    p.dskip[env] = s.dskip;
     if (p.replay) p.rcur[env] = s.rcur;
   }
 }

@@ -109,21 +109,6 @@ __device__ __forceinline__ double k_cos(double x, double y) {
   return w + (((1.0 - w) - hz) + (z * r - x * y));
 }
 
-// cos(2 pi u), u in [0,1)
-__device__ __forceinline__ double det_cos2pi(double u) {
-  const double pio2 = bits_to_d(0x3FF921FB54442D18ull);
-  const double t = 4.0 * u;
-  const double q = floor(t + 0.5);
-  const double f = t - q;
-  const double r = f * pio2;
-  const int iq = ((int)q) & 3;
-  const double c = k_cos(r, 0.0);
-  const double s = k_sin(r, 0.0, false);
-  // branch-free quadrant select (same values as the oracle's switch)
-  double v = (iq & 1) ? s : c;
-  return (iq == 1 || iq == 2) ? -v : v;
-}
-
 // sin(x) with fdlibm's medium Cody-Waite reduction
 __device__ __noinline__ double det_sin(double x) {
   const double invpio2 = bits_to_d(0x3FE45F306DC9C883ull);
@@ -196,43 +181,146 @@ __device__ __forceinline__ double rt_sqrt(double x) {
   return __builtin_fma(__builtin_fma(-g, g, x), h, g);
 }
 
-// Variates of one (env, asset, tick) from its slot-0 block x0..x3:
-//   u1 = ((x1:x0 >> 11) + 1) 2^-53 in (0,1],  u2 = x2 2^-32 in [0,1)
-//   z  = sqrt(-2 log u1) cos(2 pi u2)            (Box-Muller)
-//   ut = x3 2^-32 in [0,1)                        (TrendOU regime switch)
-//   dbit = x0 & 1                                 (TrendOU direction, a bit u1 drops)
+// Variates, specification v3 (this framework's own: the reference's streams
+// are seeded from the wall clock and cannot be replayed).  Every tick of an
+// (env, asset) has a draw index d = timestamp + resets (Lane.dskip: each
+// Env::reset skips one index, so an auto-reset keeps d's parity in step with
+// the other envs').  Ticks come in pairs P = d >> 1 that share one
+// Box-Muller transform of block A = Philox4x32-10(key seed, counter (P, env,
+// asset | 0 << 16)):
+//   u1 = ((xA1:xA0 >> 11) + 1) 2^-53 in (0,1],  u2 = xA2 2^-32 in [0,1)
+//   r  = sqrt(-2 log u1)
+//   d even: z = r cos(2 pi u2),  ut = xA3 2^-32,  dbit = xA0 & 1 (a bit u1 drops)
+//   d odd:  z = r sin(2 pi u2),  ut = xB3 2^-32,  dbit = xB0 & 1 from block B
+//           (counter slot 3 of the same pair)
+// (z: the normal variate; ut: the TrendOU regime-switch uniform; dbit: the
+// trend direction.)  The other blocks -- slot 1 (trend length and slope),
+// OUPair's slot 2, SineAdder's slot c, SineDynamic's 0 and 16 + c -- are keyed
+// by d itself.  log, cos and sin are fdlibm's algorithms with their
+// polynomials in fused multiply-add Horner form (v_log2pi / v_sincos2pi;
+// fma is correctly rounded, so the host restatement reproduces every bit).
+// A lane keeps the odd half of its last pair (zc, tagged P + 1): in a kernel
+// whose lanes tick in step the pair's transform runs on even ticks only and
+// an odd tick draws block B alone.
 struct Draw {
   double z, ut;
   uint32_t dbit;
 };
 
-__device__ __forceinline__ Draw draw_from(const u4& x) {
+// fdlibm e_log.c for the variate's u1 in (0, 1] (normal, positive), the
+// polynomial in fma form
+__device__ __forceinline__ double v_log(double x) {
+  const double ln2_hi = bits_to_d(0x3fe62e42fee00000ull);
+  const double ln2_lo = bits_to_d(0x3dea39ef35793c76ull);
+  const double Lg1 = bits_to_d(0x3FE5555555555593ull), Lg2 = bits_to_d(0x3FD999999997FA04ull),
+               Lg3 = bits_to_d(0x3FD2492494229359ull), Lg4 = bits_to_d(0x3FCC71C51D8E78AFull),
+               Lg5 = bits_to_d(0x3FC7466496CB03DEull), Lg6 = bits_to_d(0x3FC39A09D078C69Full),
+               Lg7 = bits_to_d(0x3FC2F112DF3E5244ull);
+  const uint64_t ix = d_to_bits(x);
+  int32_t hx = (int32_t)(ix >> 32);
+  int32_t k = ((hx >> 20) & 0x7ff) - 1023;
+  hx &= 0x000fffff;
+  const int32_t i = (hx + 0x95f64) & 0x100000;
+  k += (i >> 20);
+  const uint64_t mb = ((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (ix & 0xffffffffull);
+  const double f = bits_to_d(mb) - 1.0;
+  const double s = f / (2.0 + f);
+  const double dk = (double)k;
+  const double z = s * s;
+  const double w = z * z;
+  const double t1 = w * __builtin_fma(w, __builtin_fma(w, Lg6, Lg4), Lg2);
+  const double t2 = z * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, Lg7, Lg5), Lg3), Lg1);
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
+// cos(2 pi u) and sin(2 pi u), u in [0,1): t = 4u, q = floor(t + 1/2),
+// r = (t - q) pi/2, fdlibm's __kernel_cos / __kernel_sin (y = 0) on r in fma
+// form, placed by the quadrant q mod 4
+__device__ __forceinline__ void v_sincos2pi(double u, double& sn, double& cs) {
+  const double S1 = bits_to_d(0xBFC5555555555549ull), S2 = bits_to_d(0x3F8111111110F8A6ull),
+               S3 = bits_to_d(0xBF2A01A019C161D5ull), S4 = bits_to_d(0x3EC71DE357B1FE7Dull),
+               S5 = bits_to_d(0xBE5AE5E68A2B9CEBull), S6 = bits_to_d(0x3DE5D93A5ACFD57Cull);
+  const double C1 = bits_to_d(0x3FA555555555554Cull), C2 = bits_to_d(0xBF56C16C16C15177ull),
+               C3 = bits_to_d(0x3EFA01A019CB1590ull), C4 = bits_to_d(0xBE927E4F809C52ADull),
+               C5 = bits_to_d(0x3E21EE9EBDB4B1C4ull), C6 = bits_to_d(0xBDA8FAE9BE8838D4ull);
+  const double pio2 = bits_to_d(0x3FF921FB54442D18ull);
+  const double t = 4.0 * u;
+  const double q = floor(t + 0.5);
+  const double x = (t - q) * pio2;
+  const int iq = ((int)q) & 3;
+  const double z = x * x;
+  // __kernel_sin: x + x^3 (S1 + z r)
+  const double rs = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, S6, S5), S4), S3), S2);
+  const double ks = __builtin_fma(z * x, __builtin_fma(z, rs, S1), x);
+  // __kernel_cos: w + (((1 - w) - z/2) + z r), w = 1 - z/2
+  const double rc =
+      z * __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, C6, C5), C4), C3), C2), C1);
+  const double hz = 0.5 * z;
+  const double w = 1.0 - hz;
+  const double kc = w + (((1.0 - w) - hz) + z * rc);
+  // cos(q pi/2 + x), sin(q pi/2 + x) for q mod 4 = 0, 1, 2, 3
+  const double c0 = (iq & 1) ? ks : kc, s0 = (iq & 1) ? kc : ks;
+  cs = (iq == 1 || iq == 2) ? -c0 : c0;
+  sn = (iq >= 2) ? -s0 : s0;
+}
+
+// the radius and angle uniform of pair block A
+__device__ __forceinline__ double v_radius(const u4& x) {
   const uint64_t a = (((uint64_t)x.y << 32) | x.x) >> 11;
   const double u1 = (double)(a + 1) * TWO_M53;
-  const double u2 = (double)x.z * TWO_M32;
-  Draw d;
-  d.z = sqrt(-2.0 * det_log(u1)) * det_cos2pi(u2);
-  d.ut = (double)x.w * TWO_M32;
-  d.dbit = x.x & 1u;
-  return d;
+  return sqrt(-2.0 * v_log(u1));
 }
 
-__device__ __forceinline__ Draw draw_s(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot,
-                                      uint64_t tick) {
-  return draw_from(block(seed, env, asset, slot, tick));
-}
-
-__device__ __forceinline__ Draw draw0(uint64_t seed, uint64_t env, uint32_t asset, uint64_t tick) {
+// the variate of draw index d (v3 above); zc / ztag: the lane's cached odd
+// half (ztag = P + 1 when zc holds pair P's r sin(2 pi u2))
+__device__ __forceinline__ Draw draw_d(uint64_t seed, uint64_t env, uint32_t asset, uint64_t d, double& zc,
+                                       uint64_t& ztag) {
+  const uint64_t P = d >> 1;
+  Draw r;
 #ifdef MGN_ABL_DRAW  // diagnostic timing build: a cheap stand-in for the variate (wrong values)
-  const uint32_t h = ((uint32_t)tick * 0x9E3779B1u) ^ ((uint32_t)env * 0x85EBCA6Bu) ^ (asset * 0xC2B2AE35u);
-  Draw d;
-  d.z = (double)(int32_t)(h & 0xffffu) * (1.0 / 32768.0) - 1.0;
-  d.ut = (double)(h >> 16) * (1.0 / 65536.0);
-  d.dbit = h & 1u;
-  return d;
+  const uint32_t h = ((uint32_t)d * 0x9E3779B1u) ^ ((uint32_t)env * 0x85EBCA6Bu) ^ (asset * 0xC2B2AE35u);
+  r.z = (double)(int32_t)(h & 0xffffu) * (1.0 / 32768.0) - 1.0;
+  r.ut = (double)(h >> 16) * (1.0 / 65536.0);
+  r.dbit = h & 1u;
+  (void)P;
+  (void)zc;
+  (void)ztag;
+  return r;
 #else
-  return draw_s(seed, env, asset, 0, tick);
+  if (d & 1) {
+    if (ztag != P + 1) {  // the pair's transform did not run here (first tick, or out of step)
+      const u4 x = block(seed, env, asset, 0, P);
+      double sn, cs;
+      v_sincos2pi((double)x.z * TWO_M32, sn, cs);
+      zc = v_radius(x) * sn;
+    }
+    const u4 y = block(seed, env, asset, 3, P);
+    r.z = zc;
+    r.ut = (double)y.w * TWO_M32;
+    r.dbit = y.x & 1u;
+  } else {
+    const u4 x = block(seed, env, asset, 0, P);
+    double sn, cs;
+    v_sincos2pi((double)x.z * TWO_M32, sn, cs);
+    const double rad = v_radius(x);
+    r.z = rad * cs;
+    zc = rad * sn;
+    ztag = P + 1;
+    r.ut = (double)x.w * TWO_M32;
+    r.dbit = x.x & 1u;
+  }
+  return r;
 #endif
+}
+
+// the normal variate alone of a full block (the per-tick blocks: OUPair's
+// mean walk, SineAdder's components, SineDynamic's noise): r cos(2 pi u2)
+__device__ __forceinline__ double normal_of(const u4& x) {
+  double sn, cs;
+  v_sincos2pi((double)x.z * TWO_M32, sn, cs);
+  return v_radius(x) * cs;
 }
 
 // std::modf's fractional part: x - trunc(x) is exact; its sign follows x (modf(-3.0) = -0.0)

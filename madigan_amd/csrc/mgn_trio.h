@@ -266,6 +266,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
       for (int i = 0; i < NQ; ++i) qr[i] = q[i];
     }
     ts = p.ts[envc];
+    s.dskip = p.dskip[envc];
     if (RP) s.rcur = p.rcur[envc];
   } else if (role == 1) {
     if (s.valid[0]) {
@@ -335,6 +336,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     p.seed = in_vgpr(p.seed);
     p.env_offset = in_vgpr(p.env_offset);
     drain_vmem();
+    MGN_IT(54, 0);
     int k = 0;
     // the source state before the last speculative tick (restored when F
     // finds that the previous step ended the episode)
@@ -379,7 +381,10 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
           p.tfl[i] = s.tfl[0];
         }
       }
-      if (ls == 0) p.ts[env] = ts;
+      if (ls == 0) {
+        p.ts[env] = ts;
+        p.dskip[env] = s.dskip;
+      }
     };
     for (int j = 0;; ++j) {
       const int cur = j & 1, prv = cur ^ 1;
@@ -398,6 +403,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
           // was not speculated (none ran in the previous iteration) it reads the next
           if (prev_step) k -= 1;
           else tick();
+          s.dskip += 1;  // Env::reset counts (the draw index; no draws from a tape)
           if (WIN) gpend = p.W - 1;
         } else if (rst) {
           if (prev_step) {  // roll the speculative tick back
@@ -495,6 +501,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     // orders, lp with the prices; `fresh` = recompute all four (start, reset)
     Sums sa = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
     drain_vmem();
+    MGN_IT(51, TRIO_W);
     int k = 0;
     int lpend = 0;  // WIN: refill ticks still to come after the reset tick
     // the ledger write-back at exit
@@ -588,7 +595,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
 #else
         if (in_kind != IN_NONE) {
 #endif
+          if (j == 0) MGN_IT(52, TRIO_W);
           broker_spec<S, RQ1, true>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, after, any_mc);
+          if (j == 0) MGN_IT(53, TRIO_W);
         }
         sa = after;
         // BrokerResponse of step k (overwritten if rolled back)

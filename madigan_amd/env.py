@@ -244,6 +244,8 @@ class BatchedEnv:
         self.trend_flags = self._t(v.trend_flags, u8, NA)
         self.cash = self._t(v.cash, f64, (N,))
         self.timestamp = self._t(v.timestamp, i64, (N,))
+        # resets so far: the variates' draw index is timestamp + draw_skip (DESIGN, variates v3)
+        self.draw_skip = self._t(v.draw_skip, i64, (N,))
         self.shaper_a = self._t(v.shaper_a, f64, Dsh)
         self.shaper_b = self._t(v.shaper_b, f64, Dsh)
         self.ep_stats = self._t(v.ep_stats, f64, (N, 2))

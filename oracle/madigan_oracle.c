@@ -125,19 +125,62 @@ static double k_cos(double x, double y) {
   return w + (((1.0 - w) - hz) + (z * r - x * y));
 }
 
-/* cos(2*pi*u), u in [0,1): exact octant reduction t=4u, q=rint(t). */
-double orc_cos2pi(double u) {
+/* The variates' math (specification v3, the device's mgn_math.h v_log /
+ * v_sincos2pi): fdlibm's log and __kernel_sin / __kernel_cos with their
+ * polynomials in fused multiply-add Horner form.  C99 fma() is correctly
+ * rounded, as the device's v_fma_f64, so every bit is reproduced. */
+double orc_vlog(double x) {
+  const double ln2_hi = from_bits(0x3fe62e42fee00000ull);
+  const double ln2_lo = from_bits(0x3dea39ef35793c76ull);
+  const double Lg1 = from_bits(0x3FE5555555555593ull), Lg2 = from_bits(0x3FD999999997FA04ull),
+               Lg3 = from_bits(0x3FD2492494229359ull), Lg4 = from_bits(0x3FCC71C51D8E78AFull),
+               Lg5 = from_bits(0x3FC7466496CB03DEull), Lg6 = from_bits(0x3FC39A09D078C69Full),
+               Lg7 = from_bits(0x3FC2F112DF3E5244ull);
+  uint64_t ix = to_bits(x);
+  int32_t hx = (int32_t)(ix >> 32);
+  int32_t k = ((hx >> 20) & 0x7ff) - 1023;
+  hx &= 0x000fffff;
+  int32_t i = (hx + 0x95f64) & 0x100000;
+  k += (i >> 20);
+  uint64_t mb = ((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (ix & 0xffffffffull);
+  double f = from_bits(mb) - 1.0;
+  double s = f / (2.0 + f);
+  double dk = (double)k;
+  double z = s * s;
+  double w = z * z;
+  double t1 = w * fma(w, fma(w, Lg6, Lg4), Lg2);
+  double t2 = z * fma(w, fma(w, fma(w, Lg7, Lg5), Lg3), Lg1);
+  double R = t2 + t1;
+  double hfsq = 0.5 * f * f;
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
+/* cos(2 pi u) and sin(2 pi u), u in [0,1): t = 4u, q = floor(t + 1/2),
+ * x = (t - q) pi/2 (|x| <= pi/4), the kernels placed by the quadrant q mod 4 */
+void orc_vsincos2pi(double u, double *sn, double *cs) {
+  const double S1 = from_bits(0xBFC5555555555549ull), S2 = from_bits(0x3F8111111110F8A6ull),
+               S3 = from_bits(0xBF2A01A019C161D5ull), S4 = from_bits(0x3EC71DE357B1FE7Dull),
+               S5 = from_bits(0xBE5AE5E68A2B9CEBull), S6 = from_bits(0x3DE5D93A5ACFD57Cull);
+  const double C1 = from_bits(0x3FA555555555554Cull), C2 = from_bits(0xBF56C16C16C15177ull),
+               C3 = from_bits(0x3EFA01A019CB1590ull), C4 = from_bits(0xBE927E4F809C52ADull),
+               C5 = from_bits(0x3E21EE9EBDB4B1C4ull), C6 = from_bits(0xBDA8FAE9BE8838D4ull);
   const double pio2 = from_bits(0x3FF921FB54442D18ull);
   double t = 4.0 * u;
   double q = floor(t + 0.5);
-  double f = t - q;           /* exact, |f| <= 0.5 */
-  double r = f * pio2;        /* |r| <= pi/4 */
+  double x = (t - q) * pio2;
   int iq = ((int)q) & 3;
+  double z = x * x;
+  double rs = fma(z, fma(z, fma(z, fma(z, S6, S5), S4), S3), S2);
+  double ks = fma(z * x, fma(z, rs, S1), x);               /* __kernel_sin, y = 0 */
+  double rc = z * fma(z, fma(z, fma(z, fma(z, fma(z, C6, C5), C4), C3), C2), C1);
+  double hz = 0.5 * z;
+  double w = 1.0 - hz;
+  double kc = w + (((1.0 - w) - hz) + z * rc);            /* __kernel_cos, y = 0 */
   switch (iq) {
-    case 0: return k_cos(r, 0.0);
-    case 1: return -k_sin(r, 0.0, 0);
-    case 2: return -k_cos(r, 0.0);
-    default: return k_sin(r, 0.0, 0);
+    case 0: *cs = kc; *sn = ks; break;
+    case 1: *cs = -ks; *sn = kc; break;
+    case 2: *cs = -kc; *sn = -ks; break;
+    default: *cs = ks; *sn = -kc; break;
   }
 }
 
@@ -183,40 +226,56 @@ double orc_sin(double x) {
 
 static const double TWO_M32 = 2.3283064365386962890625e-10; /* 2^-32 */
 
-/* Variates of one (env, asset, tick) from its slot-0 Philox block x0..x3:
- *   u1 = ((x1:x0 >> 11) + 1) 2^-53 in (0,1],  u2 = x2 2^-32 in [0,1)
- *   z  = sqrt(-2 log u1) cos(2 pi u2)           (Box-Muller)
- *   ut = x3 2^-32                                (TrendOU regime-switch uniform)
- *   dbit = x0 & 1                                (TrendOU direction; u1 drops it) */
-void orc_draw0(uint64_t seed, uint64_t env, uint32_t asset, uint64_t tick, double *z, double *ut,
-               uint32_t *dbit) {
-  uint32_t ctr[4] = {(uint32_t)tick, (uint32_t)env, asset,
-                     (uint32_t)(tick >> 32) ^ (uint32_t)(env >> 32)};
+/* the raw Philox block of counter slot `slot` at counter value c */
+static void block_at(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot, uint64_t c,
+                     uint32_t x[4]) {
+  uint32_t ctr[4] = {(uint32_t)c, (uint32_t)env, asset | (slot << 16),
+                     (uint32_t)(c >> 32) ^ (uint32_t)(env >> 32)};
   uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-  uint32_t x[4];
   orc_philox4x32_10(ctr, key, x);
-  uint64_t a = (((uint64_t)x[1] << 32) | x[0]) >> 11;
-  double u1 = (double)(a + 1) * TWO_M53;
-  double u2 = (double)x[2] * TWO_M32;
-  *z = sqrt(-2.0 * orc_log(u1)) * orc_cos2pi(u2);
-  *ut = (double)x[3] * TWO_M32;
-  *dbit = x[0] & 1u;
 }
 
-/* the same variates from the block of counter slot `slot` (orc_draw0 = slot 0) */
-static void draw_slot(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot, uint64_t tick,
-                      double *z, double *ut, uint32_t *dbit) {
-  uint32_t ctr[4] = {(uint32_t)tick, (uint32_t)env, asset | (slot << 16),
-                     (uint32_t)(tick >> 32) ^ (uint32_t)(env >> 32)};
-  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-  uint32_t x[4];
-  orc_philox4x32_10(ctr, key, x);
+/* Box-Muller radius sqrt(-2 log u1), u1 = ((x1:x0 >> 11) + 1) 2^-53 */
+static double radius_of(const uint32_t x[4]) {
   uint64_t a = (((uint64_t)x[1] << 32) | x[0]) >> 11;
   double u1 = (double)(a + 1) * TWO_M53;
-  double u2 = (double)x[2] * TWO_M32;
-  *z = sqrt(-2.0 * orc_log(u1)) * orc_cos2pi(u2);
-  *ut = (double)x[3] * TWO_M32;
-  *dbit = x[0] & 1u;
+  return sqrt(-2.0 * orc_vlog(u1));
+}
+
+/* Variates of draw index d (specification v3; d = timestamp + resets of the
+ * env).  Ticks pair up: P = d >> 1, block A = slot 0 at counter P:
+ *   u2 = xA2 2^-32, r = radius_of(A)
+ *   d even: z = r cos(2 pi u2), ut = xA3 2^-32, dbit = xA0 & 1
+ *   d odd:  z = r sin(2 pi u2), ut = xB3 2^-32, dbit = xB0 & 1, block B = slot 3 at P
+ * (z: the normal variate, ut: the TrendOU regime-switch uniform, dbit: the
+ * trend direction) */
+void orc_draw0(uint64_t seed, uint64_t env, uint32_t asset, uint64_t d, double *z, double *ut,
+               uint32_t *dbit) {
+  uint32_t x[4];
+  const uint64_t P = d >> 1;
+  block_at(seed, env, asset, 0, P, x);
+  double sn, cs;
+  orc_vsincos2pi((double)x[2] * TWO_M32, &sn, &cs);
+  const double r = radius_of(x);
+  if ((d & 1) == 0) {
+    *z = r * cs;
+    *ut = (double)x[3] * TWO_M32;
+    *dbit = x[0] & 1u;
+  } else {
+    uint32_t y[4];
+    block_at(seed, env, asset, 3, P, y);
+    *z = r * sn;
+    *ut = (double)y[3] * TWO_M32;
+    *dbit = y[0] & 1u;
+  }
+}
+
+/* the normal variate of a full block (per-tick blocks: OUPair's mean walk,
+ * SineAdder's components, SineDynamic's noise): r cos(2 pi u2) */
+static double normal_of(const uint32_t x[4]) {
+  double sn, cs;
+  orc_vsincos2pi((double)x[2] * TWO_M32, &sn, &cs);
+  return radius_of(x) * cs;
 }
 
 /* fdlibm e_asin.c (Sun Microsystems) on |x| <= 1, plain binary64 */
@@ -298,6 +357,7 @@ typedef struct {
   uint8_t trending[MAXA];
   int8_t dir[MAXA];
   uint64_t ts;
+  uint64_t dskip;  /* resets so far: the variates' draw index is ts + dskip (v3) */
   /* HDFSourceSingle (DataSource.h:136-148): currentData_, currentIdx_,
    * currentCacheIdx_, currentCacheSize_, first file row of the cache */
   double feat[MAXA];
@@ -498,15 +558,6 @@ static const double *state_price(const orc_batch *b, const orc_env *s) {
   return b->replay ? s->feat : s->P;
 }
 
-/* the raw Philox block of counter slot `slot` */
-static void block_slot(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot, uint64_t tick,
-                       uint32_t x[4]) {
-  uint32_t ctr[4] = {(uint32_t)tick, (uint32_t)env, asset | (slot << 16),
-                     (uint32_t)(tick >> 32) ^ (uint32_t)(env >> 32)};
-  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-  orc_philox4x32_10(ctr, key, x);
-}
-
 /* WaveTableOsc<double> of setSineOsc (WaveTableOsc.h:104-174): every table of
  * the oscillator holds the same len samples sin(i*2*pi/len) (scale stays 1),
  * with sample len = sample 0; the interpolated read of getOutput (:84-95)
@@ -551,19 +602,12 @@ static void sd_sample(const double *p, double *ax, uint64_t seed, uint64_t env, 
   for (int c = 0; c < C; ++c) {
     const double *r = p + 3 + C + 9 * c;
     uint32_t x[4];
-    block_slot(seed, env, asset, 16u + (uint32_t)c, tick, x);
+    block_at(seed, env, asset, 16u + (uint32_t)c, tick, x);
     ax[4 * c + 1] = (r[1] - r[0]) * ((double)x[0] * TWO_M32) + r[0];
     ax[4 * c + 2] = (r[4] - r[3]) * ((double)x[1] * TWO_M32) + r[3];
     ax[4 * c + 3] = (r[7] - r[6]) * ((double)x[2] * TWO_M32) + r[6];
   }
 }
-static double normal_of(const uint32_t x[4]) {
-  uint64_t a = (((uint64_t)x[1] << 32) | x[0]) >> 11;
-  double u1 = (double)(a + 1) * TWO_M53;
-  double u2 = (double)x[2] * TWO_M32;
-  return sqrt(-2.0 * orc_log(u1)) * orc_cos2pi(u2);
-}
-
 static void src_get_data(orc_batch *b, int e) {
   orc_env *s = &b->envs[e];
   if (b->replay) {
@@ -572,7 +616,7 @@ static void src_get_data(orc_batch *b, int e) {
   }
   uint64_t genv = (uint64_t)(b->cfg.env_offset + e);
   uint64_t seed = b->cfg.seed;
-  uint64_t tick = s->ts;
+  uint64_t tick = s->ts + s->dskip;  /* the draw index (variates v3) */
   for (int i = 0; i < b->A; ++i) {
     const double *p = b->src[i].p;
     switch (b->src[i].kind) {
@@ -709,9 +753,9 @@ static void src_get_data(orc_batch *b, int e) {
                                 keyed by the pair's first asset, counter slot 2) */
         if (p[3] == 0.0) {
           const uint32_t a0 = (uint32_t)i;
-          double zm, um;
-          uint32_t bm;
-          draw_slot(seed, genv, a0, 2, tick, &zm, &um, &bm);
+          uint32_t xm[4];
+          block_at(seed, genv, a0, 2, tick, xm);
+          const double zm = normal_of(xm);
           double mean = s->ouMean[i];
           mean += mean * (zm * p[2] + 0.0);
           for (int j = 0; j < 2; ++j) {
@@ -733,10 +777,9 @@ static void src_get_data(orc_batch *b, int e) {
         for (int c = 0; c < C; ++c) {
           double nz = 0.0;  /* component c's noise: the block of counter slot c */
           if (p[2] != 0.0) {
-            double z, u;
-            uint32_t bb;
-            draw_slot(seed, genv, (uint32_t)i, (uint32_t)c, tick, &z, &u, &bb);
-            nz = z * p[2] + 0.0;
+            uint32_t xc[4];
+            block_at(seed, genv, (uint32_t)i, (uint32_t)c, tick, xc);
+            nz = normal_of(xc) * p[2] + 0.0;
           }
           sum += (nz + p[3 + C + c]) + p[3 + 2 * C + c] * orc_sin(PI2 * ax[c] * p[3 + c]);
           ax[c] += p[1];
@@ -750,7 +793,7 @@ static void src_get_data(orc_batch *b, int e) {
         const int C = (int)p[0];
         const int trend = b->src[i].kind == ORC_SRC_SINEDYNTREND;
         uint32_t x0[4];
-        block_slot(seed, genv, (uint32_t)i, 0, tick, x0);
+        block_at(seed, genv, (uint32_t)i, 0, tick, x0);
         sd_update(p, ax, x0[3]);
         double tc = ax[16];
         double sum = 0.;
@@ -778,7 +821,7 @@ static void src_get_data(orc_batch *b, int e) {
             st[2] -= 1.;
             if (st[2] == 0.) st[0] = 0.;
           } else {
-            if (!have1) { block_slot(seed, genv, (uint32_t)i, 1, tick, x1); have1 = 1; }
+            if (!have1) { block_at(seed, genv, (uint32_t)i, 1, tick, x1); have1 = 1; }
             double u = (double)x1[t] * TWO_M32;
             if (u < q[3]) {
               st[0] = 1.;
@@ -807,6 +850,7 @@ static void src_get_data(orc_batch *b, int e) {
  * TrendOU restores start (DataSource.cpp:1495-1502). */
 static void src_reset(orc_batch *b, int e) {
   orc_env *s = &b->envs[e];
+  s->dskip += 1;  /* every Env::reset skips one draw index (variates v3) */
   for (int i = 0; i < b->A; ++i) {
     const double *p = b->src[i].p;
     switch (b->src[i].kind) {
@@ -827,7 +871,7 @@ static void src_reset(orc_batch *b, int e) {
         break;
       case ORC_SRC_SINEDYNAMIC: case ORC_SRC_SINEDYNTREND:  /* :794-800, :994-1000 */
         sd_sample(p, b->aux + ((size_t)e * b->A + i) * ORC_AUX_WIDTH, b->cfg.seed,
-                  (uint64_t)(b->cfg.env_offset + e), (uint32_t)i, s->ts);
+                  (uint64_t)(b->cfg.env_offset + e), (uint32_t)i, s->ts + s->dskip);
         break;
       default: break;           /* Synth family, SineAdder, OU, Gaussian: no-op */
     }
@@ -874,6 +918,7 @@ static void src_init(orc_batch *b, int e) {
     }
   }
   s->ts = 0;
+  s->dskip = 0;
 }
 
 /* Env::initAccountants -- Env.h:150-165: fresh Broker/Portfolio, one getData */
@@ -1484,6 +1529,7 @@ void orc_get_scalar(const orc_batch *b, int which, double *out) {
       case ORC_S_LAST_LEN: v = s->last_len; break;
       case ORC_S_LAST_EQUITY: v = s->last_eq; break;
       case ORC_S_N_DONE: v = s->n_done; break;
+      case ORC_S_DSKIP: v = (double)s->dskip; break;
     }
     out[e] = v;
   }

@@ -183,7 +183,7 @@ enum { ORC_S_CASH = 0, ORC_S_EQUITY = 1, ORC_S_PNL = 2, ORC_S_BALANCE = 3,
        ORC_S_BORROWED_ASSET_VALUE = 7, ORC_S_ASSET_VALUE = 8, ORC_S_TIMESTAMP = 9,
        ORC_S_CHECK_RISK = 10, ORC_S_SHAPER_A = 11, ORC_S_SHAPER_B = 12,
        ORC_S_EP_RET = 13, ORC_S_EP_LEN = 14, ORC_S_LAST_RET = 15, ORC_S_LAST_LEN = 16,
-       ORC_S_LAST_EQUITY = 17, ORC_S_N_DONE = 18 };
+       ORC_S_LAST_EQUITY = 17, ORC_S_N_DONE = 18, ORC_S_DSKIP = 19 };
 void orc_get_scalar(const orc_batch *b, int which, double *out); /* (N) */
 void orc_set_cash(orc_batch *b, const double *cash);
 
@@ -226,10 +226,12 @@ void orc_naive(int shaper, const double *rewards, int L, int D, const double *di
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 double orc_log(double x);
 double orc_sin(double x);
-double orc_cos2pi(double u);
 double orc_asin(double x);
-double orc_normal(uint64_t seed, uint64_t env, uint32_t asset, uint64_t tick);
-void orc_draw0(uint64_t seed, uint64_t env, uint32_t asset, uint64_t tick, double *z, double *ut,
+/* the variates (specification v3, mgn_math.h): d = draw index */
+double orc_vlog(double x);
+void orc_vsincos2pi(double u, double *sn, double *cs);
+double orc_normal(uint64_t seed, uint64_t env, uint32_t asset, uint64_t d);
+void orc_draw0(uint64_t seed, uint64_t env, uint32_t asset, uint64_t d, double *z, double *ut,
                uint32_t *dbit);
 void orc_uniform2(uint64_t seed, uint64_t env, uint32_t asset, uint32_t slot, uint64_t tick,
                   double *u0, double *u1);

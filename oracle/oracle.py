@@ -35,7 +35,7 @@ F_LEDGER, F_MEP, F_BORROWED, F_PRICE, F_SINE_X, F_OU_MEAN, F_DY, F_TLEN, F_TREND
     F_SHAPER_A, F_SHAPER_B = range(12)
 S_NAMES = ["cash", "equity", "pnl", "balance", "availableMargin", "usedMargin", "borrowedMargin",
            "borrowedAssetValue", "assetValue", "timestamp", "checkRisk", "shaperA", "shaperB",
-           "ep_ret", "ep_len", "last_ret", "last_len", "last_equity", "n_done"]
+           "ep_ret", "ep_len", "last_ret", "last_len", "last_equity", "n_done", "draw_skip"]
 
 
 class AssetSrc(C.Structure):
@@ -112,9 +112,10 @@ def lib(fast: bool = False):
         L.orc_ppc.argtypes = [P, P, C.c_int, C.c_int, C.c_int, P, C.c_double, P, P]
         L.orc_naive.argtypes = [C.c_int, P, C.c_int, C.c_int, P, C.c_double, P]
         L.orc_philox4x32_10.argtypes = [P, P, P]
-        for fn in (L.orc_log, L.orc_sin, L.orc_cos2pi, L.orc_asin):
+        for fn in (L.orc_log, L.orc_sin, L.orc_asin, L.orc_vlog):
             fn.argtypes = [C.c_double]
             fn.restype = C.c_double
+        L.orc_vsincos2pi.argtypes = [C.c_double, P, P]
         L.orc_normal.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64]
         L.orc_draw0.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, P, P, P]
         L.orc_normal.restype = C.c_double

@@ -35,23 +35,68 @@ def test_fdlibm_accuracy_vs_libm():
         assert abs(L.orc_log(x) - math.log(x)) <= 2 * np.spacing(abs(math.log(x)))
     for x in np.concatenate([rng.uniform(-1e5, 1e5, 5000), np.arange(1, 200) * math.pi]):
         assert abs(L.orc_sin(x) - math.sin(x)) <= 2e-16 + 2 * np.spacing(abs(math.sin(x)))
+    # the variates' fma-form kernels (specification v3)
+    sn, cs = C.c_double(), C.c_double()
     for u in rng.uniform(0, 1, 5000):
-        assert abs(L.orc_cos2pi(u) - math.cos(2 * math.pi * u)) < 1e-15
+        L.orc_vsincos2pi(u, C.byref(sn), C.byref(cs))
+        assert abs(cs.value - math.cos(2 * math.pi * u)) < 1e-15
+        assert abs(sn.value - math.sin(2 * math.pi * u)) < 1e-15
+    for x in rng.uniform(1e-300, 1.0, 5000):
+        assert abs(L.orc_vlog(x) - math.log(x)) <= 2 * np.spacing(abs(math.log(x)))
+
+
+def _draws(n, d_of):
+    L = O.lib()
+    z, ut = np.zeros(n), np.zeros(n)
+    bit = np.zeros(n, np.uint32)
+    zz, uu, bb = C.c_double(), C.c_double(), C.c_uint32()
+    for i in range(n):
+        env, asset, d = d_of(i)
+        L.orc_draw0(11, env, asset, d, C.byref(zz), C.byref(uu), C.byref(bb))
+        z[i], ut[i], bit[i] = zz.value, uu.value, bb.value
+    return z, ut, bit
 
 
 def test_variates_moments():
-    L = O.lib()
-    z, ut = np.zeros(200_000), np.zeros(200_000)
-    bit = np.zeros(200_000, np.uint32)
-    zz, uu, bb = C.c_double(), C.c_double(), C.c_uint32()
-    for i in range(200_000):
-        L.orc_draw0(11, i % 1000, i // 1000 % 8, i // 8000, C.byref(zz), C.byref(uu), C.byref(bb))
-        z[i], ut[i], bit[i] = zz.value, uu.value, bb.value
+    """Specification v3: the even and odd draw index of a pair are the
+    Box-Muller pair (r cos, r sin) of one block, each with its own switch
+    uniform and direction bit."""
+    z, ut, bit = _draws(200_000, lambda i: (i % 1000, i // 1000 % 8, i // 8000))
     assert abs(z.mean()) < 0.01 and abs(z.std() - 1) < 0.01
     assert abs(np.mean(z ** 4) - 3) < 0.1        # normal kurtosis
     assert abs(ut.mean() - 0.5) < 0.005 and ut.min() >= 0 and ut.max() < 1
     assert abs(bit.mean() - 0.5) < 0.01
-    assert abs(np.corrcoef(z[:-1], z[1:])[0, 1]) < 0.01
+    # consecutive draw indices of one (env, asset): both halves of every pair
+    zs, us, bs = _draws(200_000, lambda i: (i // 500, 3, i % 500))
+    e, o = zs[0::2], zs[1::2]                    # (even, odd) halves of each pair
+    for x in (e, o):
+        assert abs(x.mean()) < 0.01 and abs(x.std() - 1) < 0.01
+    assert abs(np.corrcoef(e, o)[0, 1]) < 0.01   # the Box-Muller pair is independent
+    assert abs(np.corrcoef(e ** 2, o ** 2)[0, 1]) < 0.01
+    assert abs(np.corrcoef(zs[1:-1:2], zs[2::2])[0, 1]) < 0.01  # across pairs
+    assert abs(np.corrcoef(us[0::2], us[1::2])[0, 1]) < 0.01    # the halves' switch uniforms
+    assert abs(np.corrcoef(us[1::2], np.abs(o))[0, 1]) < 0.01   # odd uniform vs the odd normal
+    assert abs(bs[1::2].mean() - 0.5) < 0.01
+
+
+def test_variates_pair_definition():
+    """The pair's halves are r cos(2 pi u2) and r sin(2 pi u2) of block A at
+    counter d >> 1 (restated here from the Philox block in Python)."""
+    L = O.lib()
+    zz, uu, bb = C.c_double(), C.c_double(), C.c_uint32()
+    sn, cs = C.c_double(), C.c_double()
+    seed, env, asset = 0x1234_5678_9ABC, 77, 5
+    for P in (0, 1, 12345, 2 ** 33 + 7):
+        x = O.philox([P & 0xFFFFFFFF, env, asset, (P >> 32) ^ 0], [seed & 0xFFFFFFFF, seed >> 32])
+        a = ((int(x[1]) << 32) | int(x[0])) >> 11
+        r = math.sqrt(-2.0 * L.orc_vlog((a + 1) * 2.0 ** -53))
+        L.orc_vsincos2pi(int(x[2]) * 2.0 ** -32, C.byref(sn), C.byref(cs))
+        L.orc_draw0(seed, env, asset, 2 * P, C.byref(zz), C.byref(uu), C.byref(bb))
+        assert zz.value == r * cs.value and uu.value == int(x[3]) * 2.0 ** -32 and bb.value == x[0] & 1
+        L.orc_draw0(seed, env, asset, 2 * P + 1, C.byref(zz), C.byref(uu), C.byref(bb))
+        y = O.philox([P & 0xFFFFFFFF, env, asset | (3 << 16), (P >> 32) ^ 0],
+                     [seed & 0xFFFFFFFF, seed >> 32])
+        assert zz.value == r * sn.value and uu.value == int(y[3]) * 2.0 ** -32 and bb.value == y[0] & 1
 
 
 def test_ou_stationary_moments():

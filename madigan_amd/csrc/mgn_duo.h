@@ -637,6 +637,9 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
     insuff = (own.need_insuff != 0) & ((availM <= own.aPX) | (balance <= 0.));
     go = act & !mc & !insuff;
     const uint32_t bad = (uint32_t)seg_or<S>((go != (int)((go_bits >> ls) & 1)) ? (1 << ls) : 0);
+#ifdef MGN_STAMPS
+    if (threadIdx.x == DUO_HALF) s_duo_sub[6] += 1;  // passes of the wave
+#endif
     if (bad == 0) break;
     const int i0 = __builtin_ctz(bad);
     const uint32_t go_now = (uint32_t)seg_or<S>(go << ls);
@@ -684,6 +687,7 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
     s_duo_sub[0] += t_b - t_a;
     s_duo_sub[1] += t_c - t_b;
     s_duo_sub[2] += t_d - t_c;
+    s_duo_sub[5] += 1;  // broker calls
   }
 #endif
 }

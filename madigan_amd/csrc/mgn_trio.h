@@ -655,6 +655,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
       atomicAdd(&g_duo_stamps[4], acc0);
       atomicAdd(&g_duo_stamps[5], acc1);
       for (int i = 0; i < 3; ++i) atomicAdd(&g_duo_stamps[13 + i], s_duo_sub[i]);
+      atomicAdd(&g_duo_stamps[18], s_duo_sub[5]);
+      atomicAdd(&g_duo_stamps[19], s_duo_sub[6]);
     }
 #endif
 #ifdef MGN_TRIO_ABL_EPI  // diagnostic timing build: no state write-back

@@ -504,6 +504,18 @@ __device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s,
 #ifndef MGN_DUO_VAR
 #define MGN_DUO_VAR 0
 #endif
+// broker_spec's cash chain walked by one lane per env (published to LDS)
+// instead of by every lane of the env (each reading every record)
+#ifndef MGN_SPEC_CH1
+#define MGN_SPEC_CH1 1
+#endif
+// broker_spec: only the lanes whose check reads the sums (and the last lane)
+// walk the canonical tree (measured 6 % slower per step at C3: the branch
+// around the tree keeps its LDS reads from overlapping the cash chain;
+// profiles/r04_ab_tree_skip.txt)
+#ifndef MGN_SPEC_TREE_SKIP
+#define MGN_SPEC_TREE_SKIP 0
+#endif
 
 // Broker::handleTransaction(units) for a segment of S lanes, one asset per
 // lane, resolved speculatively.  The serial dependency between orders (each
@@ -572,6 +584,16 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
 #endif
   const OrderRec& own = er.r[ls];
   const int act = uc[0] != 0. ? 1 : 0;
+  // the lanes whose risk check reads the sums before their order (an order
+  // that is checked at all: Portfolio.cpp:257-265 leaves an opposite-side
+  // order with u <= -cur unchecked), and the last lane, whose tree also
+  // yields the sums after every order: the others skip the tree's LDS reads
+  // (their lanes idle in its instructions)
+#if MGN_SPEC_TREE_SKIP
+  const bool need_tree = (act && (own.need_mc || own.need_insuff)) || ls == S - 1;
+#else
+  const bool need_tree = true;
+#endif
   const uint32_t act_bits = (uint32_t)seg_or<S>(act << ls);
   uint32_t go_bits = act_bits;  // the guess
   const double cash0 = cash;
@@ -585,32 +607,18 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
   Q4 sib[6];
   double lv[4][STREAM ? 1 : S];
   for (int it = 0; it <= S; ++it) {
-    // cash before this lane's order, and after the last order, under the guess
-    double c = cash0, c_own = cash0;
-#pragma unroll
-    for (int i = 0; i < S; ++i) {
-      // the three-role kernel at S = 16: records read four at a time (a
-      // scheduling fence per group, as tree4's FENCE)
-      if constexpr (LOWREG && S >= 16) {
-        if (i > 0 && i % 4 == 0) __builtin_amdgcn_sched_barrier(0);
-      }
-      if (i == ls) c_own = c;
-      const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
-      const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
-      const double ci = ((c + xz.y) - yz.x) - yz.y;
-      c = ((go_bits >> i) & 1) ? ci : c;
-    }
-    cend = c;
     // canonical sums before this lane's order: leaves of executed earlier
     // orders after the order, the others before
-    double r0, r1, r2, r3;
+    double r0 = 0., r1 = 0., r2 = 0., r3 = 0.;
     if constexpr (STREAM) {
-      const Q4 rt = tree4<S, 0, S, true, LOWREG && S >= 16>(er, go_bits & ((1u << ls) - 1u), sib);
-      r0 = rt.a;
-      r1 = rt.b;
-      r2 = rt.c;
-      r3 = rt.d;
-    } else {
+      if (need_tree) {
+        const Q4 rt = tree4<S, 0, S, true, LOWREG && S >= 16>(er, go_bits & ((1u << ls) - 1u), sib);
+        r0 = rt.a;
+        r1 = rt.b;
+        r2 = rt.c;
+        r3 = rt.d;
+      }
+    } else if (need_tree) {
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         const bool post = (j < ls) && ((go_bits >> j) & 1);
@@ -626,6 +634,48 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
       r2 = tree<S>(lv[2]);
       r3 = tree<S>(lv[3]);
     }
+    // cash before this lane's order, and after the last order, under the guess
+    double c_own = cash0;
+#if MGN_SPEC_CH1
+    // the chain is the env's, not the lane's: its first lane walks it (its
+    // records' cash terms read by one lane of the env, not all of them) and
+    // publishes the cash before every order and after the last
+    if (ls == 0) {
+      double c = cash0;
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        er.cpre[i] = c;
+        const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
+        const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
+        const double ci = ((c + xz.y) - yz.x) - yz.y;
+        c = ((go_bits >> i) & 1) ? ci : c;
+      }
+      er.cpre[S] = c;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    c_own = er.cpre[ls];
+    cend = er.cpre[S];
+#else
+    {
+      double c = cash0;
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        // the three-role kernel at S = 16: records read four at a time (a
+        // scheduling fence per group, as tree4's FENCE)
+        if constexpr (LOWREG && S >= 16) {
+          if (i > 0 && i % 4 == 0) __builtin_amdgcn_sched_barrier(0);
+        }
+        if (i == ls) c_own = c;
+        const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
+        const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
+        const double ci = ((c + xz.y) - yz.x) - yz.y;
+        c = ((go_bits >> i) & 1) ? ci : c;
+      }
+      cend = c;
+    }
+#endif
     // Portfolio::checkRisk(i, u), Portfolio.cpp:254-279 (as XRounds)
     const double pnl = r0 - r1;
     const double balance = c_own + r2;

@@ -818,10 +818,17 @@ struct alignas(16) OrderRec {
   double Z;        // borrowed repaid / negative-borrow cleared, else +0.0
   uint32_t act, need_mc, need_insuff, pad;
 };
+// cpre: the speculative broker's cash chain (broker_spec, one lane per env):
+// the cash before each order, then after the last.  The stride of an env's
+// records is 4 (mod 8) dwords, so the segments of a wave start in distinct
+// groups of four LDS banks
 template <int APAD>
 struct alignas(16) EnvRecs {
+  static constexpr int kBaseDw = APAD * 28 + (APAD + 2) * 2;
+  static constexpr int kPadD = (((4 - kBaseDw) % 8 + 8) % 8) / 2;
   OrderRec r[APAD];
-  double pad[2];  // 16 B skew: the segments of a wave read distinct LDS banks
+  double cpre[APAD + 2];
+  double pad[kPadD > 0 ? kPadD : 4];
 };
 
 // heap-indexed canonical tree over APAD leaves: node K (1-based) spans

@@ -504,6 +504,11 @@ __device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s,
 #ifndef MGN_DUO_VAR
 #define MGN_DUO_VAR 0
 #endif
+// broker_spec's canonical trees over DPP in registers instead of every lane
+// reading every record's leaves from LDS
+#ifndef MGN_SPEC_DPP
+#define MGN_SPEC_DPP 1
+#endif
 // broker_spec's cash chain walked by one lane per env (published to LDS)
 // instead of by every lane of the env (each reading every record)
 #ifndef MGN_SPEC_CH1
@@ -569,6 +574,49 @@ __device__ __forceinline__ Q4 tree4(const EnvRecs<S>& er, uint32_t post, Q4 (&si
   }
 }
 
+// The canonical trees of broker_spec in registers (MGN_SPEC_DPP): every lane
+// holds its own order's four leaves before (pre) and after (post) the order;
+// the tree of lane ls's check has post leaves for the executed orders j < ls
+// and pre leaves elsewhere.  Level by level, a lane takes its sibling
+// subtree's two versions over DPP -- P (post leaves where executed) and Q
+// (all pre) -- and adds the one its check needs to its own path (the sibling
+// lies left: P, right: Q), while P and Q of the joined subtree are formed
+// for the next level (row_half_mirror / row_mirror reach the sibling half of
+// 8 / 16 lanes: its lanes all hold the same subtree values by then).  Each
+// node is the sum of the same two children as the heap tree's (IEEE addition
+// commutes), so the sums are bit-identical to the LDS form; the root of P is
+// the sums after every executed order.
+template <int S>
+__device__ __forceinline__ void dpp_tree4(const double (&pre)[4], const double (&post)[4], bool go_own, int ls,
+                                          double (&path)[4], double (&rootP)[4]) {
+  double nP[4], nQ[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    path[q] = pre[q];
+    nQ[q] = pre[q];
+    nP[q] = go_own ? post[q] : pre[q];
+  }
+  auto level = [&](auto sibP, auto sibQ, bool right) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const double sp = sibP(nP[q]), sq = sibQ(nQ[q]);
+      path[q] = path[q] + (right ? sp : sq);
+      nP[q] = nP[q] + sp;
+      nQ[q] = nQ[q] + sq;
+    }
+  };
+  if constexpr (S >= 2)
+    level([](double v) { return dpp_f64<0xB1>(v); }, [](double v) { return dpp_f64<0xB1>(v); }, (ls & 1) != 0);
+  if constexpr (S >= 4)
+    level([](double v) { return dpp_f64<0x4E>(v); }, [](double v) { return dpp_f64<0x4E>(v); }, (ls & 2) != 0);
+  if constexpr (S >= 8)
+    level([](double v) { return dpp_f64<0x141>(v); }, [](double v) { return dpp_f64<0x141>(v); }, (ls & 4) != 0);
+  if constexpr (S >= 16)
+    level([](double v) { return dpp_f64<0x140>(v); }, [](double v) { return dpp_f64<0x140>(v); }, (ls & 8) != 0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) rootP[q] = nP[q];
+}
+
 template <int S, bool RQ1, bool LOWREG>
 __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRecs<S>& er,
                                             double& cash, const double (&uc)[1], double (&tp)[1],
@@ -578,7 +626,8 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
 #ifdef MGN_STAMPS
   const unsigned long long t_a = __builtin_amdgcn_s_memtime();
 #endif
-  order_prep<1, S>(s, p, er, uc, ls, cu2, me2, bm3, tpr, tco);
+  double lf_pre[4], lf_post[4];  // MGN_SPEC_DPP: the own leaves, in registers
+  order_prep<1, S, !MGN_SPEC_DPP>(s, p, er, uc, ls, cu2, me2, bm3, tpr, tco, lf_pre, lf_post);
 #ifdef MGN_STAMPS
   const unsigned long long t_b = __builtin_amdgcn_s_memtime();
 #endif
@@ -592,7 +641,7 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
 #if MGN_SPEC_TREE_SKIP
   const bool need_tree = (act && (own.need_mc || own.need_insuff)) || ls == S - 1;
 #else
-  const bool need_tree = true;
+  constexpr bool need_tree = true;
 #endif
   const uint32_t act_bits = (uint32_t)seg_or<S>(act << ls);
   uint32_t go_bits = act_bits;  // the guess
@@ -604,12 +653,25 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
   // three-role kernel's 168-VGPR budget): the streaming tree, its
   // rightmost-path left children kept
   constexpr bool STREAM = LOWREG || S >= 16;
+#if !MGN_SPEC_DPP
   Q4 sib[6];
   double lv[4][STREAM ? 1 : S];
+#endif
+  double rootP[4];  // MGN_SPEC_DPP: the sums after the orders the pass took
   for (int it = 0; it <= S; ++it) {
     // canonical sums before this lane's order: leaves of executed earlier
     // orders after the order, the others before
     double r0 = 0., r1 = 0., r2 = 0., r3 = 0.;
+#if MGN_SPEC_DPP
+    {
+      double path[4];
+      dpp_tree4<S>(lf_pre, lf_post, ((go_bits >> ls) & 1) != 0, ls, path, rootP);
+      r0 = path[0];
+      r1 = path[1];
+      r2 = path[2];
+      r3 = path[3];
+    }
+#else
     if constexpr (STREAM) {
       if (need_tree) {
         const Q4 rt = tree4<S, 0, S, true, LOWREG && S >= 16>(er, go_bits & ((1u << ls) - 1u), sib);
@@ -634,6 +696,7 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
       r2 = tree<S>(lv[2]);
       r3 = tree<S>(lv[3]);
     }
+#endif
     // cash before this lane's order, and after the last order, under the guess
     double c_own = cash0;
 #if MGN_SPEC_CH1
@@ -706,6 +769,13 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
   // the post-transaction sums: the last lane's leaves are final but its own;
   // settle that one (its leaf at the bottom of the rightmost path, the left
   // children recorded) and broadcast its trees to the segment
+#if MGN_SPEC_DPP
+  // the root of the last pass's P tree: its guess held for every order
+  after.lp = rootP[0];
+  after.ml = rootP[1];
+  after.sh = rootP[2];
+  after.b = rootP[3];
+#else
   Q4 x;
   if constexpr (STREAM) {
     const d2* rv = reinterpret_cast<const d2*>(&er.r[S - 1]) + ((ls == S - 1 && go) ? 2 : 0);
@@ -728,6 +798,7 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
   after.ml = seg_bcast<S, S - 1>(x.b);
   after.sh = seg_bcast<S, S - 1>(x.c);
   after.b = seg_bcast<S, S - 1>(x.d);
+#endif
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   apply_orders<1>(s, go_own, cu2, me2, bm3, tpr, tco, uc, tp, tu, tc);

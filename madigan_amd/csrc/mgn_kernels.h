@@ -938,11 +938,14 @@ struct XRounds {
 // before and after it, and the cash increments; published to the segment's
 // LDS records.  The risk checks and cash updates that chain the orders are
 // resolved afterwards (XRounds, or the speculative form in mgn_duo.h).
-template <int M, int S>
+// WPP: publish the sum leaves (pre / post) to LDS (the in-register DPP tree
+// of broker_spec keeps them in lf_pre / lf_post instead)
+template <int M, int S, bool WPP = true>
 __device__ __forceinline__ void order_prep(const Lane<M>& s, const KParams& p, EnvRecs<M * S>& er,
                                            const double (&uc)[M], int ls, double (&cu2)[M],
                                            double (&me2)[M], double (&bm3)[M], double (&tpr)[M],
-                                           double (&tco)[M]) {
+                                           double (&tco)[M], double* lf_pre = nullptr,
+                                           double* lf_post = nullptr) {
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     const double u = uc[m];
@@ -978,15 +981,19 @@ __device__ __forceinline__ void order_prep(const Lane<M>& s, const KParams& p, E
     tco[m] = tcost;
     OrderRec& r = er.r[ls * M + m];
     const double mk0 = (cur < 0.) ? 1.0 : 0.0;
-    r.pre[0] = cur * price;
-    r.pre[1] = me0 * cur;
-    r.pre[2] = cur * (me0 * mk0);
-    r.pre[3] = bm0;
     const double mk1 = (cu2[m] < 0.) ? 1.0 : 0.0;
-    r.post[0] = cu2[m] * price;
-    r.post[1] = me2[m] * cu2[m];
-    r.post[2] = cu2[m] * (me2[m] * mk1);
-    r.post[3] = bm3[m];
+    const double pr[4] = {cur * price, me0 * cur, cur * (me0 * mk0), bm0};
+    const double po[4] = {cu2[m] * price, me2[m] * cu2[m], cu2[m] * (me2[m] * mk1), bm3[m]};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if constexpr (WPP) {
+        r.pre[q] = pr[q];
+        r.post[q] = po[q];
+      } else {
+        lf_pre[4 * m + q] = pr[q];
+        lf_post[4 * m + q] = po[q];
+      }
+    }
     r.aPX = opp ? fabs(price * excess) : fabs(price * u);
     r.X1 = close ? cur * tprice : -0.0;
     r.y = use + tcost;

@@ -626,12 +626,17 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
 #ifdef MGN_STAMPS
   const unsigned long long t_a = __builtin_amdgcn_s_memtime();
 #endif
-  double lf_pre[4], lf_post[4];  // MGN_SPEC_DPP: the own leaves, in registers
-  order_prep<1, S, !MGN_SPEC_DPP>(s, p, er, uc, ls, cu2, me2, bm3, tpr, tco, lf_pre, lf_post);
+  double lf_pre[4], lf_post[4];  // MGN_SPEC_DPP: the own leaves and check operands, in registers
+  OwnChk oc[1];
+  order_prep<1, S, !MGN_SPEC_DPP>(s, p, er, uc, ls, cu2, me2, bm3, tpr, tco, lf_pre, lf_post, oc);
 #ifdef MGN_STAMPS
   const unsigned long long t_b = __builtin_amdgcn_s_memtime();
 #endif
+#if MGN_SPEC_DPP
+  const OwnChk& own = oc[0];
+#else
   const OrderRec& own = er.r[ls];
+#endif
   const int act = uc[0] != 0. ? 1 : 0;
   // the lanes whose risk check reads the sums before their order (an order
   // that is checked at all: Portfolio.cpp:257-265 leaves an opposite-side

@@ -938,14 +938,19 @@ struct XRounds {
 // before and after it, and the cash increments; published to the segment's
 // LDS records.  The risk checks and cash updates that chain the orders are
 // resolved afterwards (XRounds, or the speculative form in mgn_duo.h).
-// WPP: publish the sum leaves (pre / post) to LDS (the in-register DPP tree
-// of broker_spec keeps them in lf_pre / lf_post instead)
+// WPP: publish the sum leaves (pre / post) and the check operands to LDS
+// (the in-register DPP tree of broker_spec keeps them in lf_pre / lf_post /
+// own instead; every order's cash terms X1, y, Z are published either way)
+struct OwnChk {
+  double aPX;
+  bool need_mc, need_insuff;
+};
 template <int M, int S, bool WPP = true>
 __device__ __forceinline__ void order_prep(const Lane<M>& s, const KParams& p, EnvRecs<M * S>& er,
                                            const double (&uc)[M], int ls, double (&cu2)[M],
                                            double (&me2)[M], double (&bm3)[M], double (&tpr)[M],
                                            double (&tco)[M], double* lf_pre = nullptr,
-                                           double* lf_post = nullptr) {
+                                           double* lf_post = nullptr, OwnChk* own = nullptr) {
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     const double u = uc[m];
@@ -994,15 +999,22 @@ __device__ __forceinline__ void order_prep(const Lane<M>& s, const KParams& p, E
         lf_post[4 * m + q] = po[q];
       }
     }
-    r.aPX = opp ? fabs(price * excess) : fabs(price * u);
+    const double aPX = opp ? fabs(price * excess) : fabs(price * u);
     r.X1 = close ? cur * tprice : -0.0;
     r.y = use + tcost;
     r.Z = (repay || neg) ? bm1 : 0.0;
     const bool act = u != 0.;
-    r.act = act;
-    r.need_mc = !opp;
-    r.need_insuff = !opp || rev;
-    r.pad = 0;
+    if constexpr (WPP) {  // XRounds reads every order's check operands from LDS
+      r.aPX = aPX;
+      r.act = act;
+      r.need_mc = !opp;
+      r.need_insuff = !opp || rev;
+      r.pad = 0;
+    } else {  // broker_spec: the lane checks its own order only
+      own[m].aPX = aPX;
+      own[m].need_mc = !opp;
+      own[m].need_insuff = !opp || rev;
+    }
   }
   // the segment's records are written by its own lanes: wave-scope ordering
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -24,8 +24,11 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmadigan_hip.so")
 OBJ = os.path.join(HERE, "_obj")
 ARCH = os.environ.get("MADIGAN_OFFLOAD_ARCH", "gfx950")
+# kernarg preload: a kernel's leading scalar / pointer arguments (up to 16
+# SGPRs) arrive in SGPRs with the wave instead of through the kernel-argument
+# segment (k_step_trio passes its ledger-role pointers first)
 FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-         "-fno-fast-math", "-Wall"]
+         "-fno-fast-math", "-Wall", "-mllvm", "-amdgpu-kernarg-preload-count=6"]
 
 
 def hipcc() -> str:

@@ -88,8 +88,8 @@ void launch_trio(const StepArgs& a) {
   const int epb = (small ? 64 : TRIO_W) / S;
   const int grid = (a.p.N + epb - 1) / epb;
   auto go = [&](auto kern) {
-    launch_timed(a.ev0, a.ev1, kern, dim3(grid), dim3(small ? 192 : TRIO_BLOCK), 0, a.stream, a.p, a.out,
-                 a.in_kind, a.units, a.aidx, a.act, a.K);
+    launch_timed(a.ev0, a.ev1, kern, dim3(grid), dim3(small ? 192 : TRIO_BLOCK), 0, a.stream, a.p.L, a.p.mep,
+                 a.p.Bm, a.p.P, a.p.cash, a.act, a.p, a.out, a.in_kind, a.units, a.aidx, a.K);
   };
   const bool disc = a.in_kind == IN_DISCRETE;
   const uint32_t om = traj_mask(a.out);
@@ -122,7 +122,7 @@ void launch_trio(const StepArgs& a) {
           hipSuccess)
         return;
       launch_timed(a.ev0, a.ev1, kern, dim3(grid), dim3(small ? 192 : TRIO_BLOCK), (uint32_t)lds, a.stream,
-                   a.p, a.out, a.in_kind, a.units, a.aidx, a.act, a.K);
+                   a.p.L, a.p.mep, a.p.Bm, a.p.P, a.p.cash, a.act, a.p, a.out, a.in_kind, a.units, a.aidx, a.K);
     };
     if (small) {
       if (disc) {

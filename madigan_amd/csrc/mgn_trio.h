@@ -178,10 +178,19 @@ inline size_t trio_nst_dyn_lds(int S, int TW, int nstep) {
 // keeps the tick's state as the reset tick's.
 template <int S, bool RQ1, bool DISC, uint32_t OMC = 0, bool WIN = false, int TW = TRIO_W, bool NST = false,
           int GK = -1, bool RP = false>
-__global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out, int in_kind_rt,
+// The leading pointer arguments are the ledger role's state and actions:
+// built with -amdgpu-kernarg-preload-count (madigan_amd/build.py) they arrive
+// in SGPRs with the wave, so the orders' loads issue without waiting for the
+// kernel-argument segment (a one-step launch is one dependent chain)
+__global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restrict__ kL,
+                                                          const double* __restrict__ kmep,
+                                                          const double* __restrict__ kBm,
+                                                          const double* __restrict__ kP,
+                                                          const double* __restrict__ kcash,
+                                                          const int8_t* __restrict__ act_in, KParams p,
+                                                          mgn_traj out, int in_kind_rt,
                                                           const double* __restrict__ units_in,
-                                                          const int32_t* __restrict__ aidx_in,
-                                                          const int8_t* __restrict__ act_in, int K) {
+                                                          const int32_t* __restrict__ aidx_in, int K) {
   MGN_IT(0, 0);
   warm_kernargs<(int)(sizeof(KParams) + sizeof(mgn_traj) + 48)>();
   MGN_IT(47, 0);
@@ -226,7 +235,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
   s.P[0] = 5.0;
 #else
   // the finish role takes its prices from the generator's LDS records
-  s.P[0] = (s.valid[0] && role != 2) ? p.P[li] : 0.;
+  s.P[0] = (s.valid[0] && role != 2) ? kP[li] : 0.;
 #endif
   s.L[0] = s.mep[0] = s.Bm[0] = s.sx[0] = s.oum[0] = s.dy[0] = 0.;
   s.tlen[0] = 0;
@@ -270,11 +279,11 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(KParams p, mgn_traj out
     if (RP) s.rcur = p.rcur[envc];
   } else if (role == 1) {
     if (s.valid[0]) {
-      s.L[0] = p.L[li];
-      s.mep[0] = p.mep[li];
-      s.Bm[0] = p.Bm[li];
+      s.L[0] = kL[li];
+      s.mep[0] = kmep[li];
+      s.Bm[0] = kBm[li];
     }
-    cash = p.cash[envc];
+    cash = kcash[envc];
     if (in_kind == IN_DISCRETE && K > 0) act_cur = act_lane[0];
   } else {
     ep_ret = p.ep[(size_t)envc * 2];

@@ -25,7 +25,9 @@ def main():
     fuse = int(os.environ.get("FUSE", 64))
     nst = int(os.environ.get("NSTEP", 1))
     extra = dict(nstep_return=nst, discount=0.99) if nst > 1 else {}
-    env, _, _ = bench.workload_env("C3", N, 8, 0, "cuda:0", **extra)
+    wl = os.environ.get("WORKLOAD", "C3")
+    A = int(os.environ.get("ASSETS", 8))
+    env, _, _ = bench.workload_env(wl, N, A, 0, "cuda:0", **(extra if wl == "C3" else {}))
     assert int(env.lib.mgn_get_schedule(env.h)) == L.SCHED_TRIO
     fn = env.lib.mgn_diag_stamps
     fn.argtypes = [C.POINTER(C.c_ulonglong)]
@@ -47,7 +49,7 @@ def main():
     fn(buf)
     v = list(buf)
     it = max(v[8], 1)
-    res = {"N": N, "fuse": fuse, "us_per_launch": e0.elapsed_time(e1) * 1000 / reps,
+    res = {"workload": wl, "assets": env.A, "N": N, "fuse": fuse, "us_per_launch": e0.elapsed_time(e1) * 1000 / reps,
            "iters_per_block": v[8] / max(v[10], 1),
            "gen": {"work": round(v[0] / it, 1), "wait": round(v[1] / it, 1)},
            "ledger": {"work": round(v[4] / it, 1), "wait": round(v[5] / it, 1),

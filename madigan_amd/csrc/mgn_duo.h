@@ -1091,7 +1091,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
             duo_replay_tick(s, p, ts, rp, rnx);
           } else {
             if (sh.reset[el]) src_reset<M, false, GK>(s, p, env, ts);  // Env::reset -> dataSource->reset (Env.h:183)
-            if (!(ABL && (p.ablate & 2))) gen_tick<M, false, false, GK>(s, p, env, ts);
+            if (!(ABL && (p.ablate & 2))) gen_tick<M, false, false, GK, true>(s, p, env, ts);
             ts = ts + 1;
           }
           sh.price[l] = s.P[0];

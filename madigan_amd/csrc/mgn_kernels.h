@@ -343,7 +343,8 @@ __device__ __noinline__ double sinedyn_tick(const double* q, double* ax, bool tr
 // per-lane kind dispatch folds away at compile time.
 // qreg: the lane's parameters in registers (the three-role kernel with a
 // compile-time kind, M = 1), else read from p.src
-template <int M, bool RP = true, bool AUX = true, int GK = -1>
+// INL: the Sine kinds' sin inlined (the pipelined kernels), else called
+template <int M, bool RP = true, bool AUX = true, int GK = -1, bool INL = false>
 __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, uint64_t tick,
                                          const double* qreg = nullptr) {
   if (RP && p.replay) {
@@ -425,7 +426,7 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
       if (q[5] != 0.0) noise = d.z * q[5] + 0.0;
       const double PI2 = 3.141592653589793238463 * 2;
       double wave;
-      if (kind == MGN_SRC_SINE) wave = q[2] * det_sin(PI2 * s.sx[m] * q[0]);
+      if (kind == MGN_SRC_SINE) wave = q[2] * (INL ? det_sin_inl(PI2 * s.sx[m] * q[0]) : det_sin(PI2 * s.sx[m] * q[0]));
       else if (kind == MGN_SRC_SAWTOOTH) wave = q[2] * frac_part(s.sx[m] * q[0]);
       else wave = 4 * q[2] / PI2 * det_asin(det_sin(PI2 * s.sx[m] / q[0]));
       s.P[m] = noise + q[1] + wave;

@@ -109,8 +109,11 @@ __device__ __forceinline__ double k_cos(double x, double y) {
   return w + (((1.0 - w) - hz) + (z * r - x * y));
 }
 
-// sin(x) with fdlibm's medium Cody-Waite reduction
-__device__ __noinline__ double det_sin(double x) {
+// sin(x) with fdlibm's medium Cody-Waite reduction; det_sin is its called
+// form (the multi-slot kernels), det_sin_inl the inlined one (the pipelined
+// kernels' generator role: a call there spilled live registers to scratch
+// around every Sine tick)
+__device__ __forceinline__ double det_sin_inl(double x) {
   const double invpio2 = bits_to_d(0x3FE45F306DC9C883ull);
   const double pio2_1 = bits_to_d(0x3FF921FB54400000ull), pio2_1t = bits_to_d(0x3DD0B4611A626331ull);
   const double pio2_2 = bits_to_d(0x3DD0B4611A600000ull), pio2_2t = bits_to_d(0x3BA3198A2E037073ull);
@@ -145,6 +148,7 @@ __device__ __noinline__ double det_sin(double x) {
   const double v = (q & 1) ? k_cos(y0, y1) : k_sin(y0, y1, true);
   return (q >= 2) ? -v : v;
 }
+__device__ __noinline__ double det_sin(double x) { return det_sin_inl(x); }
 
 constexpr double TWO_M32 = 2.3283064365386962890625e-10;
 

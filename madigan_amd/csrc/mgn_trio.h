@@ -84,6 +84,16 @@ constexpr int TRIO_W = 256;  // lanes per role
 #endif
 
 
+// generator lanes slot-major on handles of several source kinds (k_step_trio)
+#ifndef MGN_TRIO_GSLOT
+#define MGN_TRIO_GSLOT 1
+#endif
+
+// NST: the pop's ordered sum read back by the env's first lane only
+#ifndef MGN_NST_SUM1
+#define MGN_NST_SUM1 1
+#endif
+
 // NST: rounds of a pop's summands evaluated together (the terms' chains
 // interleave; rounds past the buffer's are computed and dropped)
 #ifndef MGN_NST_U
@@ -207,8 +217,17 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   extern __shared__ __attribute__((aligned(16))) double s_nst[];          // NST: (EPB, 2 nst_pad(n, S))
   const int role = threadIdx.x / TRIO_W;  // 0 generator, 1 ledger, 2 finish
   const int l = threadIdx.x % TRIO_W;
-  const int el = l / S;
-  const int ls = l % S;
+  // GSLOT: a handle whose assets are of several source kinds (a Composite)
+  // gives its generator lanes slot-major: lane l ticks asset slot l / EPB of
+  // env l % EPB, so a generator wave holds 64 / EPB asset slots of every env
+  // of the block -- one or two source kinds -- instead of every slot of a
+  // few envs, each kind's branch executed by the waves that hold it (the
+  // Composite's Sine, OU and TrendOU branches no longer run in every
+  // generator wave).  Records stay env-major: the lane publishes at el S + ls.
+  constexpr bool GSLOT = MGN_TRIO_GSLOT && GK < 0 && !RP && TW / S > 1;
+  const int el = (GSLOT && role == 0) ? l % EPB : l / S;
+  const int ls = (GSLOT && role == 0) ? l / EPB : l % S;
+  const int lx = el * S + ls;  // the lane's (env, asset) record index
   const int env = blockIdx.x * EPB + el;
   const bool live = env < p.N;
   const int envc = live ? env : 0;
@@ -366,7 +385,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       if constexpr (RP) {
         duo_replay_tick(s, p, ts, rp, rnx);
       } else {
-        gen_tick<M, false, false, GK>(s, p, env, ts, QREG ? qr : nullptr);
+        gen_tick<M, false, false, GK, true>(s, p, env, ts, QREG ? qr : nullptr);
         ts = ts + 1;
       }
     };
@@ -427,7 +446,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           }
           // Env::reset -> dataSource->reset + getData (Env.h:181-187)
           src_reset<M, false, GK>(s, p, env, ts, QREG ? qr : nullptr);
-          gen_tick<M, false, false, GK>(s, p, env, ts, QREG ? qr : nullptr);
+          gen_tick<M, false, false, GK, true>(s, p, env, ts, QREG ? qr : nullptr);
           ts = ts + 1;
           if (WIN) gpend = p.W - 1;
         } else if (k < K) {
@@ -454,7 +473,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           k += 1;
         }
       }
-      sh.price[cur][l] = s.P[0];
+      sh.price[cur][lx] = s.P[0];
       if (!MGN_TRIO_GST && ls == 0) sh.ts[cur][el] = ts;
       if constexpr (RP) {
         if (ls == 0) {
@@ -749,8 +768,15 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     const int R = p.F + A + 1;
     MGN_G double* row = gs.ring + ((size_t)env * p.W + rhead) * R;
     MGN_G double* hrow = p.hist ? gs.hist + ((size_t)env * p.hrows + hcnt) * R : nullptr;
-    put_price(row, P, p.ring_log != 0, q);
-    if (hrow) put_price(hrow, P, p.ring_log != 0, q);
+    if (!RP && s.valid[0]) {
+      // the lane's price column, normalised once for the ring and the history row
+      const double pv = p.ring_log != 0 ? log_norm(P) : P;
+      ost(row + s.asset[0], pv);
+      if (hrow) ost(hrow + s.asset[0], pv);
+    } else if (RP) {
+      put_price(row, P, p.ring_log != 0, q);
+      if (hrow) put_price(hrow, P, p.ring_log != 0, q);
+    }
     if (s.valid[0]) {
       ost(row + (p.F + 1 + s.asset[0]), portA);
       if (hrow) ost(hrow + (p.F + 1 + s.asset[0]), portA);
@@ -897,6 +923,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #ifdef MGN_NST_ABL_SUM  // diagnostic timing build (outputs wrong): no ordered sum
           acc = scr[0];
 #else
+          // the ordered sum only feeds the popped value the env's first lane
+          // stores: only that lane reads the summands back (MGN_NST_SUM1)
+          if (!MGN_NST_SUM1 || ls == 0) {
           const d2* sc = reinterpret_cast<const d2*>(scr);
           d2 cur[S / 2];
 #pragma unroll
@@ -913,6 +942,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
             }
 #pragma unroll
             for (int u = 0; u < S / 2; ++u) cur[u] = nxt[u];
+          }
           }
 #endif
           double res = acc;

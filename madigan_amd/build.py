@@ -29,6 +29,12 @@ ARCH = os.environ.get("MADIGAN_OFFLOAD_ARCH", "gfx950")
 # segment (k_step_trio passes its ledger-role pointers first)
 FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-fno-fast-math", "-Wall", "-mllvm", "-amdgpu-kernarg-preload-count=6"]
+# per-unit flags: the three-role kernel's two-slots-per-lane instantiations
+# (mgn_launch_a16m2.hip) are built without machine-level loop-invariant code
+# motion -- hoisting the math kernels' 64-bit polynomial constants out of the
+# step loop left them live across it at the 168-register budget and spilled
+# them to scratch (48 -> 4 spilled registers in the generic generator build)
+UNIT_FLAGS = {"mgn_launch_a16m2.hip": ["-mllvm", "-disable-machine-licm"]}
 
 
 def hipcc() -> str:
@@ -123,7 +129,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
 
     def compile_one(src):
         obj = os.path.join(OBJ, os.path.basename(src).replace(".hip", ".o"))
-        cmd = [cc, *FLAGS, "-c", "-o", obj, src]
+        cmd = [cc, *FLAGS, *UNIT_FLAGS.get(os.path.basename(src), []), "-c", "-o", obj, src]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -373,9 +373,13 @@ void choose_sched(mgn_env* e) {
   } else {
     // 16 assets: the three-role kernel where measured faster -- generator
     // sources with one-step rewards and no window (5.2 vs 6.3 us/step at
-    // 8192 x 16 TrendOU) and replay tapes (C5: 405 vs 485 us per 64-step launch)
+    // 8192 x 16 TrendOU) and replay tapes (C5: 405 vs 485 us per 64-step launch),
+    // and, where its two-slots-per-lane layout runs the agent loop's discrete
+    // steps (trio_m2_ok), windowed generator handles too
     e->trio = trio_eligible(e) && e->m == 1 &&
-              (e->apad <= 8 || (e->apad <= 16 && ((e->W == 0 && e->cfg.nstep == 1) || e->replay)));
+              (e->apad <= 8 ||
+               (e->apad <= 16 && ((e->W == 0 && e->cfg.nstep == 1) || e->replay ||
+                                  mgn::trio_m2_ok(e->N, e->A, e->cfg.nstep, e->D, mgn::IN_DISCRETE))));
     e->duo = !e->trio && duo_eligible(e) && e->m == 1;
   }
 }

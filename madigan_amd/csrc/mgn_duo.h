@@ -818,6 +818,150 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
 #endif
 }
 
+// broker_spec with two orders per lane (slots 2 ls, 2 ls + 1 of a 2 S-asset
+// env: the three-role kernel's 16-asset layout on 8 lanes).  The canonical
+// tree's first level is the lane's own pair, formed in registers: the check
+// of slot 0 reads the pair pre + pre, slot 1 (post of slot 0 where it
+// executes) + pre, and the pair's P / Q versions go on to dpp_tree4's
+// cross-lane levels, which add the same sibling to both slots' paths.  The
+// cash chain is walked by the env's first lane over all 2 S orders, as
+// broker_spec's MGN_SPEC_CH1; the fix-up of a wrong guess is broker_spec's
+// (the first order whose check disagrees decides, the later ones are guessed
+// again), so the result is the sequential Broker's.
+template <int S, bool RQ1>
+__device__ __forceinline__ void broker_spec_m2(Lane<2>& s, const KParams& p, EnvRecs<2 * S>& er, double& cash,
+                                               const double (&uc)[2], double (&tp)[2], double (&tu)[2],
+                                               double (&tc)[2], int (&rk)[2], int ls, Sums& after, int& any_mc) {
+  constexpr int M = 2, APAD = 2 * S;
+  double cu2[M], me2[M], bm3[M], tpr[M], tco[M];
+  double lf_pre[4 * M], lf_post[4 * M];
+  OwnChk oc[M];
+  order_prep<M, S, false>(s, p, er, uc, ls, cu2, me2, bm3, tpr, tco, lf_pre, lf_post, oc);
+  // the leaves are re-formed in every pass from the slot state the lane
+  // holds anyway (ledger, price, and the order's outcome): the same products
+  // (order_prep's), so the same bits, without 16 leaf registers live across
+  // the passes (the 168-register budget)
+  auto leaves = [&](int m, double (&pr)[4], double (&po)[4]) {
+    double L0 = s.L[m], me0 = s.mep[m], bm0 = s.Bm[m], P = s.P[m], c2 = cu2[m], e2 = me2[m], b2 = bm3[m];
+    asm volatile("" : "+v"(L0), "+v"(me0), "+v"(bm0), "+v"(P), "+v"(c2), "+v"(e2), "+v"(b2));
+    const double mk0 = (L0 < 0.) ? 1.0 : 0.0;
+    const double mk1 = (c2 < 0.) ? 1.0 : 0.0;
+    pr[0] = L0 * P;
+    pr[1] = me0 * L0;
+    pr[2] = L0 * (me0 * mk0);
+    pr[3] = bm0;
+    po[0] = c2 * P;
+    po[1] = e2 * c2;
+    po[2] = c2 * (e2 * mk1);
+    po[3] = b2;
+  };
+  const int sh0 = ls * M;
+  int act[M];
+  act[0] = uc[0] != 0. ? 1 : 0;
+  act[1] = uc[1] != 0. ? 1 : 0;
+  const uint32_t act_bits = (uint32_t)seg_or<S>((act[0] << sh0) | (act[1] << (sh0 + 1)));
+  uint32_t go_bits = act_bits;  // the guess
+  const double cash0 = cash;
+  int go[M] = {0, 0}, mc[M] = {0, 0}, insuff[M] = {0, 0};
+  double cend = cash0;
+  double rootP[4];
+  for (int it = 0; it <= APAD; ++it) {
+    const bool g0 = ((go_bits >> sh0) & 1) != 0, g1 = ((go_bits >> (sh0 + 1)) & 1) != 0;
+    double path0[4], path1[4];
+    {
+      double nP[4], nQ[4], pr0[4], po0[4], pr1[4], po1[4];
+      leaves(0, pr0, po0);
+      leaves(1, pr1, po1);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double a0 = pr0[q], a1 = pr1[q];
+        const double b0 = g0 ? po0[q] : a0;
+        nQ[q] = a0 + a1;
+        path0[q] = nQ[q];
+        path1[q] = b0 + a1;
+        nP[q] = b0 + (g1 ? po1[q] : a1);
+      }
+      auto level = [&](auto sib, bool right) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const double sp = sib(nP[q]), sq = sib(nQ[q]);
+          const double add = right ? sp : sq;
+          path0[q] = path0[q] + add;
+          path1[q] = path1[q] + add;
+          nP[q] = nP[q] + sp;
+          nQ[q] = nQ[q] + sq;
+        }
+      };
+      if constexpr (S >= 2) level([](double v) { return dpp_f64<0xB1>(v); }, (ls & 1) != 0);
+      if constexpr (S >= 4) level([](double v) { return dpp_f64<0x4E>(v); }, (ls & 2) != 0);
+      if constexpr (S >= 8) level([](double v) { return dpp_f64<0x141>(v); }, (ls & 4) != 0);
+      if constexpr (S >= 16) level([](double v) { return dpp_f64<0x140>(v); }, (ls & 8) != 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) rootP[q] = nP[q];
+    }
+    if (ls == 0) {
+      double c = cash0;
+#pragma unroll
+      for (int i = 0; i < APAD; ++i) {
+        er.cpre[i] = c;
+        const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
+        const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
+        const double ci = ((c + xz.y) - yz.x) - yz.y;
+        c = ((go_bits >> i) & 1) ? ci : c;
+      }
+      er.cpre[APAD] = c;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const d2 cown = *reinterpret_cast<const d2*>(&er.cpre[sh0]);
+    cend = er.cpre[APAD];
+    uint32_t badm = 0, gom = 0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const double* r = m == 0 ? path0 : path1;
+      const double c_own = m == 0 ? cown.x : cown.y;
+      // Portfolio::checkRisk(i, u), Portfolio.cpp:254-279 (as XRounds)
+      const double pnl = r[0] - r[1];
+      const double balance = c_own + r[2];
+      const double bp = balance + pnl;
+      const double availM = RQ1 ? bp : bp / p.reqM;
+      const double equity = (c_own + r[0]) - r[3];
+      const double mr = p.mainM * pnl;
+      mc[m] = (oc[m].need_mc != 0) & ((equity <= -mr) | (bp <= -mr));
+      insuff[m] = (oc[m].need_insuff != 0) & ((availM <= oc[m].aPX) | (balance <= 0.));
+      go[m] = act[m] & !mc[m] & !insuff[m];
+      badm |= (go[m] != (int)((go_bits >> (sh0 + m)) & 1)) ? (1u << (sh0 + m)) : 0u;
+      gom |= (uint32_t)go[m] << (sh0 + m);
+    }
+    const uint32_t bad = (uint32_t)seg_or<S>((int)badm);
+#ifdef MGN_STAMPS
+    if (threadIdx.x == DUO_HALF) s_duo_sub[6] += 1;  // passes of the wave
+#endif
+    if (bad == 0) break;
+    const int i0 = __builtin_ctz(bad);
+    const uint32_t go_now = (uint32_t)seg_or<S>((int)gom);
+    const uint32_t below = (1u << i0) - 1u;
+    go_bits = (go_bits & below) | (go_now & (1u << i0)) | (act_bits & ~(below | (1u << i0)));
+  }
+  cash = cend;
+  any_mc = seg_or<S>((act[0] & mc[0]) | (act[1] & mc[1])) != 0;
+#pragma unroll
+  for (int m = 0; m < M; ++m)
+    rk[m] = act[m] ? (mc[m] ? MGN_MARGIN_CALL : (insuff[m] ? MGN_INSUFF_MARGIN : MGN_GREEN)) : rk[m];
+  const bool go_own[M] = {go[0] != 0, go[1] != 0};
+  after.lp = rootP[0];
+  after.ml = rootP[1];
+  after.sh = rootP[2];
+  after.b = rootP[3];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  apply_orders<M>(s, go_own, cu2, me2, bm3, tpr, tco, uc, tp, tu, tc);
+#ifdef MGN_STAMPS
+  if (threadIdx.x == DUO_HALF) s_duo_sub[5] += 1;  // broker calls
+#endif
+}
+
 // The kernel arguments (KParams + mgn_traj, ~640 bytes) are read through the
 // scalar cache in chunks the register allocator interleaves with their uses,
 // each chunk a dependent miss on a cold cache at launch (~1.7 us of the

@@ -344,7 +344,9 @@ __device__ __noinline__ double sinedyn_tick(const double* q, double* ax, bool tr
 // qreg: the lane's parameters in registers (the three-role kernel with a
 // compile-time kind, M = 1), else read from p.src
 // INL: the Sine kinds' sin inlined (the pipelined kernels), else called
-template <int M, bool RP = true, bool AUX = true, int GK = -1, bool INL = false>
+// SEQ: the slots ticked one after another (a scheduling fence between them:
+// the three-role kernel's 168-register budget at two slots per lane)
+template <int M, bool RP = true, bool AUX = true, int GK = -1, bool INL = false, bool SEQ = false>
 __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, uint64_t tick,
                                          const double* qreg = nullptr) {
   if (RP && p.replay) {
@@ -371,6 +373,9 @@ __device__ __forceinline__ void gen_tick(Lane<M>& s, const KParams& p, int env, 
   tick += s.dskip;  // the draw index (mgn_math.h, v3)
 #pragma unroll
   for (int m = 0; m < M; ++m) {
+    if constexpr (SEQ) {
+      if (m > 0) __builtin_amdgcn_sched_barrier(0);
+    }
     if (!s.valid[m]) continue;
     const int a = s.asset[m];
     const double* q = qreg ? qreg : p.src[a].p;

@@ -50,6 +50,18 @@ struct ValArgs {
 // a workgroup's LDS on gfx950 (the three-role kernel's n-step eligibility)
 constexpr size_t kTrioLdsMax = 160 * 1024;
 
+// the three-role kernel's two-slots-per-lane layout (launch_trio_m2): 9..16
+// assets at the 256-lane layout (N x 16 >= 256 x 256 lanes), discrete
+// actions, one-step rewards with a scalar shaper
+#ifndef MGN_TRIO_M2
+#define MGN_TRIO_M2 1
+#endif
+inline bool trio_m2_ok(long long n_envs, int A, int nstep, int D, int in_kind) {
+  return MGN_TRIO_M2 && A > 8 && A <= 16 && n_envs * 16 >= 65536 && nstep == 1 && D == 1 &&
+         in_kind == IN_DISCRETE;
+}
+void launch_trio_m2_a16(const StepArgs& a);
+
 // smallest assets-per-lane with at most 16 lanes per env (DPP-only reductions)
 constexpr int min_m(int apad) { return apad > 16 ? apad / 16 : 1; }
 

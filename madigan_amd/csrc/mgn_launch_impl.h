@@ -80,9 +80,49 @@ void launch_duo(const StepArgs& a) {
   }
 }
 
+// three-role kernel, two asset slots per lane (MM = 2): a 16-asset env on 8
+// lanes per role, so the 256-lane layout holds 32 envs per workgroup (8192
+// envs: 256 workgroups, one round over the CUs, where one slot per lane needs
+// 512 in two rounds).  Discrete actions (the agent loop), one-step rewards
+// with a scalar shaper (trio_m2_ok)
+template <int S>
+void launch_trio_m2(const StepArgs& a) {
+  constexpr int epb = TRIO_W / S;
+  const int grid = (a.p.N + epb - 1) / epb;
+  auto go = [&](auto kern) {
+    launch_timed(a.ev0, a.ev1, kern, dim3(grid), dim3(TRIO_BLOCK), 0, a.stream, a.p.L, a.p.mep, a.p.Bm, a.p.P,
+                 a.p.cash, a.act, a.p, a.out, a.in_kind, a.units, a.aidx, a.K);
+  };
+  const bool win = a.p.W > 0;
+  if (a.p.replay) {
+    if (win) {
+      if (a.p.reqm_one) go(k_step_trio<S, true, true, 0, true, TRIO_W, false, -1, true, 2>);
+      else go(k_step_trio<S, false, true, 0, true, TRIO_W, false, -1, true, 2>);
+    } else {
+      if (a.p.reqm_one) go(k_step_trio<S, true, true, 0, false, TRIO_W, false, -1, true, 2>);
+      else go(k_step_trio<S, false, true, 0, false, TRIO_W, false, -1, true, 2>);
+    }
+  } else if (win) {
+    if (a.p.reqm_one) go(k_step_trio<S, true, true, 0, true, TRIO_W, false, -1, false, 2>);
+    else go(k_step_trio<S, false, true, 0, true, TRIO_W, false, -1, false, 2>);
+  } else if (a.gkind == MGN_SRC_TRENDOU && traj_mask(a.out) == O_STD) {
+    if (a.p.reqm_one) go(k_step_trio<S, true, true, O_STD, false, TRIO_W, false, MGN_SRC_TRENDOU, false, 2>);
+    else go(k_step_trio<S, false, true, O_STD, false, TRIO_W, false, MGN_SRC_TRENDOU, false, 2>);
+  } else {
+    if (a.p.reqm_one) go(k_step_trio<S, true, true, 0, false, TRIO_W, false, -1, false, 2>);
+    else go(k_step_trio<S, false, true, 0, false, TRIO_W, false, -1, false, 2>);
+  }
+}
+
 // three-role pipelined step kernel (mgn_trio.h): S = APAD lanes per env per role
 template <int S>
 void launch_trio(const StepArgs& a) {
+  if constexpr (S == 16) {
+    if (trio_m2_ok(a.p.N, a.p.A, a.p.nstep, a.p.D, a.in_kind)) {
+      launch_trio_m2_a16(a);  // mgn_launch_a16m2.hip
+      return;
+    }
+  }
   // one wave per role when 256 lanes per role would leave CUs idle
   const bool small = (long long)a.p.N * S < 256LL * TRIO_W;
   const int epb = (small ? 64 : TRIO_W) / S;

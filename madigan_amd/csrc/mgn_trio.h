@@ -127,15 +127,17 @@ __host__ __device__ constexpr int nst_pad(int n, int S) {
   return (n + (S > 8 ? S : 8) - 1) / (S > 8 ? S : 8) * (S > 8 ? S : 8);
 }
 
-template <int S, int TW = TRIO_W>
+// per asset slot (M per lane: slot (env, asset) at el APAD + ls M + m)
+template <int S, int TW = TRIO_W, int M = 1>
 struct TrioShared {
   static constexpr int TRIO_W = TW;
   static constexpr int EPB = TRIO_W / S;
+  static constexpr int NSL = TRIO_W * M;  // asset slots of the block
   // prices after the iteration's tick (G -> L, F)
-  double price[2][TRIO_W];
+  double price[2][NSL];
   // the orders L ran (L -> F): ledger after the orders, responses, L*P before
-  double rL[2][TRIO_W], rTp[2][TRIO_W], rTu[2][TRIO_W], rTc[2][TRIO_W], rPv[2][TRIO_W];
-  int32_t rRk[2][TRIO_W];
+  double rL[2][NSL], rTp[2][NSL], rTu[2][NSL], rTc[2][NSL], rPv[2][NSL];
+  int32_t rRk[2][NSL];
   // per env: cash and the three price-independent sums after the orders,
   // equity before the step, the step index and TR_* flags
   double rCash[2][EPB], rMl[2][EPB], rSh[2][EPB], rB[2][EPB], rPrevEq[2][EPB];
@@ -149,17 +151,67 @@ struct TrioShared {
   // lane's feature column value (F <= S) -- G -> F for State.price / windows
   int64_t row[2][EPB];
   uint32_t dend[2][EPB];
-  double feat[2][TRIO_W];
+  double feat[2][NSL];
 };
 
-// LDS of k_step_trio<S, ..., TW, NST>: its static arrays (an upper bound of
-// the compiler's layout) plus, for NST, the rings in dynamic LDS; the
+// LDS of k_step_trio<S, ..., TW, NST, ..., M>: its static arrays (an upper
+// bound of the compiler's layout) plus, for NST, the rings in dynamic LDS; the
 // launcher's eligibility test keeps the sum within a workgroup's 160 KiB
 // (kTrioLdsMax, mgn_launch.h)
-template <int S, int TW, bool NST>
+template <int S, int TW, bool NST, int M = 1>
 constexpr size_t trio_static_lds() {
-  return sizeof(TrioShared<S, TW>) + (size_t)(TW / S) * sizeof(EnvRecs<S>) + S * sizeof(mgn_asset_source) +
-         (MGN_MAX_ASSETS + 1) * sizeof(double) + (NST ? MGN_MAX_NSTEP : 1) * sizeof(double) + 256;
+  return sizeof(TrioShared<S, TW, M>) + (size_t)(TW / S) * sizeof(EnvRecs<S * M>) +
+         S * M * sizeof(mgn_asset_source) + (MGN_MAX_ASSETS + 1) * sizeof(double) +
+         (NST ? MGN_MAX_NSTEP : 1) * sizeof(double) + 256;
+}
+
+// The replay tape's tick for the lane's M slots (duo_replay_tick's, per slot:
+// feature column fcol + m when the row's features are spread one per slot)
+template <int M>
+struct RpCurM {
+  double curF[M];
+  int64_t row;
+  uint32_t dend;
+};
+template <int M>
+struct RpNextM {
+  double P[M], F[M];
+  uint64_t ts;
+  uint32_t dend;
+};
+template <int M>
+__device__ __forceinline__ void trio_replay_tick(Lane<M>& s, const KParams& p, uint64_t& ts, RpCurM<M>& cur,
+                                                 RpNextM<M>& nx) {
+  const int64_t row = s.rcur;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const bool fown = s.fcol >= 0 && s.fcol + m < p.F;
+    if (s.pf_ok) {
+      if (s.valid[m]) s.P[m] = nx.P[m];
+      if (fown) cur.curF[m] = nx.F[m];
+    } else {
+      if (s.valid[m]) s.P[m] = p.rp_price[(size_t)row * p.A + s.asset[m]];
+      if (fown) cur.curF[m] = p.rp_feat[(size_t)row * p.F + s.fcol + m];
+    }
+  }
+  if (s.pf_ok) {
+    ts = nx.ts;
+    cur.dend = nx.dend;
+  } else {
+    ts = p.rp_ts[row];
+    cur.dend = p.rp_end[row];
+  }
+  cur.row = row;
+  s.row = row;
+  s.rcur = (row + 1 == p.rp_rows) ? 0 : row + 1;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    if (s.valid[m]) nx.P[m] = p.rp_price[(size_t)s.rcur * p.A + s.asset[m]];
+    if (s.fcol >= 0 && s.fcol + m < p.F) nx.F[m] = p.rp_feat[(size_t)s.rcur * p.F + s.fcol + m];
+  }
+  nx.ts = p.rp_ts[s.rcur];
+  nx.dend = p.rp_end[s.rcur];
+  s.pf_ok = true;
 }
 inline size_t trio_nst_dyn_lds(int S, int TW, int nstep) {
   return (size_t)(TW / S) * 2 * nst_pad(nstep, S) * sizeof(double);
@@ -186,8 +238,11 @@ inline size_t trio_nst_dyn_lds(int S, int TW, int nstep) {
 // replay source carries on through a reset (DataSource.cpp:200-206), so the
 // reset's getData reads the row the voided speculative tick read: a rollback
 // keeps the tick's state as the reset tick's.
+// MM: asset slots per lane (2: a 16-asset env on 8 lanes per role, so 8192
+// envs fit one workgroup per CU; slots ls MM + m in the canonical order, the
+// ledger's broker_spec_m2; one-step rewards with a scalar shaper, D = 1)
 template <int S, bool RQ1, bool DISC, uint32_t OMC = 0, bool WIN = false, int TW = TRIO_W, bool NST = false,
-          int GK = -1, bool RP = false>
+          int GK = -1, bool RP = false, int MM = 1>
 // The leading pointer arguments are the ledger role's state and actions:
 // built with -amdgpu-kernarg-preload-count (madigan_amd/build.py) they arrive
 // in SGPRs with the wave, so the orders' loads issue without waiting for the
@@ -205,13 +260,15 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   warm_kernargs<(int)(sizeof(KParams) + sizeof(mgn_traj) + 48)>();
   MGN_IT(47, 0);
   const int in_kind = DISC ? IN_DISCRETE : in_kind_rt;
-  constexpr int M = 1;
+  constexpr int M = MM;
+  static_assert(M == 1 || (M == 2 && !NST), "two slots per lane: one-step rewards");
+  constexpr int APAD = S * M;
   constexpr int TRIO_W = TW;
   constexpr int TRIO_BLOCK = 3 * TW;
   constexpr int EPB = TRIO_W / S;
-  __shared__ TrioShared<S, TW> sh;
-  __shared__ EnvRecs<S> recs[EPB];
-  __shared__ mgn_asset_source s_src[S];
+  __shared__ TrioShared<S, TW, M> sh;
+  __shared__ EnvRecs<APAD> recs[EPB];
+  __shared__ mgn_asset_source s_src[APAD];
   __shared__ double s_tgt[MGN_MAX_ASSETS + 1];
   __shared__ double s_disc[NST ? MGN_MAX_NSTEP : 1];                     // NST: gamma^k
   extern __shared__ __attribute__((aligned(16))) double s_nst[];          // NST: (EPB, 2 nst_pad(n, S))
@@ -224,45 +281,51 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   // few envs, each kind's branch executed by the waves that hold it (the
   // Composite's Sine, OU and TrendOU branches no longer run in every
   // generator wave).  Records stay env-major: the lane publishes at el S + ls.
-  constexpr bool GSLOT = MGN_TRIO_GSLOT && GK < 0 && !RP && TW / S > 1;
+  constexpr bool GSLOT = MGN_TRIO_GSLOT && GK < 0 && !RP && TW / S > 1 && M == 1;
   const int el = (GSLOT && role == 0) ? l % EPB : l / S;
   const int ls = (GSLOT && role == 0) ? l / EPB : l % S;
-  const int lx = el * S + ls;  // the lane's (env, asset) record index
+  const int lx = (el * S + ls) * M;  // the lane's first (env, asset) slot record index
   const int env = blockIdx.x * EPB + el;
   const bool live = env < p.N;
   const int envc = live ? env : 0;
   const int A = p.A;
   Lane<M> s;
-  s.asset[0] = ls;
-  s.valid[0] = live && ls < A;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    s.asset[m] = ls * M + m;
+    s.valid[m] = live && ls * M + m < A;
+  }
   s.rcur = 0;
   s.row = 0;
   s.pf_ok = false;
-  s.fcol = (RP && p.F <= S) ? ls : -1;  // RP: one feature column per lane
-  const size_t li = (size_t)envc * A + (s.valid[0] ? ls : 0);
+  s.fcol = (RP && p.F <= APAD) ? ls * M : -1;  // RP: one feature column per slot
+  const size_t li = (size_t)envc * A + (s.valid[0] ? ls * M : 0);  // the lane's first slot (valid[m] => valid[0])
   // QREG: the handle's one source kind is known at compile time (GK), so the
   // generator lanes hold their asset's few parameters in registers, loaded
   // with the state (TrendOU: q[0..8], OU: q[0..2]) -- no LDS staging, and no
   // prologue barrier: every role starts its first iteration as soon as its
   // own state arrives (the one-step launch's prologue was two memory round
   // trips and a barrier before the orders could start)
-  constexpr int NQ = RP ? 0 : GK == MGN_SRC_TRENDOU ? 9 : GK == MGN_SRC_OU ? 3 : 0;
+  constexpr int NQ = (RP || M > 1) ? 0 : GK == MGN_SRC_TRENDOU ? 9 : GK == MGN_SRC_OU ? 3 : 0;
   constexpr bool QREG = NQ > 0;
   double qr[QREG ? NQ : 1];
   const double* const tgt_g = p.target;  // the PPC target in global memory (F's prologue)
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
 #ifdef MGN_TRIO_ABL_PRO
-  s.P[0] = 5.0;
+    s.P[m] = 5.0;
 #else
-  // the finish role takes its prices from the generator's LDS records
-  s.P[0] = (s.valid[0] && role != 2) ? kP[li] : 0.;
+    // the finish role takes its prices from the generator's LDS records
+    s.P[m] = (s.valid[m] && role != 2) ? kP[li + m] : 0.;
 #endif
-  s.L[0] = s.mep[0] = s.Bm[0] = s.sx[0] = s.oum[0] = s.dy[0] = 0.;
-  s.tlen[0] = 0;
-  s.tfl[0] = 0;
+    s.L[m] = s.mep[m] = s.Bm[m] = s.sx[m] = s.oum[m] = s.dy[m] = 0.;
+    s.tlen[m] = 0;
+    s.tfl[m] = 0;
+  }
   // role state, loaded before the parameter staging (one round trip)
   uint64_t ts = 0;                             // G
   double cash = 0.;                            // L
-  int act_cur = 0;                             // L
+  int act_cur[M] = {};                         // L
   const MGN_G int8_t* act_lane = vptr(act_in) + li;
   double ep_ret = 0., ep_len = 0., n_done = 0.;  // F
   double shA = 0., shB = 0.;                     // F
@@ -279,13 +342,16 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     constexpr bool r_oum = GK < 0 || GK == MGN_SRC_TRENDOU || GK == MGN_SRC_TRENDYOU || GK == MGN_SRC_OUPAIR;
     constexpr bool r_trend = GK < 0 || GK == MGN_SRC_TRENDOU || GK == MGN_SRC_SIMPLETREND ||
                              GK == MGN_SRC_TRENDYOU;
-    if (s.valid[0]) {
-      if (r_sx) s.sx[0] = p.sx[li];
-      if (r_oum) s.oum[0] = p.oum[li];
-      if (r_trend) {
-        s.dy[0] = p.dy[li];
-        s.tlen[0] = p.tlen[li];
-        s.tfl[0] = p.tfl[li];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      if (s.valid[m]) {
+        if (r_sx) s.sx[m] = p.sx[li + m];
+        if (r_oum) s.oum[m] = p.oum[li + m];
+        if (r_trend) {
+          s.dy[m] = p.dy[li + m];
+          s.tlen[m] = p.tlen[li + m];
+          s.tfl[m] = p.tfl[li + m];
+        }
       }
     }
     if constexpr (QREG) {
@@ -297,13 +363,19 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     s.dskip = p.dskip[envc];
     if (RP) s.rcur = p.rcur[envc];
   } else if (role == 1) {
-    if (s.valid[0]) {
-      s.L[0] = kL[li];
-      s.mep[0] = kmep[li];
-      s.Bm[0] = kBm[li];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      if (s.valid[m]) {
+        s.L[m] = kL[li + m];
+        s.mep[m] = kmep[li + m];
+        s.Bm[m] = kBm[li + m];
+      }
     }
     cash = kcash[envc];
-    if (in_kind == IN_DISCRETE && K > 0) act_cur = act_lane[0];
+    if (in_kind == IN_DISCRETE && K > 0) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) act_cur[m] = (m == 0 || s.valid[m]) ? act_lane[m] : 0;
+    }
   } else {
     ep_ret = p.ep[(size_t)envc * 2];
     ep_len = p.ep[(size_t)envc * 2 + 1];
@@ -312,7 +384,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       rhead = p.rhead[envc];
       rlen = p.rlen[envc];
     }
-    if (p.D == 1) {
+    if (M > 1 || p.D == 1) {  // M > 1: D = 1 (launch_trio)
       shA = p.sA[envc];
       shB = p.sB[envc];
     } else if (s.valid[0]) {
@@ -355,7 +427,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #endif
   if (!QREG || K == 0 || !MGN_TRIO_MORESKIP) __syncthreads();
   MGN_IT(1, 0);
-  s.kind[0] = s.valid[0] ? (QREG ? GK : s_src[ls].kind) : -1;
+#pragma unroll
+  for (int m = 0; m < M; ++m) s.kind[m] = s.valid[m] ? (QREG ? GK : s_src[s.asset[m]].kind) : -1;
 
   if (role == 0) {
     // ---------------- generator waves: tick of step j, State.price / timestamp
@@ -368,9 +441,17 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     int k = 0;
     // the source state before the last speculative tick (restored when F
     // finds that the previous step ended the episode)
-    double svP = 0., svSx = 0., svOum = 0., svDy = 0.;
-    int32_t svTlen = 0;
-    uint8_t svTfl = 0;
+    // (only the fields the kind's source reset leaves as they are: with GK
+    // known the others are overwritten by src_reset right after the restore)
+    constexpr bool SV_P = GK < 0 || !(GK == MGN_SRC_TRENDOU || GK == MGN_SRC_SIMPLETREND ||
+                                      GK == MGN_SRC_TRENDYOU || GK == MGN_SRC_OUPAIR);
+    constexpr bool SV_SX = GK < 0 || GK != MGN_SRC_TRENDYOU;
+    constexpr bool SV_OUM = GK < 0 || !(GK == MGN_SRC_TRENDOU || GK == MGN_SRC_TRENDYOU || GK == MGN_SRC_OUPAIR);
+    constexpr bool SV_TLEN = GK < 0 || !(GK == MGN_SRC_TRENDOU || GK == MGN_SRC_SIMPLETREND || GK == MGN_SRC_TRENDYOU);
+    constexpr bool SV_TFL = GK < 0 || GK != MGN_SRC_SIMPLETREND;
+    double svP[M] = {}, svSx[M] = {}, svOum[M] = {}, svDy[M] = {};
+    int32_t svTlen[M] = {};
+    uint8_t svTfl[M] = {};
     uint64_t svTs = 0;
     __builtin_amdgcn_s_setprio(MGN_TRIO_PG);
 #ifdef MGN_STAMPS
@@ -378,14 +459,14 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     int jn = 0;
 #endif
     int gpend = 0;  // WIN: refill ticks still to come after the reset tick
-    RpCur rp{0., 0, 0u};  // RP: the current State's tape row, feature, dataEnd
-    RpNext rnx{0., 0., 0, 0u};
+    RpCurM<M> rp{};  // RP: the current State's tape row, features, dataEnd
+    RpNextM<M> rnx{};
     // one tick: the tape row (RP; its timestamp) or the generator and ++ts
     auto tick = [&]() {
       if constexpr (RP) {
-        duo_replay_tick(s, p, ts, rp, rnx);
+        trio_replay_tick<M>(s, p, ts, rp, rnx);
       } else {
-        gen_tick<M, false, false, GK, true>(s, p, env, ts, QREG ? qr : nullptr);
+        gen_tick<M, false, false, GK, true, (M > 1)>(s, p, env, ts, QREG ? qr : nullptr);
         ts = ts + 1;
       }
     };
@@ -393,20 +474,24 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     // not stored (their value in HBM is the one loaded).  (Storing it in the
     // first idle iteration, under the finish role's last iteration, measured
     // 1-2.5 % slower per step: profiles/r03k_early_store_fast_rt_ab.txt.)
-    const int kd = GK >= 0 ? GK : s.kind[0];
-    const bool w_sx = kd == MGN_SRC_SINE || kd == MGN_SRC_SAWTOOTH || kd == MGN_SRC_TRIANGLE || kd == MGN_SRC_TRENDYOU;
-    const bool w_oum = kd == MGN_SRC_TRENDOU || kd == MGN_SRC_TRENDYOU || kd == MGN_SRC_OUPAIR;
-    const bool w_trend = kd == MGN_SRC_TRENDOU || kd == MGN_SRC_SIMPLETREND || kd == MGN_SRC_TRENDYOU;
     auto g_store = [&]() {
-      if (s.valid[0]) {
-        const size_t i = (size_t)env * A + s.asset[0];
-        p.P[i] = s.P[0];
-        if (w_sx) p.sx[i] = s.sx[0];
-        if (w_oum) p.oum[i] = s.oum[0];
-        if (w_trend) {
-          p.dy[i] = s.dy[0];
-          p.tlen[i] = s.tlen[0];
-          p.tfl[i] = s.tfl[0];
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const int kd = GK >= 0 ? GK : s.kind[m];
+        const bool w_sx =
+            kd == MGN_SRC_SINE || kd == MGN_SRC_SAWTOOTH || kd == MGN_SRC_TRIANGLE || kd == MGN_SRC_TRENDYOU;
+        const bool w_oum = kd == MGN_SRC_TRENDOU || kd == MGN_SRC_TRENDYOU || kd == MGN_SRC_OUPAIR;
+        const bool w_trend = kd == MGN_SRC_TRENDOU || kd == MGN_SRC_SIMPLETREND || kd == MGN_SRC_TRENDYOU;
+        if (s.valid[m]) {
+          const size_t i = (size_t)env * A + s.asset[m];
+          p.P[i] = s.P[m];
+          if (w_sx) p.sx[i] = s.sx[m];
+          if (w_oum) p.oum[i] = s.oum[m];
+          if (w_trend) {
+            p.dy[i] = s.dy[m];
+            p.tlen[i] = s.tlen[m];
+            p.tfl[i] = s.tfl[m];
+          }
         }
       }
       if (ls == 0) {
@@ -421,66 +506,82 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       if (live) {
         const bool rst = j > 0 && sh.reset[prv][el] != 0;
         const bool prev_step = j > 0 && (sh.rFlags[prv][el] & TR_STEP) != 0;
+        // every branch's tick is the one call below (one copy of the
+        // generator's code: the kind dispatch of every slot, inlined once)
+        bool tk = false, stepk = false;
         if (WIN && !rst && gpend > 0) {
           // a refill tick (not speculative: the reset is confirmed)
-          tick();
+          tk = true;
           gpend -= 1;
         } else if (RP && rst) {
           // the replay source carries on: the reset's getData reads the row the
           // voided speculative tick read, whose state stands; after a step that
           // was not speculated (none ran in the previous iteration) it reads the next
           if (prev_step) k -= 1;
-          else tick();
+          else tk = true;
           s.dskip += 1;  // Env::reset counts (the draw index; no draws from a tape)
           if (WIN) gpend = p.W - 1;
         } else if (rst) {
           if (prev_step) {  // roll the speculative tick back
-            s.P[0] = svP;
-            s.sx[0] = svSx;
-            s.oum[0] = svOum;
-            s.dy[0] = svDy;
-            s.tlen[0] = svTlen;
-            s.tfl[0] = svTfl;
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+              if (SV_P) s.P[m] = svP[m];
+              if (SV_SX) s.sx[m] = svSx[m];
+              if (SV_OUM) s.oum[m] = svOum[m];
+              s.dy[m] = svDy[m];
+              if (SV_TLEN) s.tlen[m] = svTlen[m];
+              if (SV_TFL) s.tfl[m] = svTfl[m];
+            }
             ts = svTs;
             k -= 1;
           }
           // Env::reset -> dataSource->reset + getData (Env.h:181-187)
           src_reset<M, false, GK>(s, p, env, ts, QREG ? qr : nullptr);
-          gen_tick<M, false, false, GK, true>(s, p, env, ts, QREG ? qr : nullptr);
-          ts = ts + 1;
+          tk = true;
           if (WIN) gpend = p.W - 1;
         } else if (k < K) {
           if (!RP) {
-            svP = s.P[0];
-            svSx = s.sx[0];
-            svOum = s.oum[0];
-            svDy = s.dy[0];
-            svTlen = s.tlen[0];
-            svTfl = s.tfl[0];
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+              if (SV_P) svP[m] = s.P[m];
+              if (SV_SX) svSx[m] = s.sx[m];
+              if (SV_OUM) svOum[m] = s.oum[m];
+              svDy[m] = s.dy[m];
+              if (SV_TLEN) svTlen[m] = s.tlen[m];
+              if (SV_TFL) svTfl[m] = s.tfl[m];
+            }
             svTs = ts;
           }
 #ifndef MGN_TRIO_ABL_G  // diagnostic timing build: no tick (prices frozen)
-          tick();
+          tk = true;
 #else
           ts = ts + 1;
 #endif
+          stepk = true;
+        }
+        if (tk) tick();
+        if (stepk) {
           // State.price and timestamp of step k (overwritten if rolled back)
           if (MGN_TRIO_GST) {
             const size_t oN = (size_t)k * p.N;
-            if (s.valid[0] && (om & O_OPR)) ost(ov.obs_price + ((oN + env) * (size_t)p.F + s.asset[0]), s.P[0]);
+#pragma unroll
+            for (int m = 0; m < M; ++m)
+              if (s.valid[m] && (om & O_OPR)) ost(ov.obs_price + ((oN + env) * (size_t)p.F + s.asset[m]), s.P[m]);
             if (ls == 0 && (om & O_TS)) ost(ov.timestamp + (oN + env), (uint64_t)ts);
           }
           k += 1;
         }
       }
-      sh.price[cur][lx] = s.P[0];
+#pragma unroll
+      for (int m = 0; m < M; ++m) sh.price[cur][lx + m] = s.P[m];
       if (!MGN_TRIO_GST && ls == 0) sh.ts[cur][el] = ts;
       if constexpr (RP) {
         if (ls == 0) {
           sh.row[cur][el] = rp.row;
           sh.dend[cur][el] = rp.dend;
         }
-        sh.feat[cur][l] = rp.curF;
+#pragma unroll
+        for (int m = 0; m < M; ++m) sh.feat[cur][lx + m] = rp.curF[m];
       }
       if (j == 0) MGN_IT(48, 0);
       MGN_T(T1);
@@ -534,11 +635,14 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     int lpend = 0;  // WIN: refill ticks still to come after the reset tick
     // the ledger write-back at exit
     auto l_store = [&]() {
-      if (s.valid[0]) {
-        const size_t i = (size_t)env * A + s.asset[0];
-        p.L[i] = s.L[0];
-        p.mep[i] = s.mep[0];
-        p.Bm[i] = s.Bm[0];
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        if (s.valid[m]) {
+          const size_t i = (size_t)env * A + s.asset[m];
+          p.L[i] = s.L[m];
+          p.mep[i] = s.mep[m];
+          p.Bm[i] = s.Bm[m];
+        }
       }
       if (ls == 0) p.cash[env] = cash;
     };
@@ -557,25 +661,34 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       if (WIN && !rst && lpend > 0) lpend -= 1;
       // prices of the last tick (the step's pre-tick prices; iteration 0:
       // the handle's current prices)
-      if (j > 0 && live && s.valid[0]) s.P[0] = sh.price[prv][l];
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        if (j > 0 && live && s.valid[m]) s.P[m] = sh.price[prv][lx + m];
       if (rst) {
         // the episode ended at the step F evaluated: the speculative step of
         // iteration j-1 is void; a fresh Broker (Env.h:181-187) waits for the
         // reset tick's prices
         if (prev_step) k -= 1;
-        s.L[0] = 0.;
-        s.mep[0] = 0.;
-        s.Bm[0] = 0.;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          s.L[m] = 0.;
+          s.mep[m] = 0.;
+          s.Bm[m] = 0.;
+        }
         cash = p.init_cash;
         if (WIN) lpend = p.W - 1;
       }
       const bool stepping = live && !rst && !refill && k < K;
-      const int act_now = act_cur;
+      int act_now[M];
+#pragma unroll
+      for (int m = 0; m < M; ++m) act_now[m] = act_cur[m];
       if (in_kind == IN_DISCRETE && K > 0) {
         // the action of the next step this lane runs (k + 1 if this one
         // steps; a rollback re-reads step k's, clamped in range)
         const int kn = k + (stepping ? 1 : 0);
-        act_cur = act_lane[kidx(kn < K ? kn : K - 1, act_step, 0)];
+        const MGN_G int8_t* ar = act_lane + kidx(kn < K ? kn : K - 1, act_step, 0);
+#pragma unroll
+        for (int m = 0; m < M; ++m) act_cur[m] = (m == 0 || s.valid[m]) ? ar[m] : 0;
       }
       int flags = 0;
       if (stepping) {
@@ -585,36 +698,53 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           s0 = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);  // after a reset tick
         } else {
           double tlp[M];
-          tlp[0] = s.L[0] * s.P[0];
+#pragma unroll
+          for (int m = 0; m < M; ++m) tlp[m] = s.L[m] * s.P[m];
           s0 = sa;
           s0.lp = canon<M, S>(tlp);
           if (j == 0) s0 = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
         }
         const double prevEq = (cash + s0.lp) - s0.b;  // Env.h:208
-        double uc[M], tp[M], tu[M], tc[M];
+        double uc[M], tp[M], tu[M], tc[M], prevVal[M];
         int rk[M];
-        tp[0] = 0.;
-        tu[0] = 0.;
-        tc[0] = 0.;
-        rk[0] = MGN_GREEN;
-        uc[0] = 0.;
         const size_t oN = (size_t)k * p.N, oNA = (size_t)k * p.N * A;
-        const double prevVal = s.L[0] * s.P[0];
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          tp[m] = 0.;
+          tu[m] = 0.;
+          tc[m] = 0.;
+          rk[m] = MGN_GREEN;
+          uc[m] = 0.;
+          prevVal[m] = s.L[m] * s.P[m];
+        }
         if (in_kind == IN_DISCRETE) {  // dqn.py:160-179
           const double bp = (cash + s0.sh) + (s0.lp - s0.ml);
           const double avM = RQ1 ? bp : bp / p.reqM;
           const int half = p.atoms / 2;
-          if (s.valid[0]) {
-            const double u = p.unit_size * avM / s.P[0];
-            uc[0] = (double)(act_now - half) * u;
-            if (act_now == 0) uc[0] = (s.L[0] != 0) ? -s.L[0] : 0.;
+#pragma unroll
+          for (int m = 0; m < M; ++m) {
+            if (s.valid[m]) {
+              const double u = p.unit_size * avM / s.P[m];
+              uc[m] = (double)(act_now[m] - half) * u;
+              if (act_now[m] == 0) uc[m] = (s.L[m] != 0) ? -s.L[m] : 0.;
+            }
           }
         } else if (in_kind == IN_UNITS) {
-          uc[0] = s.valid[0] ? gunits[oNA + (size_t)env * A + s.asset[0]] : 0.;
+#pragma unroll
+          for (int m = 0; m < M; ++m) uc[m] = s.valid[m] ? gunits[oNA + (size_t)env * A + s.asset[m]] : 0.;
         } else if (in_kind == IN_SINGLE) {
           const int ai = gaidx[env];
           const double u = gunits[oN + env];
-          uc[0] = (s.valid[0] && s.asset[0] == ai) ? u : 0.;
+#pragma unroll
+          for (int m = 0; m < M; ++m) uc[m] = (s.valid[m] && s.asset[m] == ai) ? u : 0.;
+        }
+        if constexpr (M > 1) {
+          // published before the orders (not live across them: the
+          // 168-register budget at two slots per lane)
+#pragma unroll
+          for (int m = 0; m < M; ++m)
+            if (need_ar) sh.rPv[cur][lx + m] = prevVal[m];
+          if (ls == 0) sh.rPrevEq[cur][el] = prevEq;
         }
         Sums after = s0;
         int any_mc = 0;
@@ -624,30 +754,36 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         if (in_kind != IN_NONE) {
 #endif
           if (j == 0) MGN_IT(52, TRIO_W);
-          broker_spec<S, RQ1, true>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, after, any_mc);
+          if constexpr (M == 1)
+            broker_spec<S, RQ1, true>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, after, any_mc);
+          else
+            broker_spec_m2<S, RQ1>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, after, any_mc);
           if (j == 0) MGN_IT(53, TRIO_W);
         }
         sa = after;
-        // BrokerResponse of step k (overwritten if rolled back)
-        if (MGN_TRIO_LST && s.valid[0]) {
-          const size_t i = oNA + (size_t)env * A + s.asset[0];
-          if (om & O_TP) ost(ov.tprice + i, tp[0]);
-          if (om & O_TU) ost(ov.tunits + i, tu[0]);
-          if (om & O_TC) ost(ov.tcost + i, tc[0]);
-          if (om & O_RISK) ost(ov.risk + i, (uint8_t)rk[0]);
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          // BrokerResponse of step k (overwritten if rolled back)
+          if (MGN_TRIO_LST && s.valid[m]) {
+            const size_t i = oNA + (size_t)env * A + s.asset[m];
+            if (om & O_TP) ost(ov.tprice + i, tp[m]);
+            if (om & O_TU) ost(ov.tunits + i, tu[m]);
+            if (om & O_TC) ost(ov.tcost + i, tc[m]);
+            if (om & O_RISK) ost(ov.risk + i, (uint8_t)rk[m]);
+          }
+          sh.rL[cur][lx + m] = s.L[m];
+          sh.rTp[cur][lx + m] = tp[m];
+          sh.rTu[cur][lx + m] = tu[m];
+          sh.rTc[cur][lx + m] = tc[m];
+          if (M == 1 && need_ar) sh.rPv[cur][lx + m] = prevVal[m];  // the agent reward's L * P before the orders
+          sh.rRk[cur][lx + m] = rk[m];
         }
-        sh.rL[cur][l] = s.L[0];
-        sh.rTp[cur][l] = tp[0];
-        sh.rTu[cur][l] = tu[0];
-        sh.rTc[cur][l] = tc[0];
-        if (need_ar) sh.rPv[cur][l] = prevVal;  // the agent reward's L * P before the orders
-        sh.rRk[cur][l] = rk[0];
         if (ls == 0) {
           sh.rCash[cur][el] = cash;
           sh.rMl[cur][el] = after.ml;
           sh.rSh[cur][el] = after.sh;
           sh.rB[cur][el] = after.b;
-          sh.rPrevEq[cur][el] = prevEq;
+          if (M == 1) sh.rPrevEq[cur][el] = prevEq;
           sh.rLpA[cur][el] = after.lp;
           sh.rK[cur][el] = k;
         }
@@ -658,7 +794,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       }
       if (WIN && refill) {
         // the refill row's portfolio (the fresh Broker's): F evaluates it
-        sh.rL[cur][l] = s.L[0];
+#pragma unroll
+        for (int m = 0; m < M; ++m) sh.rL[cur][lx + m] = s.L[m];
         if (ls == 0) {
           sh.rCash[cur][el] = cash;
           sh.rB[cur][el] = 0.;  // canonical sum of the fresh Broker's borrowed margins (+0)
@@ -717,15 +854,18 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   p.mainM = in_vgpr(p.mainM);
   p.eta = in_vgpr(p.eta);
   p.cos_temp = in_vgpr(p.cos_temp);
-  const int D = p.D;
+  const int D = M > 1 ? 1 : p.D;
   LedOut g;
   g.shA = shA;
   g.shB = shB;
   g.cos_qn = 0.;
   if (p.shaper == MGN_SHAPER_PPC) {
     double qq[M];
-    const double q = s.valid[0] ? tgt_g[1 + s.asset[0]] : 0.;
-    qq[0] = q * q;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const double q = s.valid[m] ? tgt_g[1 + s.asset[m]] : 0.;
+      qq[m] = q * q;
+    }
     g.cos_qn = sqrt(tgt_g[0] * tgt_g[0] + canon<M, S>(qq));
   }
   const bool need_ar = (p.reward_mode != MGN_REWARD_ENV_LOG) || (om & O_AREW);
@@ -735,7 +875,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   const uint32_t sN = (uint32_t)p.N, sNA = (uint32_t)p.N * (uint32_t)A, sNF = (uint32_t)p.N * (uint32_t)p.F,
                  sNA1 = (uint32_t)p.N * (uint32_t)(A + 1);
   const size_t bA = (size_t)env * A + s.asset[0], bP = (size_t)env * p.F + s.asset[0],
-               bO = (size_t)env * (A + 1);
+               bO = (size_t)env * (A + 1);  // slot m at + m
   // WIN: StackerDiscrete.stream_state of a State (preprocessor.py:172-175):
   // log-normalised (as the ring stores them) prices, ledgerNormedFull and the
   // timestamp into ring slot head + 1 and history row hcnt (ring_push's
@@ -744,12 +884,15 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   // lane's asset price, or (RP) the tape row's features (duo_feats' split:
   // one column per lane when F <= S, else read back per column); lg:
   // StackerDiscrete's log
-  const auto put_price = [&](MGN_G double* dst, double P, bool lg, int q) {
+  const auto put_price = [&](MGN_G double* dst, const double(&P)[M], bool lg, int q) {
     if constexpr (RP) {
       if (s.fcol >= 0) {
-        if (s.fcol < p.F) {
-          const double v = sh.feat[q][l];
-          ost(dst + s.fcol, lg ? log_norm(v) : v);
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          if (s.fcol + m < p.F) {
+            const double v = sh.feat[q][lx + m];
+            ost(dst + (s.fcol + m), lg ? log_norm(v) : v);
+          }
         }
       } else {
         const int64_t row = sh.row[q][el];
@@ -758,28 +901,39 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           ost(dst + f, lg ? log_norm(v) : v);
         }
       }
-    } else if (s.valid[0]) {
-      ost(dst + s.asset[0], lg ? log_norm(P) : P);
+    } else {
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        if (s.valid[m]) ost(dst + s.asset[m], lg ? log_norm(P[m]) : P[m]);
     }
   };
-  const auto push_row = [&](double P, double portA, double port0, uint64_t tsv, int kmark, int q) {
+  const auto push_row = [&](const double(&P)[M], const double(&portA)[M], double port0, uint64_t tsv, int kmark,
+                            int q) {
     rhead = (rhead + 1) % p.W;
     if (rlen < p.W) rlen += 1;
     const int R = p.F + A + 1;
     MGN_G double* row = gs.ring + ((size_t)env * p.W + rhead) * R;
     MGN_G double* hrow = p.hist ? gs.hist + ((size_t)env * p.hrows + hcnt) * R : nullptr;
-    if (!RP && s.valid[0]) {
-      // the lane's price column, normalised once for the ring and the history row
-      const double pv = p.ring_log != 0 ? log_norm(P) : P;
-      ost(row + s.asset[0], pv);
-      if (hrow) ost(hrow + s.asset[0], pv);
-    } else if (RP) {
+    if constexpr (RP) {
       put_price(row, P, p.ring_log != 0, q);
       if (hrow) put_price(hrow, P, p.ring_log != 0, q);
+    } else {
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        if (s.valid[m]) {
+          // the slot's price column, normalised once for the ring and the history row
+          const double pv = p.ring_log != 0 ? log_norm(P[m]) : P[m];
+          ost(row + s.asset[m], pv);
+          if (hrow) ost(hrow + s.asset[m], pv);
+        }
+      }
     }
-    if (s.valid[0]) {
-      ost(row + (p.F + 1 + s.asset[0]), portA);
-      if (hrow) ost(hrow + (p.F + 1 + s.asset[0]), portA);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      if (s.valid[m]) {
+        ost(row + (p.F + 1 + s.asset[m]), portA[m]);
+        if (hrow) ost(hrow + (p.F + 1 + s.asset[m]), portA[m]);
+      }
     }
     if (ls == 0) {
       ost(row + p.F, port0);
@@ -816,15 +970,19 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #endif
       const int k = sh.rK[prv][el];
       Lane<M> f = s;
-      f.L[0] = sh.rL[prv][l];
-      f.P[0] = sh.price[prv][l];
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        f.L[m] = sh.rL[prv][lx + m];
+        f.P[m] = sh.price[prv][lx + m];
+      }
       const double cashv = sh.rCash[prv][el];
       const double prevEq = sh.rPrevEq[prv][el];
       // post-tick sums, equity, reward, done (Env.h:211-223)
       Sums q;
       {
         double tlp[M];
-        tlp[0] = f.L[0] * f.P[0];
+#pragma unroll
+        for (int m = 0; m < M; ++m) tlp[m] = f.L[m] * f.P[m];
         q.lp = canon<M, S>(tlp);
       }
       q.ml = sh.rMl[prv][el];
@@ -836,23 +994,31 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       const double reward = log_ratio((ratio < clampv) ? clampv : ratio);
       const bool done = (flags & TR_ANYMC) || margin_call(q, cashv, p.mainM) || (curEq < 0.1 * p.init_cash);
       // ledgerNormedFull, agent reward, PPC, shaper (as k_step_duo's finish)
-      const double Lc = f.L[0], P = f.P[0];
-      double ar = 0.;
-      if (f.valid[0] && need_ar) {
-        double v = (((Lc * P) - sh.rPv[prv][l]) - (sh.rTu[prv][l] * sh.rTp[prv][l] + sh.rTc[prv][l])) / prevEq;
-        v += 1;
-        v = (v < .35) ? .35 : v;
-        ar = log_ratio(v);
-      }
+      double ar[M], portA[M];
       const double port0 = (cashv - q.b) / curEq;
-      const double portA = (Lc * P) / curEq;
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const double Lc = f.L[m], P = f.P[m];
+        ar[m] = 0.;
+        if (f.valid[m] && need_ar) {
+          const int x = lx + m;
+          double v = (((Lc * P) - sh.rPv[prv][x]) - (sh.rTu[prv][x] * sh.rTp[prv][x] + sh.rTc[prv][x])) / prevEq;
+          v += 1;
+          v = (v < .35) ? .35 : v;
+          ar[m] = log_ratio(v);
+        }
+        portA[m] = (Lc * P) / curEq;
+      }
       double cos_term = 0.;
       if (p.shaper == MGN_SHAPER_PPC) {
         double pp[M], pq[M];
-        const double qv = f.valid[0] ? s_tgt[1 + f.asset[0]] : 0.;
-        const double pv = f.valid[0] ? portA : 0.;
-        pp[0] = pv * pv;
-        pq[0] = pv * qv;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          const double qv = f.valid[m] ? s_tgt[1 + f.asset[m]] : 0.;
+          const double pv = f.valid[m] ? portA[m] : 0.;
+          pp[m] = pv * pv;
+          pq[m] = pv * qv;
+        }
         const double np_ = sqrt(port0 * port0 + canon<M, S>(pp));
         const double dot = port0 * s_tgt[0] + canon<M, S>(pq);
         cos_term = p.cos_temp * (dot / (np_ * g.cos_qn));
@@ -864,9 +1030,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         // replay_buffer.py:68-80) for the env's scalar column: append, pop once
         // when full, every entry on done; the row of step k (n entries, zero
         // after the pops) is stored here
-        double arr[M];
-        arr[0] = ar;
-        rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(arr) : reward;
+        rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
         const int n = p.nstep;
         double* ring = s_nst + (size_t)el * 2 * nst_pad(n, S);  // ring, then the pop's summands
         double* scr = ring + nst_pad(n, S);
@@ -970,9 +1134,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         while (nhead >= n) nhead -= n;
         nlen = L1 - pops;
       } else if (D == 1) {
-        double arr[M];
-        arr[0] = ar;
-        rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(arr) : reward;
+        rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
         if (p.shaper == MGN_SHAPER_DDR) {  // shape() for DDR (nstep_buffer.py:128-162)
           const double r = rin_s;
           shaped_s = clip1((0.0 + 1.0 * ddr_one_pre(r, g.shA, g.shB, ddr_pre(g.shA, g.shB))) / 1);
@@ -984,26 +1146,30 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           shaped_s = shape(p.shaper, rin_s, g.shA, g.shB, p.eta, cos_term, p.sexp);
         }
       } else {
-        shaped_v = f.valid[0] ? shape(p.shaper, ar, g.shA, g.shB, p.eta, cos_term, p.sexp) : 0.;
+        shaped_v = f.valid[0] ? shape(p.shaper, ar[0], g.shA, g.shB, p.eta, cos_term, p.sexp) : 0.;  // M = 1
       }
       // outputs of step k (the speculative runs never reach F)
 #ifndef MGN_ABL_NOSTORE_ASSET
-      if (f.valid[0]) {
-        const size_t i = kidx(k, sNA, bA);
-        if (!MGN_TRIO_LST) {
-          if (om & O_TP) ost(ov.tprice + i, sh.rTp[prv][l]);
-          if (om & O_TU) ost(ov.tunits + i, sh.rTu[prv][l]);
-          if (om & O_TC) ost(ov.tcost + i, sh.rTc[prv][l]);
-          if (om & O_RISK) ost(ov.risk + i, (uint8_t)sh.rRk[prv][l]);
-        }
-        if (!RP && !MGN_TRIO_GST && (om & O_OPR)) ost(ov.obs_price + kidx(k, sNF, bP), P);
-        if (om & O_OPT) ost(ov.obs_port + (kidx(k, sNA1, bO) + 1 + f.asset[0]), portA);
-        if (D != 1) {
-          if (om & O_AREW) ost(ov.agent_reward + i, ar);
-          if (om & O_SHP) ost(ov.shaped + i, shaped_v);
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        if (f.valid[m]) {
+          const size_t i = kidx(k, sNA, bA) + m;
+          const int x = lx + m;
+          if (!MGN_TRIO_LST) {
+            if (om & O_TP) ost(ov.tprice + i, sh.rTp[prv][x]);
+            if (om & O_TU) ost(ov.tunits + i, sh.rTu[prv][x]);
+            if (om & O_TC) ost(ov.tcost + i, sh.rTc[prv][x]);
+            if (om & O_RISK) ost(ov.risk + i, (uint8_t)sh.rRk[prv][x]);
+          }
+          if (!RP && !MGN_TRIO_GST && (om & O_OPR)) ost(ov.obs_price + (kidx(k, sNF, bP) + m), f.P[m]);
+          if (om & O_OPT) ost(ov.obs_port + (kidx(k, sNA1, bO) + 1 + f.asset[m]), portA[m]);
+          if (D != 1) {
+            if (om & O_AREW) ost(ov.agent_reward + i, ar[m]);
+            if (om & O_SHP) ost(ov.shaped + i, shaped_v);
+          }
         }
       }
-      if (RP && live && (om & O_OPR)) put_price(ov.obs_price + kidx(k, sNF, (size_t)env * p.F), P, false, prv);
+      if (RP && live && (om & O_OPR)) put_price(ov.obs_price + kidx(k, sNF, (size_t)env * p.F), f.P, false, prv);
 #endif
 #ifndef MGN_ABL_NOSTORE_ENV
       if (ls == 0) {
@@ -1027,7 +1193,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       }
 #endif
       if (WIN) {
-        push_row(P, portA, port0, (uint64_t)sh.ts[prv][el], k, prv);
+        push_row(f.P, portA, port0, (uint64_t)sh.ts[prv][el], k, prv);
         if (done && p.auto_reset) {  // a reset empties the window before its refill ticks
           rlen = 0;
           rhead = p.W - 1;
@@ -1053,13 +1219,18 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     if (WIN && live && (flags & TR_REFILL)) {
       // a refill tick's row: the fresh Broker's portfolio on the tick's prices
       // (the sums ring_push / k_step_duo's refill record evaluate)
-      const double Pf = sh.price[prv][l];
-      const double Lf = sh.rL[prv][l];
+      double Pf[M], Lf[M], tlp[M], pa[M];
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        Pf[m] = sh.price[prv][lx + m];
+        Lf[m] = sh.rL[prv][lx + m];
+        tlp[m] = Lf[m] * Pf[m];
+      }
       const double cashf = sh.rCash[prv][el], bf = sh.rB[prv][el];
-      double tlp[M];
-      tlp[0] = Lf * Pf;
       const double eq = (cashf + canon<M, S>(tlp)) - bf;
-      push_row(Pf, (Lf * Pf) / eq, (cashf - bf) / eq, (uint64_t)sh.ts[prv][el], klast, prv);
+#pragma unroll
+      for (int m = 0; m < M; ++m) pa[m] = (Lf[m] * Pf[m]) / eq;
+      push_row(Pf, pa, (cashf - bf) / eq, (uint64_t)sh.ts[prv][el], klast, prv);
     }
     if (ls == 0) sh.reset[cur][el] = rst_out;
     if (rst_out) sh.more[j % 3] = 1;  // the reset tick runs next iteration

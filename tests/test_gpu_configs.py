@@ -306,12 +306,13 @@ def test_rollout_launcher_matches_rollout(gpu, binding, monkeypatch):
     state_check(g, orc, f"launcher {binding}")
 
 
-def test_sixteen_assets_auto_schedule_vs_oracle(gpu):
+@pytest.mark.parametrize("N", [2048, 4096])
+def test_sixteen_assets_auto_schedule_vs_oracle(gpu, N):
     """16 TrendOU assets at the automatic schedule (the three-role kernel since
-    round 3: its ledger's broker trees behind scheduling fences), 20- and
-    64-step launches against the oracle: every output and the final state."""
+    round 3; at 4096 envs its two-slots-per-lane layout, launch_trio_m2), 20-
+    and 64-step launches against the oracle: every output and the final state."""
     from madigan_amd import _lib as L
-    N, A = 2048, 16
+    A = 16
     g, orc = make_pair(trendou_sources(A, TRENDOU_P), N, seed=0x6D6164 + 7, **C3_KW)
     assert g.lib.mgn_get_schedule(g.h) == L.SCHED_TRIO
     acts = g.generate_actions(20 + 64, seed=0x6D6164)

@@ -384,6 +384,58 @@ def test_schedules_bit_identical(gpu, A, kw):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("A,src,kw", [
+    (16, "trendou", dict(reward_shaper="DDR")),
+    (13, "trendou", dict(reward_shaper="DSR", reward_mode="agent_sum", window=6)),
+    (16, "mixed", dict(reward_shaper="PPC", cosine_temp=0.05, window=5, norm_type="log")),
+    (11, "mixed", dict(reward_shaper=None)),
+])
+def test_trio_two_slots_bit_identical(gpu, A, src, kw):
+    """The three-role kernel's two-slots-per-lane layout (launch_trio_m2: a
+    9..16-asset env on 8 lanes per role, at N x 16 >= 65536 lanes, discrete
+    steps, scalar reward) against the two-role kernel, bit for bit: speculative
+    steps rolled back at every auto-reset, windows with their refill rows,
+    padded slots (A < 16), a mixed-kind handle (the generic generator); then
+    unit and no-op steps on the same handle (the one-slot layout) and the
+    final state."""
+    from madigan_amd import BatchedEnv
+    from madigan_amd import _lib as L
+    N = 4096
+    base = dict(required_margin=0.02, maintenance_margin=0.25, transaction_cost_rel=0.02,
+                slippage_rel=1e-4, unit_size=0.9, auto_reset=True, init_cash=1e5, seed=23)
+    p = [0.2, 2, 6, 0.05, 0.2, 5.0, 0.15, 0.3, 0.2, 0.99]
+    mixed = composite_sources()[:5] + trendou_sources(3, p)
+    sources = trendou_sources(A, p) if src == "trendou" else [mixed[i % len(mixed)] for i in range(A)]
+    spec = spec_from_sources(sources)
+    units = np.random.default_rng(A).normal(0, 3e3, (N, A))
+    res = []
+    for sched in (L.SCHED_DUO, L.SCHED_TRIO):
+        g = BatchedEnv(spec, N, **base, **kw)
+        L.check(g.lib.mgn_set_schedule(g.h, sched), g.h)
+        assert g.lib.mgn_get_schedule(g.h) == sched
+        acts = g.generate_actions(25, seed=9)
+        out = {k: v.cpu().numpy() for k, v in g.rollout(acts[:24]).items()}
+        out.update({"k1_" + k: v.cpu().numpy() for k, v in g.rollout(acts[24:]).items()})
+        g.step(units)
+        out.update({"s_" + k: v for k, v in g.host_outputs().items()})
+        g.step()
+        out.update({"n_" + k: v for k, v in g.host_outputs().items()})
+        for name in ("ledger", "mean_entry", "borrowed", "cash", "prices", "timestamp", "episode_stats",
+                     "shaper_a", "shaper_b"):
+            out[name] = getattr(g, name).cpu().numpy()
+        if g.W:
+            out.update({"w_" + str(i): t.cpu().numpy() for i, t in enumerate(g.window())})
+        res.append(out)
+    assert res[0]["done"].sum() > 0, "no episode ended"
+    for k, v in res[0].items():
+        w = res[1][k]
+        if np.asarray(v).dtype == np.float64:
+            assert_bits(w, v, f"trio (two slots) vs duo {k}")
+        else:
+            assert np.array_equal(np.asarray(w), np.asarray(v)), f"trio (two slots) vs duo {k}"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("norm,W,N,sched", [(None, 8, 96, "duo"), ("log", 8, 96, "duo"),
                                             ("lookback", 6, 50, "single"), ("log", 8, 70, "single"),
                                             (None, 256, 20, "duo"), ("lookback_log", 1024, 12, "duo"),

@@ -35,7 +35,8 @@ def main():
         if base not in redo:
             return os.path.join(B.OBJ, base.replace(".hip", ".o"))
         obj = os.path.join(out_dir, base.replace(".hip", ".o"))
-        subprocess.run([cc, *B.FLAGS, "-DMGN_DIAG", *extra, "-c", "-o", obj, src], check=True)
+        subprocess.run([cc, *B.FLAGS, *B.UNIT_FLAGS.get(base, []), "-DMGN_DIAG", *extra, "-c", "-o", obj, src],
+                       check=True)
         return obj
 
     with ThreadPoolExecutor(4) as ex:

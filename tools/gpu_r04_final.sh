@@ -36,8 +36,9 @@ B256="python bench.py --steps 512 --warmup 256 --no-cpu-baseline --no-probe --no
 BC4="python bench.py --workload C4 --steps 128 --warmup 64 --no-cpu-baseline --no-probe --no-k-sweep"
 BC5="python bench.py --workload C5 --steps 128 --warmup 64 --no-cpu-baseline --no-probe --no-k-sweep"
 BC2="python bench.py --workload C2 --steps 128 --warmup 64 --no-cpu-baseline --no-probe --no-k-sweep"
-for tag in 20 1 256 C2 C4 C5; do
-  case $tag in 20) B=$B20;; 1) B=$B1;; 256) B=$B256;; C2) B=$BC2;; C4) B=$BC4;; C5) B=$BC5;; esac
+BA16="python bench.py --assets 16 --steps 128 --warmup 64 --fuse 64 --no-cpu-baseline --no-probe --no-k-sweep"
+for tag in 20 1 256 C2 C4 C5 a16; do
+  case $tag in 20) B=$B20;; 1) B=$B1;; 256) B=$B256;; C2) B=$BC2;; C4) B=$BC4;; C5) B=$BC5;; a16) B=$BA16;; esac
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt$tag -o kt -- $B > $O/kt$tag.log 2>&1 || { echo "kt$tag failed"; tail -20 $O/kt$tag.log; exit 1; }
   timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc$tag/fetch -o p -- $B > $O/pmc${tag}_fetch.log 2>&1 || { echo "pmc fetch $tag failed"; tail -20 $O/pmc${tag}_fetch.log; exit 1; }
   timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc$tag/write -o p -- $B > $O/pmc${tag}_write.log 2>&1 || { echo "pmc write $tag failed"; tail -20 $O/pmc${tag}_write.log; exit 1; }

@@ -312,6 +312,8 @@ def main():
     ap.add_argument("--fuse", type=int, default=256)
     ap.add_argument("--win-fuse", type=int, default=64,
                     help="steps per launch of the windowed workloads (capped by --fuse)")
+    ap.add_argument("--win-assets", type=int, default=0,
+                    help="C2 only (diagnostic): OU assets per env, at --n-envs envs")
     ap.add_argument("--win-overlap", action="store_true",
                     help="windowed workloads: gather on a second stream beside the next step launch")
     ap.add_argument("--n-envs", type=int, default=8192, help="envs per GPU")
@@ -630,6 +632,9 @@ def windowed(args, world, rank, dev):
     wl = args.workload
     N = {"C2": 4096}.get(wl, args.n_envs)
     A = {"C2": 4, "C4": 8, "C5": 16}[wl]
+    if wl == "C2" and args.win_assets:
+        # diagnostic: OU windows at another asset count, at --n-envs envs
+        N, A = args.n_envs, args.win_assets
     env, desc, W = workload_env(wl, N, A, rank, dev)
     Kf = max(1, min(args.fuse, args.win_fuse))
     n_warm = max(1, -(-args.warmup // Kf))

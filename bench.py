@@ -464,18 +464,23 @@ def main():
     if rank == 0 and args.k_sweep:
         stream = torch.cuda.current_stream(dev)
         big = env.alloc_traj(256, fields=list(traj.keys()))
-        # every launch reads K steps of actions (K, N, A) from sw_base
-        sw_actions = env.generate_actions(256, seed=0x6D6165)
-        sw_base = sw_actions.data_ptr()
+        # launch r reads the K steps of fresh actions (K, N, A) at step r K mod
+        # T, as an agent loop's launches do (one action row repeated launch
+        # after launch drives every env into margin calls and auto-resets,
+        # whose rollback iterations lengthen the short launches)
+        T = 1024
+        sw_actions = env.generate_actions(T, seed=0x6D6165)
+        sw_base, sw_row = sw_actions.data_ptr(), N * A * sw_actions.element_size()
         for K in ((1, 16, 64, 256) if args.sweep else (1, 16, 256)):
-            assert sw_actions.shape[0] >= K
+            assert T % K == 0
             reps = max(4, 512 // K)
+            ptr = [sw_base + ((r * K) % T) * sw_row for r in range(2 * reps + 1)]
             fn = env.rollout_launcher({kk: v[:K] for kk, v in big.items()}, K)
-            fn(sw_base)  # warm
+            fn(ptr[-1])  # warm
             torch.cuda.synchronize()
             L.check(lib.mgn_set_timing(h, 2), h)
             for r in range(reps):
-                fn(sw_base)
+                fn(ptr[r])
             torch.cuda.synchronize()
             tk = (C.c_double * 4)()
             L.check(lib.mgn_get_timing(h, tk), h)
@@ -484,7 +489,7 @@ def main():
             s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s_ev.record(stream)
             for r in range(reps):
-                fn(sw_base)
+                fn(ptr[reps + r])
             e_ev.record(stream)
             torch.cuda.synchronize()
             us = s_ev.elapsed_time(e_ev) * 1e3 / (reps * K)

@@ -89,6 +89,20 @@ constexpr int TRIO_W = 256;  // lanes per role
 #define MGN_TRIO_GSLOT 1
 #endif
 
+// one-step launches (the agent loop): an auto-reset after the step absorbed
+// in the iteration that finds it (no window, generator sources): the
+// generator role, idle once its tick is done, forms the reset tick's state
+// beside the finish role's evaluation, and the generator / ledger roles adopt
+// it (or drop it) after the loop, where the reset took another iteration --
+// in about half of the one-step launches at C3 some workgroup has one.
+// Measured: K = 1 7.30-7.40 -> 7.20-7.23 us; at 16- and 20-step launches the
+// candidate tick under the finish role's last iteration cost 1-2 %, so longer
+// launches run the reset in an iteration of its own
+// (profiles/r04_ab_tail_reset.txt)
+#ifndef MGN_TRIO_TAILRST
+#define MGN_TRIO_TAILRST 1
+#endif
+
 // NST: the pop's ordered sum read back by the env's first lane only
 #ifndef MGN_NST_SUM1
 #define MGN_NST_SUM1 1
@@ -238,6 +252,24 @@ inline size_t trio_nst_dyn_lds(int S, int TW, int nstep) {
 // replay source carries on through a reset (DataSource.cpp:200-206), so the
 // reset's getData reads the row the voided speculative tick read: a rollback
 // keeps the tick's state as the reset tick's.
+// the generator state of a lane's slots (what src_reset / gen_tick change),
+// field by field: a whole-struct copy of Lane went through scratch memory.
+// The variate cache (zc, ztag) is not state: an entry is the draw its tag
+// names whichever tick cached it, so a dropped candidate's entry stays valid
+template <int M>
+__device__ __forceinline__ void gen_state_copy(Lane<M>& d, const Lane<M>& s) {
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    d.P[m] = s.P[m];
+    d.sx[m] = s.sx[m];
+    d.oum[m] = s.oum[m];
+    d.dy[m] = s.dy[m];
+    d.tlen[m] = s.tlen[m];
+    d.tfl[m] = s.tfl[m];
+  }
+  d.dskip = s.dskip;
+}
+
 // MM: asset slots per lane (2: a 16-asset env on 8 lanes per role, so 8192
 // envs fit one workgroup per CU; slots ls MM + m in the canonical order, the
 // ledger's broker_spec_m2; one-step rewards with a scalar shaper, D = 1)
@@ -261,6 +293,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   MGN_IT(47, 0);
   const int in_kind = DISC ? IN_DISCRETE : in_kind_rt;
   constexpr int M = MM;
+  constexpr bool TAIL = MGN_TRIO_TAILRST && !RP && !WIN;
   static_assert(M == 1 || (M == 2 && !NST), "two slots per lane: one-step rewards");
   constexpr int APAD = S * M;
   constexpr int TRIO_W = TW;
@@ -453,6 +486,13 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     int32_t svTlen[M] = {};
     uint8_t svTfl[M] = {};
     uint64_t svTs = 0;
+    // TAIL: the state before the tail reset candidate (s holds the candidate
+    // while `shadow`), and the last iteration
+    Lane<M> s2;
+    gen_state_copy<M>(s2, s);
+    uint64_t ts2 = 0;
+    bool shadow = false;
+    int jlast = 0;
     __builtin_amdgcn_s_setprio(MGN_TRIO_PG);
 #ifdef MGN_STAMPS
     unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0;
@@ -504,6 +544,15 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       MGN_T(T0);
       if (threadIdx.x == 0) sh.more[(j + 1) % 3] = 0;
       if (live) {
+        if constexpr (TAIL) {
+          // another iteration: the previous one's candidate is dropped (a
+          // reset found there is run below as any other)
+          if (shadow) {
+            gen_state_copy<M>(s, s2);
+            ts = ts2;
+            shadow = false;
+          }
+        }
         const bool rst = j > 0 && sh.reset[prv][el] != 0;
         const bool prev_step = j > 0 && (sh.rFlags[prv][el] & TR_STEP) != 0;
         // every branch's tick is the one call below (one copy of the
@@ -558,6 +607,15 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           ts = ts + 1;
 #endif
           stepk = true;
+        } else if (TAIL && K == 1) {
+          // idle (the launch's ticks done, no reset pending): the candidate of
+          // a reset the finish role may find in this iteration -- Env::reset's
+          // source reset and getData on the final state, kept in s2
+          gen_state_copy<M>(s2, s);
+          ts2 = ts;
+          shadow = true;
+          src_reset<M, false, GK>(s, p, env, ts, QREG ? qr : nullptr);
+          tk = true;
         }
         if (tk) tick();
         if (stepk) {
@@ -593,6 +651,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       acc1 += T2 - T1;
       jn = j;
 #endif
+      jlast = j;
       if (trio_exit(j, K, sh.more[j % 3])) break;
     }
 #ifdef MGN_STAMPS
@@ -606,6 +665,14 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #ifdef MGN_TRIO_ABL_EPI  // diagnostic timing build: no state write-back
     return;
 #endif
+    if constexpr (TAIL) {
+      // the last iteration's candidate stands where the finish role found the
+      // episode's end there (a tail reset: it raised no further iteration)
+      if (live && shadow && !sh.reset[jlast & 1][el]) {
+        gen_state_copy<M>(s, s2);
+        ts = ts2;
+      }
+    }
     if (live) {
       g_store();
       if (RP && ls == 0) p.rcur[env] = s.rcur;
@@ -633,6 +700,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     MGN_IT(51, TRIO_W);
     int k = 0;
     int lpend = 0;  // WIN: refill ticks still to come after the reset tick
+    int jlast = 0;  // TAIL: the last iteration
     // the ledger write-back at exit
     auto l_store = [&]() {
 #pragma unroll
@@ -803,8 +871,11 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         flags = TR_REFILL;
       }
       if (ls == 0) sh.rFlags[cur][el] = flags;
-      // another iteration: F evaluates this step, or steps remain
-      if (live && (stepping || rst || refill || k < K || (WIN && lpend > 0))) sh.more[j % 3] = 1;
+      // another iteration: F evaluates this step, or steps remain (a reset
+      // that voided nothing leaves none: its tick ran in this iteration;
+      // WIN: its refill rows follow)
+      if (live && (stepping || refill || k < K || (WIN && (rst || lpend > 0)))) sh.more[j % 3] = 1;
+      jlast = j;
       if (j == 0) MGN_IT(49, TRIO_W);
       MGN_T(T1);
       __syncthreads();
@@ -827,6 +898,19 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #ifdef MGN_TRIO_ABL_EPI  // diagnostic timing build: no state write-back
     return;
 #endif
+    if constexpr (TAIL) {
+      // a tail reset (the finish role found the episode's end in the last
+      // iteration): the fresh Broker (Env.h:181-187)
+      if (live && sh.reset[jlast & 1][el]) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          s.L[m] = 0.;
+          s.mep[m] = 0.;
+          s.Bm[m] = 0.;
+        }
+        cash = p.init_cash;
+      }
+    }
     if (live) l_store();
     MGN_IT_DRAIN();
     MGN_IT(45, TRIO_W);
@@ -961,6 +1045,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     const int cur = j & 1, prv = cur ^ 1;
     MGN_T(T0);
     int rst_out = 0;
+    bool tail_rst = false;  // TAIL: the launch's last step ended its episode
     // the step L ran in iteration j-1, unless F voided it at iteration j-1
     const int flags = j > 0 ? sh.rFlags[prv][el] : 0;
 #ifdef MGN_TRIO_ABL_F  // diagnostic timing build: no step finish, no outputs
@@ -1213,7 +1298,10 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         }
         ep_ret = 0;
         ep_len = 0;
-        if (p.auto_reset) rst_out = 1;
+        if (p.auto_reset) {
+          rst_out = 1;
+          tail_rst = TAIL && K == 1;
+        }
       }
     }
     if (WIN && live && (flags & TR_REFILL)) {
@@ -1233,7 +1321,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       push_row(Pf, pa, (cashf - bf) / eq, (uint64_t)sh.ts[prv][el], klast, prv);
     }
     if (ls == 0) sh.reset[cur][el] = rst_out;
-    if (rst_out) sh.more[j % 3] = 1;  // the reset tick runs next iteration
+    // the reset tick runs next iteration -- a tail reset's in this one, by the
+    // idle generator role (adopted after the loop)
+    if (rst_out && !tail_rst) sh.more[j % 3] = 1;
     if (j == 1) MGN_IT(50, 2 * TRIO_W);
     MGN_T(T1);
     __syncthreads();

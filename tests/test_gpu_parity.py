@@ -436,6 +436,43 @@ def test_trio_two_slots_bit_identical(gpu, A, src, kw):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("A,N,K", [(8, 512, 1), (8, 512, 3), (16, 4096, 1), (4, 300, 1)])
+def test_trio_tail_resets_bit_identical(gpu, A, N, K):
+    """Short launches whose last step ends episodes (a leveraged, costly
+    broker: auto-resets in most launches): the three-role kernel absorbs such a
+    tail reset after its loop (the generator's candidate reset tick, the fresh
+    Broker) -- every output and the whole state after each launch equal the
+    two-role kernel's, bit for bit, launch after launch."""
+    from madigan_amd import BatchedEnv
+    from madigan_amd import _lib as L
+    base = dict(required_margin=0.02, maintenance_margin=0.25, transaction_cost_rel=0.02,
+                slippage_rel=1e-4, unit_size=0.9, auto_reset=True, init_cash=1e5, seed=29,
+                reward_shaper="DDR")
+    spec = spec_from_sources(trendou_sources(A, [0.2, 2, 6, 0.05, 0.2, 5.0, 0.15, 0.3, 0.2, 0.99]))
+    n_launch = 24
+    res = []
+    for sched in (L.SCHED_DUO, L.SCHED_TRIO):
+        g = BatchedEnv(spec, N, **base)
+        L.check(g.lib.mgn_set_schedule(g.h, sched), g.h)
+        acts = g.generate_actions(n_launch * K, seed=13)
+        outs = []
+        for i in range(n_launch):
+            o = {k: v.cpu().numpy() for k, v in g.rollout(acts[i * K:(i + 1) * K]).items()}
+            for name in ("ledger", "mean_entry", "borrowed", "cash", "prices", "timestamp", "episode_stats",
+                         "shaper_a", "shaper_b", "draw_skip"):
+                o[name] = getattr(g, name).cpu().numpy()
+            outs.append(o)
+        res.append(outs)
+    assert sum(int(o["done"].sum()) for o in res[0]) > n_launch // 2, "too few episode ends"
+    for i, (a, b) in enumerate(zip(*res)):
+        for k, v in a.items():
+            if np.asarray(v).dtype == np.float64:
+                assert_bits(b[k], v, f"launch {i} trio vs duo {k}")
+            else:
+                assert np.array_equal(np.asarray(b[k]), np.asarray(v)), f"launch {i} trio vs duo {k}"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("norm,W,N,sched", [(None, 8, 96, "duo"), ("log", 8, 96, "duo"),
                                             ("lookback", 6, 50, "single"), ("log", 8, 70, "single"),
                                             (None, 256, 20, "duo"), ("lookback_log", 1024, 12, "duo"),

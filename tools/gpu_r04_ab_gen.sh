@@ -9,6 +9,8 @@ rm -rf $O; mkdir -p $O
 args_of() {
   case $1 in
     C3_20) echo "--fuse 20 --steps 2000 --warmup 200" ;;
+    k1) echo "--fuse 1 --steps 512 --warmup 64" ;;
+    k16) echo "--fuse 16 --steps 1024 --warmup 64" ;;
     C3_256) echo "--fuse 256 --steps 2048 --warmup 256" ;;
     a16) echo "--assets 16 --fuse 64 --steps 512 --warmup 64" ;;
     a16_20) echo "--assets 16 --fuse 20 --steps 500 --warmup 60" ;;

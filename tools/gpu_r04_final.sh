@@ -13,6 +13,8 @@ export TMPDIR=/tmp
 O=gpurun_out/r04final
 mkdir -p $O
 PT="python -u -m pytest -v --timeout 180 --timeout-method thread -p no:cacheprovider"
+# PART=a: tests, smoke and bench lines; PART=b: the rocprof traces and PMC passes (gpurun's 1200 s limit)
+if [ "${PART:-a}" = a ]; then
 timeout -k 10 900 $PT -m gpu tests > $O/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -30 $O/pytest_gpu.log; exit 1; }
 tail -2 $O/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -30 $O/smoke.log; exit 1; }
@@ -30,6 +32,8 @@ run bench_a16 300 python bench.py --steps 512 --warmup 64 --fuse 64 --assets 16 
 for w in C2 C4 C5; do
   run bench_$w 600 python bench.py --workload $w --steps 256 --warmup 64 --no-cpu-baseline --no-k-sweep
 done
+fi
+if [ "${PART:-a}" = b ]; then
 B20="python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-probe --no-k-sweep"
 B1="python bench.py --steps 64 --warmup 8 --fuse 1 --no-cpu-baseline --no-probe --no-k-sweep"
 B256="python bench.py --steps 512 --warmup 256 --no-cpu-baseline --no-probe --no-k-sweep"
@@ -44,4 +48,5 @@ for tag in 20 1 256 C2 C4 C5 a16; do
   timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc$tag/write -o p -- $B > $O/pmc${tag}_write.log 2>&1 || { echo "pmc write $tag failed"; tail -20 $O/pmc${tag}_write.log; exit 1; }
   timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_WAVES --output-format csv -d $O/pmc$tag/sq -o p -- $B > $O/pmc${tag}_sq.log 2>&1 || { echo "pmc sq $tag failed"; tail -20 $O/pmc${tag}_sq.log; exit 1; }
 done
-echo r04final done
+fi
+echo r04final ${PART:-a} done

@@ -65,7 +65,8 @@ def main():
             ("C4", "k_hist_gather", "mean", "C4_gather_8192x8_W64", 8192 * 64),
             ("C4", "k_step", "mean", "C4_step_8192x8_fuse64", 8192 * 64),
             ("C5", "k_hist_gather", "mean", "C5_gather_8192x16_W64", 8192 * 64),
-            ("C5", "k_step", "mean", "C5_step_8192x16_fuse64", 8192 * 64)]
+            ("C5", "k_step", "mean", "C5_step_8192x16_fuse64", 8192 * 64),
+            ("a16", "k_step", "mean", "C3_trendou_8192x16_fuse64", 8192 * 64)]
     for tag, match, pick, key, units in plan:
         m = merged(a.src, tag, match, pick)
         if not m:
@@ -81,7 +82,7 @@ def main():
             s["valu_wave_insts_per_wave_step"] = m["SQ_INSTS_VALU"] / m["SQ_WAVES"] / steps
             s["wait_any_frac"] = m["SQ_WAIT_ANY"] / m["SQ_WAVE_CYCLES"]
         summary[key] = s
-    for tag in ("20", "1", "256", "C2", "C4", "C5"):
+    for tag in ("20", "1", "256", "C2", "C4", "C5", "a16"):
         ks = os.path.join(a.src, f"kt{tag}", "kt_kernel_stats.csv")
         if os.path.exists(ks):
             shutil.copy(ks, os.path.join(prof, f"{a.tag}_kernel_stats_{tag}.csv"))

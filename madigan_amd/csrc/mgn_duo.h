@@ -468,7 +468,7 @@ __device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s,
     // StackerDiscrete.stream_state of the State (preprocessor.py:172-175):
     // (L * P) / equity and (cash - borrowed) / equity, the values ring_push
     // computes from the same sums
-    g.head = (g.head + 1) % p.W;
+    g.head = (g.head + 1 == p.W) ? 0 : g.head + 1;
     if (g.len < p.W) g.len += 1;
     const int R = p.F + p.A + 1;
     MGN_G double* row = gs.ring + ((size_t)env * p.W + g.head) * R;

@@ -589,7 +589,7 @@ __device__ __forceinline__ void ring_push(const Lane<M>& s, const KParams& p, in
                                           int hcnt = -1) {
   const Sums q = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
   const double eq = (cash + q.lp) - q.b;
-  head = (head + 1) % p.W;
+  head = (head + 1 == p.W) ? 0 : head + 1;
   if (len < p.W) len += 1;
   const int R = p.F + p.A + 1;
   double* row = p.ring + ((size_t)env * p.W + head) * R;

@@ -103,6 +103,12 @@ constexpr int TRIO_W = 256;  // lanes per role
 #define MGN_TRIO_TAILRST 1
 #endif
 
+// WIN with a log window: the generator role forms the window rows' log
+// prices (the finish role reads them from LDS)
+#ifndef MGN_TRIO_GLOG
+#define MGN_TRIO_GLOG 1
+#endif
+
 // NST: the pop's ordered sum read back by the env's first lane only
 #ifndef MGN_NST_SUM1
 #define MGN_NST_SUM1 1
@@ -166,6 +172,9 @@ struct TrioShared {
   int64_t row[2][EPB];
   uint32_t dend[2][EPB];
   double feat[2][NSL];
+  // WIN with a log window (MGN_TRIO_GLOG): the tick's log-normalised prices,
+  // formed by the generator role for the finish role's window rows
+  double lprice[2][NSL];
 };
 
 // LDS of k_step_trio<S, ..., TW, NST, ..., M>: its static arrays (an upper
@@ -293,7 +302,10 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   MGN_IT(47, 0);
   const int in_kind = DISC ? IN_DISCRETE : in_kind_rt;
   constexpr int M = MM;
-  constexpr bool TAIL = MGN_TRIO_TAILRST && !RP && !WIN;
+  // (not at two slots per lane with a mixed-kind generator: the candidate's
+  // copy of every field of both slots spilled at the 168-register budget)
+  constexpr bool TAIL = MGN_TRIO_TAILRST && !RP && !WIN && (MM == 1 || GK >= 0);
+  constexpr bool GLOG = MGN_TRIO_GLOG && WIN && !RP;
   static_assert(M == 1 || (M == 2 && !NST), "two slots per lane: one-step rewards");
   constexpr int APAD = S * M;
   constexpr int TRIO_W = TW;
@@ -632,6 +644,14 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       }
 #pragma unroll
       for (int m = 0; m < M; ++m) sh.price[cur][lx + m] = s.P[m];
+      if constexpr (GLOG) {
+        // the window row's log price (StackerDiscrete's log normaliser,
+        // preprocessor.py:79-81) off the finish role's chain
+        if (p.ring_log != 0) {
+#pragma unroll
+          for (int m = 0; m < M; ++m) sh.lprice[cur][lx + m] = log_norm(s.P[m]);
+        }
+      }
       if (!MGN_TRIO_GST && ls == 0) sh.ts[cur][el] = ts;
       if constexpr (RP) {
         if (ls == 0) {
@@ -993,7 +1013,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   };
   const auto push_row = [&](const double(&P)[M], const double(&portA)[M], double port0, uint64_t tsv, int kmark,
                             int q) {
-    rhead = (rhead + 1) % p.W;
+    rhead = (rhead + 1 == p.W) ? 0 : rhead + 1;  // (rhead in [0, W): no integer division)
     if (rlen < p.W) rlen += 1;
     const int R = p.F + A + 1;
     MGN_G double* row = gs.ring + ((size_t)env * p.W + rhead) * R;
@@ -1006,7 +1026,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       for (int m = 0; m < M; ++m) {
         if (s.valid[m]) {
           // the slot's price column, normalised once for the ring and the history row
-          const double pv = p.ring_log != 0 ? log_norm(P[m]) : P[m];
+          const double pv = p.ring_log == 0 ? P[m] : (GLOG ? sh.lprice[q][lx + m] : log_norm(P[m]));
           ost(row + s.asset[m], pv);
           if (hrow) ost(hrow + s.asset[m], pv);
         }

@@ -436,8 +436,10 @@ def test_trio_two_slots_bit_identical(gpu, A, src, kw):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("A,N,K", [(8, 512, 1), (8, 512, 3), (16, 4096, 1), (4, 300, 1)])
-def test_trio_tail_resets_bit_identical(gpu, A, N, K):
+@pytest.mark.parametrize("A,N,K,kw", [(8, 512, 1, {}), (8, 512, 3, {}), (16, 4096, 1, {}), (4, 300, 1, {}),
+                                       (8, 512, 1, dict(nstep_return=5, discount=0.9)),
+                                       (4, 300, 1, dict(reward_shaper="PPC", cosine_temp=0.05))])
+def test_trio_tail_resets_bit_identical(gpu, A, N, K, kw):
     """Short launches whose last step ends episodes (a leveraged, costly
     broker: auto-resets in most launches): the three-role kernel absorbs such a
     tail reset after its loop (the generator's candidate reset tick, the fresh
@@ -452,7 +454,7 @@ def test_trio_tail_resets_bit_identical(gpu, A, N, K):
     n_launch = 24
     res = []
     for sched in (L.SCHED_DUO, L.SCHED_TRIO):
-        g = BatchedEnv(spec, N, **base)
+        g = BatchedEnv(spec, N, **{**base, **kw})
         L.check(g.lib.mgn_set_schedule(g.h, sched), g.h)
         acts = g.generate_actions(n_launch * K, seed=13)
         outs = []

@@ -16,6 +16,7 @@ args_of() {
     a16_20) echo "--assets 16 --fuse 20 --steps 500 --warmup 60" ;;
     C5) echo "--workload C5 --steps 256 --warmup 64" ;;
     C4) echo "--workload C4 --steps 256 --warmup 64" ;;
+    C2) echo "--workload C2 --steps 256 --warmup 64" ;;
     n20) echo "--nstep 20 --fuse 64 --steps 512 --warmup 64" ;;
     *) echo "unknown shape $1" >&2; return 1 ;;
   esac

@@ -29,7 +29,9 @@ def main():
     A = int(os.environ.get("ASSETS", 8))
     env, _, _ = bench.workload_env(wl, N, A, 0, "cuda:0", **(extra if wl == "C3" else {}))
     assert int(env.lib.mgn_get_schedule(env.h)) == L.SCHED_TRIO
-    fn = env.lib.mgn_diag_stamps
+    # the two-slot kernels (9..16 assets at >= 4096 envs) keep their stamps in
+    # their own unit (mgn_launch_a16m2.hip)
+    fn = env.lib.mgn_diag_stamps_m2 if env.A > 8 and N * 16 >= 65536 else env.lib.mgn_diag_stamps
     fn.argtypes = [C.POINTER(C.c_ulonglong)]
     acts = env.generate_actions(fuse, seed=5)
     out = env.alloc_traj(fuse, fields=["reward", "shaped", "done", "obs_price", "obs_port", "timestamp",

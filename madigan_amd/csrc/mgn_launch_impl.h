@@ -154,7 +154,10 @@ void launch_trio(const StepArgs& a) {
     return;
   }
   if (a.p.nstep > 1) {  // NST: the finish role's NStepBuffer rings in dynamic LDS (no window, D = 1)
-    const size_t lds = trio_nst_dyn_lds(S, small ? 64 : TRIO_W, a.p.nstep);
+    // the kind-specialized instantiation keeps a third pad per env for the
+    // generator's prefix summands (MGN_NST_GPFX)
+    const bool gpfx = MGN_NST_GPFX && !small && disc && a.gkind == MGN_SRC_TRENDOU;
+    const size_t lds = trio_nst_dyn_lds(S, small ? 64 : TRIO_W, a.p.nstep, gpfx);
     auto goN = [&](auto kern) {
       // a refused size is the caller's hipGetLastError (HIP records every
       // call's status); trio_eligible keeps static + dynamic LDS within 160 KiB

@@ -109,6 +109,17 @@ constexpr int TRIO_W = 256;  // lanes per role
 #define MGN_TRIO_GLOG 1
 #endif
 
+// NST (generator sources of one kind): the first pop's summands over the
+// entries already in the ring, and their ordered sum, formed by the generator
+// role at the start of the iteration while the finish role forms the step's
+// reward; the finish role waits for it (an LDS stamp) and adds the new
+// entry's summand -- the same operations in the same order.  Bit-identical
+// but neutral at n = 20 DDR (3.76-3.80 vs 3.80-3.81 us/step,
+// profiles/r04_ab_nst_prefix.txt): off
+#ifndef MGN_NST_GPFX
+#define MGN_NST_GPFX 0
+#endif
+
 // NST: the pop's ordered sum read back by the env's first lane only
 #ifndef MGN_NST_SUM1
 #define MGN_NST_SUM1 1
@@ -175,6 +186,11 @@ struct TrioShared {
   // WIN with a log window (MGN_TRIO_GLOG): the tick's log-normalised prices,
   // formed by the generator role for the finish role's window rows
   double lprice[2][NSL];
+  // NST with the generator's prefix (MGN_NST_GPFX): the finish role's buffer
+  // state after its pops (F -> G, next iteration), the prefix sum (G -> F,
+  // same iteration) and the iteration that published it
+  double nA[2][EPB], nB[2][EPB], pfx[2][EPB];
+  int32_t nhd[2][EPB], nln[2][EPB], pfx_it[EPB];
 };
 
 // LDS of k_step_trio<S, ..., TW, NST, ..., M>: its static arrays (an upper
@@ -236,8 +252,10 @@ __device__ __forceinline__ void trio_replay_tick(Lane<M>& s, const KParams& p, u
   nx.dend = p.rp_end[s.rcur];
   s.pf_ok = true;
 }
-inline size_t trio_nst_dyn_lds(int S, int TW, int nstep) {
-  return (size_t)(TW / S) * 2 * nst_pad(nstep, S) * sizeof(double);
+// per env: the ring, the finish role's pop summands and (gpfx, MGN_NST_GPFX)
+// the generator's prefix summands
+inline size_t trio_nst_dyn_lds(int S, int TW, int nstep, bool gpfx = MGN_NST_GPFX != 0) {
+  return (size_t)(TW / S) * (gpfx ? 3 : 2) * nst_pad(nstep, S) * sizeof(double);
 }
 
 // OMC: the output set when known at compile time (O_ALL, O_STD), else 0.
@@ -302,10 +320,15 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   MGN_IT(47, 0);
   const int in_kind = DISC ? IN_DISCRETE : in_kind_rt;
   constexpr int M = MM;
-  // (not at two slots per lane with a mixed-kind generator: the candidate's
-  // copy of every field of both slots spilled at the 168-register budget)
-  constexpr bool TAIL = MGN_TRIO_TAILRST && !RP && !WIN && (MM == 1 || GK >= 0);
+  // (not at two slots per lane with a mixed-kind generator, nor beside the
+  // generator's n-step prefix: the candidate's copy of the generator state
+  // spilled at the 168-register budget)
+  constexpr bool TAIL = MGN_TRIO_TAILRST && !RP && !WIN && (MM == 1 || GK >= 0) && !(NST && MGN_NST_GPFX);
   constexpr bool GLOG = MGN_TRIO_GLOG && WIN && !RP;
+  // NST: the generator role forms the first pop's prefix (env-major
+  // generator lanes: one source kind)
+  constexpr bool GPFX = MGN_NST_GPFX && NST && GK >= 0 && M == 1;
+  constexpr int NPADS = GPFX ? 3 : 2;
   static_assert(M == 1 || (M == 2 && !NST), "two slots per lane: one-step rewards");
   constexpr int APAD = S * M;
   constexpr int TRIO_W = TW;
@@ -316,7 +339,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   __shared__ mgn_asset_source s_src[APAD];
   __shared__ double s_tgt[MGN_MAX_ASSETS + 1];
   __shared__ double s_disc[NST ? MGN_MAX_NSTEP : 1];                     // NST: gamma^k
-  extern __shared__ __attribute__((aligned(16))) double s_nst[];          // NST: (EPB, 2 nst_pad(n, S))
+  extern __shared__ __attribute__((aligned(16))) double s_nst[];          // NST: (EPB, NPADS nst_pad(n, S))
   const int role = threadIdx.x / TRIO_W;  // 0 generator, 1 ledger, 2 finish
   const int l = threadIdx.x % TRIO_W;
   // GSLOT: a handle whose assets are of several source kinds (a Composite)
@@ -440,7 +463,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       nlen = p.nlen[envc];
       nhead = p.nhead[envc];
       // the env's ring into LDS (every lane of the env copies a share)
-      double* ring = s_nst + (size_t)el * 2 * nst_pad(p.nstep, S);
+      double* ring = s_nst + (size_t)el * NPADS * nst_pad(p.nstep, S);
       for (int i = ls; i < p.nstep; i += S) ring[i] = p.nring[(size_t)envc * p.nstep + i];
     }
   }
@@ -467,6 +490,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     sh.more[1] = 0;
     sh.more[2] = 0;
   }
+  if (GPFX && threadIdx.x < EPB) sh.pfx_it[threadIdx.x] = -1;  // (read from iteration 1 on)
 #ifdef MGN_STAMPS
   if (threadIdx.x < 8) s_duo_sub[threadIdx.x] = 0;
 #endif
@@ -474,6 +498,68 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   MGN_IT(1, 0);
 #pragma unroll
   for (int m = 0; m < M; ++m) s.kind[m] = s.valid[m] ? (QREG ? GK : s_src[s.asset[m]].kind) : -1;
+
+  // NST: a pop's summands (nstep_column's operands: summand kk of the entries
+  // [head, head + len) on lane kk mod S, MGN_NST_U rounds evaluated together
+  // on clamped operands so their chains interleave, slots [len, R S) +0.0)
+  // into scr, and their ordered sum in kk order (S per chunk, the next
+  // chunk's reads issued before this chunk's adds; +0.0 slots leave it
+  // unchanged: acc starts at +0.0 and is never -0.0)
+  // (U: rounds per pass, a std::integral_constant)
+  const auto nst_summands = [&](auto Uc, const double* ring, double* scr, int head, int len, double A, double B,
+                                const PopPre& c) {
+    constexpr int U = decltype(Uc)::value;
+    const int n = p.nstep;
+    const int R = (len + S - 1) / S;
+    for (int j = 0; j < R; j += U) {
+      double rr[U], dd[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int kk = ls + (j + u) * S;
+        int idx = head + kk;
+        idx -= (idx >= n) ? n : 0;
+        const bool ok = kk < len && j + u < R;
+        rr[u] = ring[ok ? idx : 0];
+        dd[u] = s_disc[ok ? kk : 0];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int kk = ls + (j + u) * S;
+#ifdef MGN_NST_ABL_TERM  // diagnostic timing build (outputs wrong): no summand arithmetic
+        const double t = rr[u];
+#else
+        const double t = pop_term(p.shaper, rr[u], A, B, c, dd[u]);
+#endif
+        if (j + u < R) scr[kk] = (kk < len) ? t : 0.0;
+      }
+    }
+  };
+  const auto nst_sum = [&](const double* scr, int len) {
+    const int R = (len + S - 1) / S;
+    double acc = 0.0;
+#ifdef MGN_NST_ABL_SUM  // diagnostic timing build (outputs wrong): no ordered sum
+    acc = scr[0];
+#else
+    const d2* sc = reinterpret_cast<const d2*>(scr);
+    d2 cur[S / 2];
+#pragma unroll
+    for (int u = 0; u < S / 2; ++u) cur[u] = sc[u];
+    for (int j = 0; j < R; ++j) {
+      d2 nxt[S / 2];
+      const int jn = (j + 1 < R) ? j + 1 : j;
+#pragma unroll
+      for (int u = 0; u < S / 2; ++u) nxt[u] = sc[jn * (S / 2) + u];
+#pragma unroll
+      for (int u = 0; u < S / 2; ++u) {
+        acc += cur[u].x;
+        acc += cur[u].y;
+      }
+#pragma unroll
+      for (int u = 0; u < S / 2; ++u) cur[u] = nxt[u];
+    }
+#endif
+    return acc;
+  };
 
   if (role == 0) {
     // ---------------- generator waves: tick of step j, State.price / timestamp
@@ -567,6 +653,28 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         }
         const bool rst = j > 0 && sh.reset[prv][el] != 0;
         const bool prev_step = j > 0 && (sh.rFlags[prv][el] & TR_STEP) != 0;
+        if constexpr (GPFX) {
+          // the finish role evaluates the env's step of the last iteration in
+          // this one (the same test as its own): the first pop's summands
+          // over the entries already in its ring and their ordered sum, with
+          // the shaper state after its last pops (MGN_NST_GPFX)
+          if (prev_step && !rst) {
+            const int pad = nst_pad(p.nstep, S);
+            const double* ring = s_nst + (size_t)el * NPADS * pad;
+            double* gscr = s_nst + (size_t)el * NPADS * pad + 2 * pad;
+            const double A = sh.nA[prv][el], B = sh.nB[prv][el];
+            const int len0 = sh.nln[prv][el];
+            nst_summands(std::integral_constant<int, MGN_NST_U>{}, ring, gscr, sh.nhd[prv][el], len0, A, B,
+                         pop_pre(p.shaper, A, B));
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (ls == 0) {
+              sh.pfx[cur][el] = nst_sum(gscr, len0);
+              __hip_atomic_store(&sh.pfx_it[el], j, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+          }
+        }
         // every branch's tick is the one call below (one copy of the
         // generator's code: the kind dispatch of every slot, inlined once)
         bool tk = false, stepk = false;
@@ -1137,7 +1245,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         // after the pops) is stored here
         rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
         const int n = p.nstep;
-        double* ring = s_nst + (size_t)el * 2 * nst_pad(n, S);  // ring, then the pop's summands
+        double* ring = s_nst + (size_t)el * NPADS * nst_pad(n, S);  // ring, then the pop's summands
         double* scr = ring + nst_pad(n, S);
         const double v = (p.shaper == MGN_SHAPER_PPC) ? rin_s + cos_term : rin_s;
         const int L1 = nlen + 1;
@@ -1159,61 +1267,25 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           const PopPre c = pop_pre(p.shaper, g.shA, g.shB);
-          const int R = (len + S - 1) / S;
-          // MGN_NST_U rounds of summands per pass, every one evaluated (on
-          // clamped operands) so their chains interleave; only the stores
-          // of rounds past R are skipped
-          for (int j = 0; j < R; j += MGN_NST_U) {
-            double rr[MGN_NST_U], dd[MGN_NST_U];
-#pragma unroll
-            for (int u = 0; u < MGN_NST_U; ++u) {
-              const int kk = ls + (j + u) * S;
-              int idx = head + kk;
-              idx -= (idx >= n) ? n : 0;
-              const bool ok = kk < len && j + u < R;
-              rr[u] = ring[ok ? idx : 0];
-              dd[u] = s_disc[ok ? kk : 0];
-            }
-#pragma unroll
-            for (int u = 0; u < MGN_NST_U; ++u) {
-              const int kk = ls + (j + u) * S;
-#ifdef MGN_NST_ABL_TERM  // diagnostic timing build (outputs wrong): no summand arithmetic
-              const double t = rr[u];
-#else
-              const double t = pop_term(p.shaper, rr[u], g.shA, g.shB, c, dd[u]);
-#endif
-              if (j + u < R) scr[kk] = (kk < len) ? t : 0.0;
-            }
-          }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           double acc = 0.0;
-#ifdef MGN_NST_ABL_SUM  // diagnostic timing build (outputs wrong): no ordered sum
-          acc = scr[0];
-#else
-          // the ordered sum only feeds the popped value the env's first lane
-          // stores: only that lane reads the summands back (MGN_NST_SUM1)
-          if (!MGN_NST_SUM1 || ls == 0) {
-          const d2* sc = reinterpret_cast<const d2*>(scr);
-          d2 cur[S / 2];
-#pragma unroll
-          for (int u = 0; u < S / 2; ++u) cur[u] = sc[u];
-          for (int j = 0; j < R; ++j) {
-            d2 nxt[S / 2];
-            const int jn = (j + 1 < R) ? j + 1 : j;
-#pragma unroll
-            for (int u = 0; u < S / 2; ++u) nxt[u] = sc[jn * (S / 2) + u];
-#pragma unroll
-            for (int u = 0; u < S / 2; ++u) {
-              acc += cur[u].x;
-              acc += cur[u].y;
+          if (GPFX && pj == 0) {
+            // the generator role's ordered sum of the summands of the
+            // entries before this step's (published in this iteration), plus
+            // this step's: the same additions in the same order
+            if (!MGN_NST_SUM1 || ls == 0) {
+              while (__hip_atomic_load(&sh.pfx_it[el], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != j)
+                __builtin_amdgcn_s_sleep(1);
+              acc = sh.pfx[cur][el] + pop_term(p.shaper, v, g.shA, g.shB, c, s_disc[len - 1]);
             }
-#pragma unroll
-            for (int u = 0; u < S / 2; ++u) cur[u] = nxt[u];
+          } else {
+            nst_summands(std::integral_constant<int, MGN_NST_U>{}, ring, scr, head, len, g.shA, g.shB, c);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // the ordered sum only feeds the popped value the env's first lane
+            // stores: only that lane reads the summands back (MGN_NST_SUM1)
+            if (!MGN_NST_SUM1 || ls == 0) acc = nst_sum(scr, len);
           }
-          }
-#endif
           double res = acc;
           if (p.shaper == MGN_SHAPER_DSR || p.shaper == MGN_SHAPER_DDR) {
             res = clip1(acc / len);
@@ -1340,6 +1412,16 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       for (int m = 0; m < M; ++m) pa[m] = (Lf[m] * Pf[m]) / eq;
       push_row(Pf, pa, (cashf - bf) / eq, (uint64_t)sh.ts[prv][el], klast, prv);
     }
+    if constexpr (GPFX) {
+      // the n-step buffer after this iteration's pops, for the generator's
+      // prefix of the next iteration's first pop
+      if (ls == 0) {
+        sh.nA[cur][el] = g.shA;
+        sh.nB[cur][el] = g.shB;
+        sh.nhd[cur][el] = nhead;
+        sh.nln[cur][el] = nlen;
+      }
+    }
     if (ls == 0) sh.reset[cur][el] = rst_out;
     // the reset tick runs next iteration -- a tail reset's in this one, by the
     // idle generator role (adopted after the loop)
@@ -1365,7 +1447,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #endif
   if (!live) return;
   if constexpr (NST) {
-    const double* ring = s_nst + (size_t)el * 2 * nst_pad(p.nstep, S);
+    const double* ring = s_nst + (size_t)el * NPADS * nst_pad(p.nstep, S);
     for (int i = ls; i < p.nstep; i += S) p.nring[(size_t)env * p.nstep + i] = ring[i];
     if (ls == 0) {
       p.nlen[env] = nlen;

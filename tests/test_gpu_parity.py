@@ -293,6 +293,36 @@ def test_nstep_rollout(gpu, shaper, mode, n):
     close(gb, orc.scalar("shaperB"), "B")
 
 
+@pytest.mark.parametrize("A,N,n,shaper", [(8, 8192, 20, "DDR"), (16, 4096, 5, "DSR"), (4, 16384, 3, "DDR")])
+def test_nstep_generator_prefix_vs_oracle(gpu, A, N, n, shaper):
+    """n-step aggregation on the 256-lane three-role kernel with one source
+    kind (the n = 20 DDR bench shape's instantiation): the generator role forms
+    each step's first-pop prefix (MGN_NST_GPFX) and the finish role adds the
+    new entry's summand -- against the oracle over two launches (the buffer
+    carries across them), auto-resets flushing buffers inside the launches."""
+    from madigan_amd import _lib as L
+    K = 24
+    kw = dict(required_margin=0.02, maintenance_margin=0.25, transaction_cost_rel=0.02,
+              unit_size=0.9, auto_reset=1, init_cash=1e5, reward_shaper=shaper,
+              adaptation_rate=0.01, nstep_return=n, discount=0.97)
+    g, orc = make_pair(trendou_sources(A, [0.2, 2, 6, 0.05, 0.2, 5.0, 0.15, 0.3, 0.2, 0.99]), N, **kw)
+    # (16 assets with n-step: the automatic schedule takes the two-role kernel)
+    L.check(g.lib.mgn_set_schedule(g.h, L.SCHED_TRIO), g.h)
+    assert g.lib.mgn_get_schedule(g.h) == L.SCHED_TRIO
+    acts = g.generate_actions(2 * K, seed=17)
+    for half in range(2):
+        a = acts[half * K:(half + 1) * K]
+        host = {k: v.cpu().numpy() for k, v in g.rollout(a).items()}
+        ref = orc.rollout(a.cpu().numpy())
+        assert ref["done"].sum() > 0
+        out_check({**host, "shaped": ref["shaped"]}, ref, f"nstep{n} A{A} {half}", 1)
+        assert np.array_equal(host["n_shaped"], ref["n_shaped"]), "n_shaped"
+        np.testing.assert_allclose(host["shaped"], ref["shaped"], rtol=1e-10, atol=1e-14, err_msg="shaped")
+        state_check(g, orc, f"nstep{n} A{A} {half}")
+    close(g.shaper_a.cpu().numpy(), orc.scalar("shaperA"), "A")
+    close(g.shaper_b.cpu().numpy(), orc.scalar("shaperB"), "B")
+
+
 def test_nstep64_two_assets_auto_schedule(gpu):
     """2 assets, n = 64, at a batch that takes the 256-lane layout: the
     three-role kernel's static arrays plus 128 envs' rings (128 KiB) exceed a

@@ -346,11 +346,12 @@ int mgn_get_layout(const mgn_env *env);
  * (generator, ledger and finish waves pipelined one step apart, `done`
  * speculated; 2..16 assets, generator sources with n = 1 with or without a
  * window, or a scalar n-step reward without a window whose rings fit the
- * workgroup's LDS, and replay tapes at 16 assets for N >= 4096);
- * MGN_SCHED_AUTO (default) = TRIO where eligible and measured faster (up to
- * 8 assets; 16 assets without window and n = 1, or replay), else DUO where
- * eligible and the layout is one asset per lane, else SINGLE.  Results are
- * bit-identical; only speed changes. */
+ * workgroup's LDS, and replay tapes at 16 assets for N >= 4096; 9..16
+ * assets at N >= 4096 with discrete actions and n = 1 run two asset slots per
+ * lane); MGN_SCHED_AUTO (default) = TRIO where eligible and measured faster
+ * (up to 8 assets; 9..16 assets with n = 1 -- windows only at N >= 4096 --
+ * or replay), else DUO where eligible and the layout is one asset per lane,
+ * else SINGLE.  Results are bit-identical; only speed changes. */
 enum { MGN_SCHED_AUTO = 0, MGN_SCHED_SINGLE = 1, MGN_SCHED_DUO = 2, MGN_SCHED_TRIO = 3 };
 int mgn_set_schedule(mgn_env *env, int32_t schedule);
 int mgn_get_schedule(const mgn_env *env);

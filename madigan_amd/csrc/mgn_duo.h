@@ -574,6 +574,25 @@ __device__ __forceinline__ Q4 tree4(const EnvRecs<S>& er, uint32_t post, Q4 (&si
   }
 }
 
+// One order of the Broker's cash chain (Broker.cpp:128-135): cash becomes
+// ((cash + X1) - y) - Z when the order executes.  MGN_SPEC_CHMASK: a skipped
+// order adds the identities of the same operations (c + -0.0 and c - +0.0 are
+// c, bit for bit, for every c), so the select of the terms leaves the chain's
+// dependency -- three dependent additions per order, no select behind them.
+// Measured slower (20-step 2.22-2.24 -> 2.29-2.30 us/step, 256-step 1.92-1.93
+// -> 2.02-2.03: profiles/r04_ab_chain_mask.txt): off
+#ifndef MGN_SPEC_CHMASK
+#define MGN_SPEC_CHMASK 0
+#endif
+// (MASK false at two slots per lane: 16 orders' masked terms formed ahead of
+// the chain spilled at the 168-register budget)
+template <bool MASK = MGN_SPEC_CHMASK != 0>
+__device__ __forceinline__ double chain_step(double c, double X1, double y, double Z, bool go) {
+  if (MASK) return ((c + (go ? X1 : -0.0)) - (go ? y : 0.0)) - (go ? Z : 0.0);
+  const double ci = ((c + X1) - y) - Z;
+  return go ? ci : c;
+}
+
 // The canonical trees of broker_spec in registers (MGN_SPEC_DPP): every lane
 // holds its own order's four leaves before (pre) and after (post) the order;
 // the tree of lane ls's check has post leaves for the executed orders j < ls
@@ -715,8 +734,7 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
         er.cpre[i] = c;
         const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
         const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
-        const double ci = ((c + xz.y) - yz.x) - yz.y;
-        c = ((go_bits >> i) & 1) ? ci : c;
+        c = chain_step(c, xz.y, yz.x, yz.y, ((go_bits >> i) & 1) != 0);
       }
       er.cpre[S] = c;
     }
@@ -906,8 +924,7 @@ __device__ __forceinline__ void broker_spec_m2(Lane<2>& s, const KParams& p, Env
         er.cpre[i] = c;
         const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
         const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
-        const double ci = ((c + xz.y) - yz.x) - yz.y;
-        c = ((go_bits >> i) & 1) ? ci : c;
+        c = chain_step<false>(c, xz.y, yz.x, yz.y, ((go_bits >> i) & 1) != 0);
       }
       er.cpre[APAD] = c;
     }

@@ -28,13 +28,14 @@
 // stands.  Every value is the same expression of the same operands as in
 // k_step, so every output is bit-identical to k_step / k_step_duo (and the
 // oracle).
-// Stores: L stores the BrokerResponse arrays of its step, G the tick's
-// State.price and timestamp, F everything that needs equity.
-// Scope: M = 1, APAD = S in {2, 4, 8, 16} (16: the ledger's broker trees read
-// behind scheduling fences, tree4's FENCE), generator sources; n = 1 with or without a window
-// (WIN: the finish role pushes the ring / launch-history row of every step it
-// confirms, and the refill rows after an auto-reset), or n-step (NST, no
-// window); k_step_duo / k_step run the rest.
+// Stores: F stores every output of the steps it confirms (MGN_TRIO_LST /
+// MGN_TRIO_GST move the BrokerResponse arrays to L, State.price and the
+// timestamp to G: measured slower); G and L write their state back at exit.
+// Scope: one asset slot per lane at APAD = S in {2, 4, 8, 16}, or two (MM = 2)
+// at S = 8 for 9..16 assets; generator sources or (16 assets) a replay tape;
+// n = 1 with or without a window (WIN: the finish role pushes the ring /
+// launch-history row of every step it confirms, and the refill rows after an
+// auto-reset), or n-step (NST, no window); k_step_duo / k_step run the rest.
 #pragma once
 
 #include "mgn_duo.h"

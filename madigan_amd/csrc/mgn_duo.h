@@ -663,9 +663,9 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
   // yields the sums after every order: the others skip the tree's LDS reads
   // (their lanes idle in its instructions)
 #if MGN_SPEC_TREE_SKIP
-  const bool need_tree = (act && (own.need_mc || own.need_insuff)) || ls == S - 1;
+  [[maybe_unused]] const bool need_tree = (act && (own.need_mc || own.need_insuff)) || ls == S - 1;
 #else
-  constexpr bool need_tree = true;
+  [[maybe_unused]] constexpr bool need_tree = true;
 #endif
   const uint32_t act_bits = (uint32_t)seg_or<S>(act << ls);
   uint32_t go_bits = act_bits;  // the guess
@@ -676,7 +676,7 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
   // ~1 % faster at S = 8 than the streaming tree); S = 16 or LOWREG (the
   // three-role kernel's 168-VGPR budget): the streaming tree, its
   // rightmost-path left children kept
-  constexpr bool STREAM = LOWREG || S >= 16;
+  [[maybe_unused]] constexpr bool STREAM = LOWREG || S >= 16;
 #if !MGN_SPEC_DPP
   Q4 sib[6];
   double lv[4][STREAM ? 1 : S];

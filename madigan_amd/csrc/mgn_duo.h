@@ -593,6 +593,19 @@ __device__ __forceinline__ double chain_step(double c, double X1, double y, doub
   return go ? ci : c;
 }
 
+// MGN_SPEC_PLAIN: when no order of the wave closes a position or settles a
+// borrowed margin (X1 = -0.0 and Z = +0.0 bit for bit: every order at a
+// required margin of 1 that buys or closes exactly), the cash update of an
+// executed order is cash - y -- c + -0.0 and x - +0.0 are c and x for every
+// value -- one dependent subtraction per order on the chain instead of three
+// (a uniform branch on the wave's ballot).  Measured mixed
+// (profiles/r04_ab_plain_chain.txt: one-step launches -3 %, 16 assets -3 %,
+// 256-step C3 +2-4 %, C5 +10 % -- the second walk's registers spill at two
+// slots per lane): off
+#ifndef MGN_SPEC_PLAIN
+#define MGN_SPEC_PLAIN 0
+#endif
+
 // The canonical trees of broker_spec in registers (MGN_SPEC_DPP): every lane
 // holds its own order's four leaves before (pre) and after (post) the order;
 // the tree of lane ls's check has post leaves for the executed orders j < ls
@@ -653,6 +666,8 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
 #endif
 #if MGN_SPEC_DPP
   const OwnChk& own = oc[0];
+  // every order of the wave plain (MGN_SPEC_PLAIN): a uniform value
+  const bool wave_plain = __builtin_amdgcn_ballot_w64(!own.plain) == 0;
 #else
   const OrderRec& own = er.r[ls];
 #endif
@@ -729,12 +744,21 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
     // publishes the cash before every order and after the last
     if (ls == 0) {
       double c = cash0;
+      if (MGN_SPEC_DPP && MGN_SPEC_PLAIN && wave_plain) {
 #pragma unroll
-      for (int i = 0; i < S; ++i) {
-        er.cpre[i] = c;
-        const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
-        const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
-        c = chain_step(c, xz.y, yz.x, yz.y, ((go_bits >> i) & 1) != 0);
+        for (int i = 0; i < S; ++i) {
+          er.cpre[i] = c;
+          const double y = er.r[i].y;
+          c = ((go_bits >> i) & 1) ? c - y : c;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+          er.cpre[i] = c;
+          const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
+          const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
+          c = chain_step(c, xz.y, yz.x, yz.y, ((go_bits >> i) & 1) != 0);
+        }
       }
       er.cpre[S] = c;
     }
@@ -855,6 +879,7 @@ __device__ __forceinline__ void broker_spec_m2(Lane<2>& s, const KParams& p, Env
   double lf_pre[4 * M], lf_post[4 * M];
   OwnChk oc[M];
   order_prep<M, S, false>(s, p, er, uc, ls, cu2, me2, bm3, tpr, tco, lf_pre, lf_post, oc);
+  const bool wave_plain = __builtin_amdgcn_ballot_w64(!(oc[0].plain && oc[1].plain)) == 0;  // (MGN_SPEC_PLAIN)
   // the leaves are re-formed in every pass from the slot state the lane
   // holds anyway (ledger, price, and the order's outcome): the same products
   // (order_prep's), so the same bits, without 16 leaf registers live across
@@ -919,12 +944,21 @@ __device__ __forceinline__ void broker_spec_m2(Lane<2>& s, const KParams& p, Env
     }
     if (ls == 0) {
       double c = cash0;
+      if (MGN_SPEC_PLAIN && wave_plain) {
 #pragma unroll
-      for (int i = 0; i < APAD; ++i) {
-        er.cpre[i] = c;
-        const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
-        const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
-        c = chain_step<false>(c, xz.y, yz.x, yz.y, ((go_bits >> i) & 1) != 0);
+        for (int i = 0; i < APAD; ++i) {
+          er.cpre[i] = c;
+          const double y = er.r[i].y;
+          c = ((go_bits >> i) & 1) ? c - y : c;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < APAD; ++i) {
+          er.cpre[i] = c;
+          const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
+          const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
+          c = chain_step<false>(c, xz.y, yz.x, yz.y, ((go_bits >> i) & 1) != 0);
+        }
       }
       er.cpre[APAD] = c;
     }

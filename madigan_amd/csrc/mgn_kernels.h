@@ -950,6 +950,7 @@ struct XRounds {
 struct OwnChk {
   double aPX;
   bool need_mc, need_insuff;
+  bool plain;  // X1 is -0.0 and Z +0.0 bit for bit: the cash update is cash - y
 };
 template <int M, int S, bool WPP = true>
 __device__ __forceinline__ void order_prep(const Lane<M>& s, const KParams& p, EnvRecs<M * S>& er,
@@ -1006,9 +1007,10 @@ __device__ __forceinline__ void order_prep(const Lane<M>& s, const KParams& p, E
       }
     }
     const double aPX = opp ? fabs(price * excess) : fabs(price * u);
-    r.X1 = close ? cur * tprice : -0.0;
+    const double X1v = close ? cur * tprice : -0.0, Zv = (repay || neg) ? bm1 : 0.0;
+    r.X1 = X1v;
     r.y = use + tcost;
-    r.Z = (repay || neg) ? bm1 : 0.0;
+    r.Z = Zv;
     const bool act = u != 0.;
     if constexpr (WPP) {  // XRounds reads every order's check operands from LDS
       r.aPX = aPX;
@@ -1020,6 +1022,7 @@ __device__ __forceinline__ void order_prep(const Lane<M>& s, const KParams& p, E
       own[m].aPX = aPX;
       own[m].need_mc = !opp;
       own[m].need_insuff = !opp || rev;
+      own[m].plain = __double_as_longlong(X1v) == (long long)0x8000000000000000ULL && __double_as_longlong(Zv) == 0;
     }
   }
   // the segment's records are written by its own lanes: wave-scope ordering

@@ -744,21 +744,15 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
     // publishes the cash before every order and after the last
     if (ls == 0) {
       double c = cash0;
-      if (MGN_SPEC_DPP && MGN_SPEC_PLAIN && wave_plain) {
 #pragma unroll
-        for (int i = 0; i < S; ++i) {
-          er.cpre[i] = c;
-          const double y = er.r[i].y;
-          c = ((go_bits >> i) & 1) ? c - y : c;
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < S; ++i) {
-          er.cpre[i] = c;
-          const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
-          const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
+      for (int i = 0; i < S; ++i) {
+        er.cpre[i] = c;
+        const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
+        const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
+        if (MGN_SPEC_DPP && MGN_SPEC_PLAIN && wave_plain)
+          c = ((go_bits >> i) & 1) ? c - yz.x : c;
+        else
           c = chain_step(c, xz.y, yz.x, yz.y, ((go_bits >> i) & 1) != 0);
-        }
       }
       er.cpre[S] = c;
     }
@@ -944,21 +938,15 @@ __device__ __forceinline__ void broker_spec_m2(Lane<2>& s, const KParams& p, Env
     }
     if (ls == 0) {
       double c = cash0;
-      if (MGN_SPEC_PLAIN && wave_plain) {
 #pragma unroll
-        for (int i = 0; i < APAD; ++i) {
-          er.cpre[i] = c;
-          const double y = er.r[i].y;
-          c = ((go_bits >> i) & 1) ? c - y : c;
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < APAD; ++i) {
-          er.cpre[i] = c;
-          const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
-          const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
+      for (int i = 0; i < APAD; ++i) {
+        er.cpre[i] = c;
+        const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
+        const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
+        if (MGN_SPEC_PLAIN && wave_plain)
+          c = ((go_bits >> i) & 1) ? c - yz.x : c;
+        else
           c = chain_step<false>(c, xz.y, yz.x, yz.y, ((go_bits >> i) & 1) != 0);
-        }
       }
       er.cpre[APAD] = c;
     }

@@ -34,7 +34,12 @@ FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=
 # motion -- hoisting the math kernels' 64-bit polynomial constants out of the
 # step loop left them live across it at the 168-register budget and spilled
 # them to scratch (48 -> 4 spilled registers in the generic generator build)
-UNIT_FLAGS = {"mgn_launch_a16m2.hip": ["-mllvm", "-disable-machine-licm"]}
+# The same holds for the n-step instantiations at APAD 8 (their own unit,
+# mgn_launch_a8nst.hip): n = 20 DDR 3.80 -> 3.69 us/step, while the one-step
+# instantiations of mgn_launch_a8.hip measured 1.5-2.7 % slower without it
+# (profiles/r04_ab_licm.txt)
+UNIT_FLAGS = {"mgn_launch_a16m2.hip": ["-mllvm", "-disable-machine-licm"],
+              "mgn_launch_a8nst.hip": ["-mllvm", "-disable-machine-licm"]}
 
 
 def hipcc() -> str:

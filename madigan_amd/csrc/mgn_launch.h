@@ -61,6 +61,8 @@ inline bool trio_m2_ok(long long n_envs, int A, int nstep, int D, int in_kind) {
          in_kind == IN_DISCRETE;
 }
 void launch_trio_m2_a16(const StepArgs& a);
+// the n-step three-role launches at APAD = 8, in their own unit (mgn_launch_a8nst.hip)
+void launch_trio_nst_a8(const StepArgs& a);
 
 // smallest assets-per-lane with at most 16 lanes per env (DPP-only reductions)
 constexpr int min_m(int apad) { return apad > 16 ? apad / 16 : 1; }

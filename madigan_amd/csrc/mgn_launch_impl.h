@@ -115,6 +115,47 @@ void launch_trio_m2(const StepArgs& a) {
 }
 
 // three-role pipelined step kernel (mgn_trio.h): S = APAD lanes per env per role
+// NST: the finish role's NStepBuffer rings in dynamic LDS (no window, D = 1).
+// APAD 8 instantiates it in its own unit (mgn_launch_a8nst.hip, UNIT_FLAGS)
+template <int S>
+void launch_trio_nst(const StepArgs& a) {
+  const bool small = (long long)a.p.N * S < 256LL * TRIO_W;
+  const int epb = (small ? 64 : TRIO_W) / S;
+  const int grid = (a.p.N + epb - 1) / epb;
+  const bool disc = a.in_kind == IN_DISCRETE;
+  // the kind-specialized instantiation keeps a third pad per env for the
+  // generator's prefix summands (MGN_NST_GPFX)
+  const bool gpfx = MGN_NST_GPFX && !small && disc && a.gkind == MGN_SRC_TRENDOU;
+  const size_t lds = trio_nst_dyn_lds(S, small ? 64 : TRIO_W, a.p.nstep, gpfx);
+  auto goN = [&](auto kern) {
+    // a refused size is the caller's hipGetLastError (HIP records every
+    // call's status); trio_eligible keeps static + dynamic LDS within 160 KiB
+    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess)
+      return;
+    launch_timed(a.ev0, a.ev1, kern, dim3(grid), dim3(small ? 192 : TRIO_BLOCK), (uint32_t)lds, a.stream,
+                 a.p.L, a.p.mep, a.p.Bm, a.p.P, a.p.cash, a.act, a.p, a.out, a.in_kind, a.units, a.aidx, a.K);
+  };
+  if (small) {
+    if (disc) {
+      if (a.p.reqm_one) goN(k_step_trio<S, true, true, 0, false, 64, true>);
+      else goN(k_step_trio<S, false, true, 0, false, 64, true>);
+    } else {
+      if (a.p.reqm_one) goN(k_step_trio<S, true, false, 0, false, 64, true>);
+      else goN(k_step_trio<S, false, false, 0, false, 64, true>);
+    }
+  } else if (disc && a.gkind == MGN_SRC_TRENDOU) {
+    if (a.p.reqm_one) goN(k_step_trio<S, true, true, 0, false, TRIO_W, true, MGN_SRC_TRENDOU>);
+    else goN(k_step_trio<S, false, true, 0, false, TRIO_W, true, MGN_SRC_TRENDOU>);
+  } else if (disc) {
+    if (a.p.reqm_one) goN(k_step_trio<S, true, true, 0, false, TRIO_W, true>);
+    else goN(k_step_trio<S, false, true, 0, false, TRIO_W, true>);
+  } else {
+    if (a.p.reqm_one) goN(k_step_trio<S, true, false, 0, false, TRIO_W, true>);
+    else goN(k_step_trio<S, false, false, 0, false, TRIO_W, true>);
+  }
+}
+
 template <int S>
 void launch_trio(const StepArgs& a) {
   if constexpr (S == 16) {
@@ -153,38 +194,9 @@ void launch_trio(const StepArgs& a) {
     }
     return;
   }
-  if (a.p.nstep > 1) {  // NST: the finish role's NStepBuffer rings in dynamic LDS (no window, D = 1)
-    // the kind-specialized instantiation keeps a third pad per env for the
-    // generator's prefix summands (MGN_NST_GPFX)
-    const bool gpfx = MGN_NST_GPFX && !small && disc && a.gkind == MGN_SRC_TRENDOU;
-    const size_t lds = trio_nst_dyn_lds(S, small ? 64 : TRIO_W, a.p.nstep, gpfx);
-    auto goN = [&](auto kern) {
-      // a refused size is the caller's hipGetLastError (HIP records every
-      // call's status); trio_eligible keeps static + dynamic LDS within 160 KiB
-      if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-          hipSuccess)
-        return;
-      launch_timed(a.ev0, a.ev1, kern, dim3(grid), dim3(small ? 192 : TRIO_BLOCK), (uint32_t)lds, a.stream,
-                   a.p.L, a.p.mep, a.p.Bm, a.p.P, a.p.cash, a.act, a.p, a.out, a.in_kind, a.units, a.aidx, a.K);
-    };
-    if (small) {
-      if (disc) {
-        if (a.p.reqm_one) goN(k_step_trio<S, true, true, 0, false, 64, true>);
-        else goN(k_step_trio<S, false, true, 0, false, 64, true>);
-      } else {
-        if (a.p.reqm_one) goN(k_step_trio<S, true, false, 0, false, 64, true>);
-        else goN(k_step_trio<S, false, false, 0, false, 64, true>);
-      }
-    } else if (disc && a.gkind == MGN_SRC_TRENDOU) {
-      if (a.p.reqm_one) goN(k_step_trio<S, true, true, 0, false, TRIO_W, true, MGN_SRC_TRENDOU>);
-      else goN(k_step_trio<S, false, true, 0, false, TRIO_W, true, MGN_SRC_TRENDOU>);
-    } else if (disc) {
-      if (a.p.reqm_one) goN(k_step_trio<S, true, true, 0, false, TRIO_W, true>);
-      else goN(k_step_trio<S, false, true, 0, false, TRIO_W, true>);
-    } else {
-      if (a.p.reqm_one) goN(k_step_trio<S, true, false, 0, false, TRIO_W, true>);
-      else goN(k_step_trio<S, false, false, 0, false, TRIO_W, true>);
-    }
+  if (a.p.nstep > 1) {
+    if constexpr (S == 8) launch_trio_nst_a8(a);  // mgn_launch_a8nst.hip
+    else launch_trio_nst<S>(a);
     return;
   }
   if (small) {  // runtime output mask, window or not

@@ -48,6 +48,7 @@ sys.path.insert(0, ROOT)
 METRIC = "env-steps/sec (batched) at 8192 envs × 8 assets; % HBM roofline"
 TRENDOU_P = [0.001, 100, 500, 0.001, 0.005, 5.0, 0.15, 0.04, 0.001, 0.99]  # config.yaml:116-138
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+GUIDE_COPY_GBS = 6290.0  # MI355X_MICROARCH.md: 6.29 TB/s measured (float4 copy)
 
 
 def c3_kwargs():
@@ -104,7 +105,7 @@ def load_pmc_traffic(workload: str):
     return d[key], key
 
 
-def bandwidth_probe(dev, nbytes: int = 1 << 30, reps: int = 10):
+def bandwidth_probe(dev, nbytes: int = 2 << 30, reps: int = 10):
     """Attainable HBM bandwidth on this box: the library's
     16-B-per-lane copy kernel over two 1 GiB buffers; (read + write) GB/s."""
     import ctypes as C
@@ -150,12 +151,28 @@ def valu_issue(workload: str, launch_s: float):
 
 
 def host_threads() -> int:
-    """The host-core share this process may use (OMP_NUM_THREADS on the GPU
-    box, which is 16 there; else the affinity mask)."""
+    """The host-core share this process may use: OMP_NUM_THREADS where set (16
+    on the GPU box, whose `nproc` shows the whole machine's CPUs, many times
+    this process's share), else the affinity mask."""
     env = os.environ.get("OMP_NUM_THREADS")
     if env and env.isdigit() and int(env) > 0:
         return int(env)
     return len(os.sched_getaffinity(0))
+
+
+def host_cpu_info() -> dict:
+    """The box's CPU counts beside the threads the baseline used (SURVEY 8d:
+    the core count stated)."""
+    info = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        with open("/proc/cpuinfo") as f:
+            names = [ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")]
+        if names:
+            info["model"] = names[0]
+    except OSError:
+        pass
+    return info
 
 
 def cpu_baseline(n_envs: int, A: int, budget_s: float = 12.0):
@@ -186,7 +203,7 @@ def cpu_baseline(n_envs: int, A: int, budget_s: float = 12.0):
     v1, s1, d1 = timed(1, budget_s / 2)
     vT, sT, dT = timed(T, budget_s / 2) if T > 1 else (v1, s1, d1)
     return dict(value=vT, unit="env-steps/s", cores=T, kind="port",
-                single_core=v1,
+                single_core=v1, host=host_cpu_info(),
                 sample=f"C3 workload, {n_envs} envs x {A} assets: {sT} steps on {T} host threads "
                        f"(OpenMP over envs, {dT:.1f} s) and {s1} steps on one core ({d1:.1f} s); "
                        f"oracle/madigan_oracle.c built -O3 -march=x86-64-v3 -ffast-math")
@@ -380,33 +397,34 @@ def main():
     traj = env.alloc_traj(F, fields=[f for f in ("reward", "shaped", "done", "obs_price", "obs_port",
                                                  "timestamp", "tprice", "tunits", "tcost", "risk",
                                                  "margin_call")])
-    base, per = actions.data_ptr(), N * A
 
-    # one launcher per launch length (the mgn_traj is validated once, outside
-    # the timed region); the timed loop is one ctypes call per launch
+    # one launcher per launch length (the mgn_traj and the action buffer are
+    # validated once, outside the timed region; a launch's action rows are
+    # bounds-checked by the launcher); the timed loop is one call per launch
     outs, launchers = {}, {}
 
     def launcher(n):
         if n not in launchers:
             outs[n] = traj if n == F else {k: v[:n] for k, v in traj.items()}
-            launchers[n] = env.rollout_launcher(outs[n], n)
+            launchers[n] = env.rollout_launcher(outs[n], n, actions)
         return launchers[n]
 
     def plan(k0, k1):
         seq, k = [], k0
         while k < k1:
             n = min(F, k1 - k)
-            seq.append((launcher(n), base + k * per, n))
+            seq.append((launcher(n), k, n))
             k += n
         return seq
 
     def run(seq):
         rc = 0
-        for fn, ptr, _ in seq:
-            rc |= fn(ptr)
+        for fn, k, _ in seq:
+            rc |= fn(k)
         return rc
 
     warm, timed = plan(0, args.warmup), plan(args.warmup, total)
+    sync = env.stream_synchronizer()  # the handle's stream (every launch is on it)
     # kernel durations: HIP events around each step launch on the handle's
     # stream (mgn_set_timing; pooled events, created during the warmup)
     tmode = 2 if args.timing == "launch" else 1
@@ -419,12 +437,14 @@ def main():
     L.check(lib.mgn_set_timing(h, tmode), h)
     t0 = time.perf_counter()
     rc = run(timed)
-    torch.cuda.synchronize()
+    # the closing wait is on the handle's stream, the only one the steps use
+    # (a device-wide synchronize costs ~3 us more on an idle device)
+    rc |= sync()
     if world > 1:
-        # barrier + synchronize; at one rank the synchronize above is both
         dist.barrier()
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    torch.cuda.synchronize()
     L.check(rc, h)
     # the sharded path's one collective, issued at log intervals
     # in a training loop, not per step: after the timed steps, timed on its own
@@ -453,53 +473,108 @@ def main():
     fused = bytes_per_env_step(A, steps_per_launch, env.D)
     value = world * N * args.steps / elapsed
     episodes = int(gathered[:, 3].sum().item())
+    age = total  # steps the handle has run
 
-    # steps fused per launch (K in {1, 16, 256} beside the headline;
-    # K = 1 is the agent loop's shape, one env.step per policy step,
-    # offpolicy_q.py:143): per launch length the step kernel's own duration
-    # (HIP events recorded by the launch), and the per-step time of launches
-    # issued back to back through the same per-launch binding as the timed
-    # loop; outside the timed region, rank 0 only
-    sweep = {}
-    if rank == 0 and args.k_sweep:
+    # after the timed region, rank 0 only: the same handle continues on fresh
+    # actions (T_ACT rows, each launch on the next rows, as an agent loop's
+    # launches read fresh actions -- one action row repeated launch after
+    # launch drives every env into margin calls and auto-resets)
+    T_ACT = 1024
+    sw_actions = env.generate_actions(T_ACT, seed=0x6D6165) if rank == 0 and args.k_sweep else None
+    sw_at = [0]
+
+    def sw_launches(fn, K, n):
+        """n K-step launches of `fn` (bound to sw_actions), fresh rows each."""
+        rc = 0
+        for _ in range(n):
+            if sw_at[0] + K > T_ACT:
+                sw_at[0] = 0
+            rc |= fn(sw_at[0])
+            sw_at[0] += K
+        return rc
+
+    def kernel_launch_us(fn, K, n):
+        """The step kernel's own duration (HIP events recorded by the launch)
+        averaged over n launches."""
+        L.check(lib.mgn_set_timing(h, 2), h)
+        L.check(sw_launches(fn, K, n), h)
+        torch.cuda.synchronize()
+        tk = (C.c_double * 4)()
+        L.check(lib.mgn_get_timing(h, tk), h)
+        L.check(lib.mgn_set_timing(h, 0), h)
+        return tk[0] / max(int(tk[1]), 1) * 1e3
+
+    sw_traj = env.alloc_traj(256, fields=list(traj.keys())) if sw_actions is not None else None
+    sw_fns = {}
+
+    def sw_fn(K):
+        if K not in sw_fns:
+            sw_fns[K] = env.rollout_launcher({kk: v[:K] for kk, v in sw_traj.items()}, K, sw_actions)
+        return sw_fns[K]
+
+    def advance_to(target):
+        nonlocal age
+        while age < target:
+            n = min(256, target - age)
+            L.check(sw_launches(sw_fn(n), n, 1), h)
+            age += n
+        torch.cuda.synchronize()
+
+    def at_age(target, n=8):
+        """The headline's launch (steps_per_launch steps) at episode age
+        `target`: kernel time per launch and step, HBM fraction on SURVEY bytes,
+        the episodes ended so far (episode age sets the per-step cost: positions
+        grow, more orders are refused, rollbacks follow episode ends)."""
+        nonlocal age
+        advance_to(target)
+        Kh = int(round(steps_per_launch))
+        us = kernel_launch_us(sw_fn(Kh), Kh, n)
+        a0 = age
+        age += Kh * n
+        ep = int(env.episode_stats[:, 3].sum().item())
+        return {"age_steps": a0, "launches": n, "steps_per_launch": Kh, "kernel_us_per_launch": us,
+                "kernel_us_per_step": us / Kh,
+                "frac_survey_bytes": N * Kh * bpes / (us * 1e-6) / 1e9 / PEAK_HBM_GBS,
+                "episodes_completed": ep}
+
+    ages, steady, sweep = {}, None, {}
+    if sw_actions is not None:
+        # per-step cost against episode age; the steady-state figure is the
+        # headline's launch after >= 2000 untimed steps
+        for tgt in (1000, 2000):
+            ages[str(tgt)] = at_age(tgt)
+        steady = ages["2000"]
+        # steps fused per launch (SURVEY 8d: K in {1, 16, 256} beside the
+        # headline; K = 1 is the agent loop's shape, one env.step per policy
+        # step, offpolicy_q.py:143), all at steady state: per launch length the
+        # step kernel's own duration (launch events) and the per-step time of
+        # launches issued back to back through the same per-launch binding as
+        # the timed loop
         stream = torch.cuda.current_stream(dev)
-        big = env.alloc_traj(256, fields=list(traj.keys()))
-        # launch r reads the K steps of fresh actions (K, N, A) at step r K mod
-        # T, as an agent loop's launches do (one action row repeated launch
-        # after launch drives every env into margin calls and auto-resets,
-        # whose rollback iterations lengthen the short launches)
-        T = 1024
-        sw_actions = env.generate_actions(T, seed=0x6D6165)
-        sw_base, sw_row = sw_actions.data_ptr(), N * A * sw_actions.element_size()
         for K in ((1, 16, 64, 256) if args.sweep else (1, 16, 256)):
-            assert T % K == 0
             reps = max(4, 512 // K)
-            ptr = [sw_base + ((r * K) % T) * sw_row for r in range(2 * reps + 1)]
-            fn = env.rollout_launcher({kk: v[:K] for kk, v in big.items()}, K)
-            fn(ptr[-1])  # warm
+            fn = sw_fn(K)
+            L.check(sw_launches(fn, K, 1), h)  # warm
             torch.cuda.synchronize()
-            L.check(lib.mgn_set_timing(h, 2), h)
-            for r in range(reps):
-                fn(ptr[r])
-            torch.cuda.synchronize()
-            tk = (C.c_double * 4)()
-            L.check(lib.mgn_get_timing(h, tk), h)
-            L.check(lib.mgn_set_timing(h, 0), h)
-            launch_us = tk[0] / max(int(tk[1]), 1) * 1e3
+            a0 = age + K
+            launch_us = kernel_launch_us(fn, K, reps)
             s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s_ev.record(stream)
-            for r in range(reps):
-                fn(ptr[reps + r])
+            L.check(sw_launches(fn, K, reps), h)
             e_ev.record(stream)
             torch.cuda.synchronize()
+            age += K * (1 + 2 * reps)
             us = s_ev.elapsed_time(e_ev) * 1e3 / (reps * K)
-            sweep[str(K)] = {"kernel_us_per_launch": launch_us, "kernel_us_per_step": launch_us / K,
+            sweep[str(K)] = {"age_steps": a0, "kernel_us_per_launch": launch_us,
+                             "kernel_us_per_step": launch_us / K,
                              "kernel_frac_survey_bytes": N * K * bpes / (launch_us * 1e-6) / 1e9 / PEAK_HBM_GBS,
                              "back_to_back_us_per_step": us, "env_steps_per_s": N / us * 1e6,
                              "achieved_GBs_survey_bytes": N * bpes / us / 1e3,
                              "fused_bytes_per_env_step": bytes_per_env_step(A, K, env.D),
                              "launches": reps}
-        del big, sw_actions
+        tgt = max(5000, age)
+        ages[str(tgt)] = at_age(tgt)
+        del sw_fns, sw_traj, sw_actions
 
     if rank == 0 and args.dump_stats:
         np.save(args.dump_stats, gathered.cpu().numpy())
@@ -543,8 +618,11 @@ def main():
             roof["bound_note"] = (f"PMC: VALU issue >= {busy:.2f} of SIMD cycles vs HBM traffic "
                                   f"{roof['measured_traffic_frac']:.2f} of 8 TB/s")
         if probe:
+            # attainable: the better of this box's copy probe and the guide's
+            # float4 copy (6.29 TB/s, MI355X_MICROARCH.md)
             roof["attainable_copy_GBs"] = probe
-            roof["frac_of_attainable"] = achieved_gbs / probe
+            roof["attainable_GBs"] = max(probe, GUIDE_COPY_GBS)
+            roof["frac_of_attainable"] = achieved_gbs / roof["attainable_GBs"]
         res = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
@@ -565,13 +643,20 @@ def main():
             "stats_allgather_us": allgather_us,
             "allgather_path": allgather_path,
         }
+        if steady:
+            res["steady_state"] = steady
+            res["episode_age"] = ages
+            res["episode_age_note"] = (
+                "the headline's launch on the same handle after the timed region, at the handle's step "
+                "index age_steps (fresh actions): kernel time from the launch's own HIP events; the "
+                "steady-state figure is the one after >= 2000 untimed steps (episodes ended)")
         if sweep:
             res["launch_lengths"] = sweep
             res["launch_lengths_note"] = (
-                "K steps per launch on the same handle after the timed region: kernel_us_per_launch "
-                "from the launch's own HIP events; back_to_back_us_per_step from events around "
-                "`launches` launches issued by the per-launch binding (host + dispatch included); "
-                "frac on SURVEY 8d bytes (1393 B per C3 env-step) over the kernel time")
+                "K steps per launch on the same handle at steady state (age_steps: the handle's step "
+                "index): kernel_us_per_launch from the launch's own HIP events; back_to_back_us_per_step "
+                "from events around `launches` launches issued by the per-launch binding (host + "
+                "dispatch included); frac on SURVEY 8d bytes (1393 B per C3 env-step) over the kernel time")
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(N, A, args.cpu_budget)
         print(json.dumps(res))

@@ -116,11 +116,45 @@ def deps():
         os.path.join(ROOT, "include", "madigan_amd.h")]
 
 
+# the compile configuration the library was built with (flags per unit and
+# the compiler): a change of FLAGS / UNIT_FLAGS alone rebuilds, so an A/B of a
+# flag never measures a stale library
+FLAGS_STAMP = os.path.join(OBJ, "flags.txt")
+# per kernel: registers, scratch and occupancy as the compiler reports them
+# (-Rpass-analysis=kernel-resource-usage), written by every build and read by
+# tests/test_build.py (no step kernel may spill to scratch)
+RESOURCE_USAGE = os.path.join(OBJ, "resource_usage.json")
+
+
+def _flags_key() -> str:
+    units = {os.path.basename(s): UNIT_FLAGS.get(os.path.basename(s), []) for s in sources()}
+    return repr((FLAGS, sorted(units.items()), ARCH))
+
+
 def needs_build() -> bool:
-    if not os.path.exists(OUT):
+    if not os.path.exists(OUT) or not os.path.exists(FLAGS_STAMP) or not os.path.exists(RESOURCE_USAGE):
         return True
+    with open(FLAGS_STAMP) as f:
+        if f.read() != _flags_key():
+            return True
     t = os.path.getmtime(OUT)
     return any(os.path.getmtime(d) > t for d in deps())
+
+
+def parse_resource_usage(text: str) -> dict:
+    """The compiler's kernel-resource-usage remarks -> {kernel: {field: int}}."""
+    import re
+    out, cur = {}, None
+    for line in text.splitlines():
+        m = re.search(r"remark: [^:]*:?\s*Function Name: (\S+)", line)
+        if m:
+            cur = out.setdefault(m.group(1), {})
+            continue
+        m = re.search(r"remark: .*?(SGPRs|VGPRs|AGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]|"
+                      r"SGPRs Spill|VGPRs Spill|LDS Size \[bytes/block\]): (\d+)", line)
+        if m and cur is not None:
+            cur[m.group(1).split(" [")[0]] = int(m.group(2))
+    return out
 
 
 def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
@@ -134,18 +168,27 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
 
     def compile_one(src):
         obj = os.path.join(OBJ, os.path.basename(src).replace(".hip", ".o"))
-        cmd = [cc, *FLAGS, *UNIT_FLAGS.get(os.path.basename(src), []), "-c", "-o", obj, src]
+        cmd = [cc, *FLAGS, *UNIT_FLAGS.get(os.path.basename(src), []),
+               "-Rpass-analysis=kernel-resource-usage", "-c", "-o", obj, src]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed on {src}:\n{r.stderr}")
-        if r.stderr.strip() and verbose:
-            print(r.stderr, file=sys.stderr)
-        return obj
+        usage = parse_resource_usage(r.stderr)
+        rest = "\n".join(ln for ln in r.stderr.splitlines() if "warning:" in ln).strip()
+        if rest and verbose:
+            print(rest, file=sys.stderr)
+        return obj, os.path.basename(src), usage
 
     with ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(compile_one, sources()))
+        res = list(ex.map(compile_one, sources()))
+    objs = [r[0] for r in res]
+    import json
+    with open(RESOURCE_USAGE, "w") as f:
+        json.dump({unit: usage for _, unit, usage in res}, f, indent=0, sort_keys=True)
+    with open(FLAGS_STAMP, "w") as f:
+        f.write(_flags_key())
     cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs, "-ldl"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

@@ -407,12 +407,22 @@ int choose_m(int n_envs, int apad) {
 void launch_step(const mgn_env* e, const mgn_traj& out, int in_kind, const double* units,
                  const int32_t* aidx, const int8_t* act, int K, hipEvent_t ev0, hipEvent_t ev1) {
   mgn::StepArgs a{kparams(e), out, in_kind, units, aidx, act, K, e->stream, ev0, ev1};
-#ifndef MGN_NO_GK  // diagnostic A/B builds: the generic generator role everywhere
+#if !(defined(MGN_DIAG) && defined(MGN_NO_GK))  // diagnostic A/B builds: the generic generator role everywhere
   a.gkind = e->kinds[0];
   for (int i = 1; i < e->A; ++i)
     if (e->kinds[i] != a.gkind) a.gkind = -1;
 #endif
-  if (e->trio) {
+  // a 9..16-asset window handle takes the three-role kernel (automatic
+  // schedule) for the launches its two-slot layout runs -- discrete steps,
+  // trio_m2_ok; its one-slot layout measured slower than the two-role kernel
+  // there, so the handle's other launches (units, single orders) run that
+  bool trio = e->trio;
+  if (trio && e->sched == MGN_SCHED_AUTO && e->apad > 8 && e->W > 0 && !e->replay &&
+      !mgn::trio_m2_ok(e->N, e->A, e->cfg.nstep, e->D, in_kind) && duo_eligible(e)) {
+    kDuo[4](a);
+    return;
+  }
+  if (trio) {
     const int idx = e->apad <= 2 ? 1 : e->apad <= 4 ? 2 : e->apad <= 8 ? 3 : 4;
     kTrio[idx](a);
     return;

@@ -1,0 +1,72 @@
+// mgn_diag.h -- diagnostic builds only (tools/build_variant.py passes
+// -DMGN_DIAG): the cycle stamps, iteration stamps and wall-clock records of
+// the step kernels, and the ablation switches, which produce wrong outputs
+// and exist to time what a part of the step costs.  In the product build
+// every hook below is empty, and setting an ablation or stamp macro without
+// MGN_DIAG is an error.
+#pragma once
+
+#if !defined(MGN_DIAG) &&                                                                            \
+    (defined(MGN_STAMPS) || defined(MGN_WALLX) || defined(MGN_ITERSTAMP) || defined(MGN_ABL_NOSTORE) ||  \
+     defined(MGN_ABL_NOSTORE_ASSET) || defined(MGN_ABL_NOSTORE_ENV) || defined(MGN_ABL_DRAW) ||          \
+     defined(MGN_TRIO_ABL_PRO) || defined(MGN_TRIO_ABL_G) || defined(MGN_TRIO_ABL_L) ||                  \
+     defined(MGN_TRIO_ABL_F) || defined(MGN_TRIO_ABL_EPI) || defined(MGN_NST_ABL_TERM) ||                \
+     defined(MGN_NST_ABL_SUM) || defined(MGN_NST_ABL_ROW) || defined(MGN_NO_GK))
+#error "stamp / ablation switches belong to diagnostic builds (-DMGN_DIAG, tools/build_variant.py)"
+#endif
+
+namespace mgn {
+
+#ifdef MGN_STAMPS
+// diagnostic build only: per role, cycles of [work 1, wait A, work 2, wait B]
+// summed over one wave per role and block, then the iteration count
+__device__ unsigned long long g_duo_stamps[24];
+// per-block sub-phase accumulators, one writer (the block's first ledger lane)
+__shared__ unsigned long long s_duo_sub[8];
+// wall clock (s_memrealtime, 100 MHz) per block (first 2048 blocks), plain
+// stores by one lane: [0] generator entry, [1] ledger entry, [2] ledger loop
+// start, [3] ledger loop end, [4] generator loop end, [5] generator exit,
+// [6] / [7] ledger after iteration 0 / 2
+__device__ unsigned long long g_duo_wall[2048 * 32];
+#define MGN_T(v) v = __builtin_amdgcn_s_memtime()
+#define MGN_WALL(i) if ((threadIdx.x & 255) == 0 && blockIdx.x < 2048) g_duo_wall[blockIdx.x * 32 + (i)] = __builtin_amdgcn_s_memrealtime()
+#elif defined(MGN_WALLX)
+// lighter diagnostic build: the wall stamps, the hardware ids and per block
+// the slowest iteration's phases ([12] generator store phase, [13] its
+// iteration, [14] ledger phase 1, [15] its iteration), no cycle accumulators
+__device__ unsigned long long g_duo_stamps[24];
+__device__ unsigned long long g_duo_wall[2048 * 32];
+#define MGN_T(v)
+#define MGN_WALL(i) if ((threadIdx.x & 255) == 0 && blockIdx.x < 2048) g_duo_wall[blockIdx.x * 32 + (i)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define MGN_T(v)
+#define MGN_WALL(i)
+#endif
+#ifdef MGN_WALLX
+#define MGN_RT(v) v = __builtin_amdgcn_s_memrealtime()
+#define MGN_WALLV(i, val_) if ((threadIdx.x & 255) == 0 && blockIdx.x < 2048) g_duo_wall[blockIdx.x * 32 + (i)] = (val_)
+#else
+#define MGN_RT(v)
+#define MGN_WALLV(i, val_)
+#endif
+
+#ifdef MGN_ITERSTAMP
+// diagnostic build: s_memtime stamps of the first 256 blocks, 64 slots each --
+// [0] entry, [1] after the prologue barrier, [2 + j] generator lane 0 after
+// iteration j's barrier (j < 40), [44] generator / [45] ledger / [46] finish
+// lane 0 after its epilogue stores (with their completion wait); [47] G lane 0
+// once the kernel arguments arrived, [48] G lane 0 once its iteration-0 tick
+// is published to LDS, [49] L lane 0 once its iteration-0 records are
+// published, [50] F lane 0 once its iteration-1 outputs are issued
+__device__ unsigned long long g_iter[256 * 64];
+#define MGN_IT(slot, lane0)                                             \
+  if (threadIdx.x == (lane0) && blockIdx.x < 256 && (slot) < 64)        \
+    g_iter[blockIdx.x * 64 + (slot)] = __builtin_amdgcn_s_memtime()
+#define MGN_IT_DRAIN() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#else
+#define MGN_IT(slot, lane0)
+#define MGN_IT_DRAIN()
+#endif
+
+
+}  // namespace mgn

@@ -37,38 +37,6 @@ namespace mgn {
 
 constexpr int DUO_BLOCK = 512;
 
-#ifdef MGN_STAMPS
-// diagnostic build only: per role, cycles of [work 1, wait A, work 2, wait B]
-// summed over one wave per role and block, then the iteration count
-__device__ unsigned long long g_duo_stamps[24];
-// per-block sub-phase accumulators, one writer (the block's first ledger lane)
-__shared__ unsigned long long s_duo_sub[8];
-// wall clock (s_memrealtime, 100 MHz) per block (first 2048 blocks), plain
-// stores by one lane: [0] generator entry, [1] ledger entry, [2] ledger loop
-// start, [3] ledger loop end, [4] generator loop end, [5] generator exit,
-// [6] / [7] ledger after iteration 0 / 2
-__device__ unsigned long long g_duo_wall[2048 * 32];
-#define MGN_T(v) v = __builtin_amdgcn_s_memtime()
-#define MGN_WALL(i) if ((threadIdx.x & 255) == 0 && blockIdx.x < 2048) g_duo_wall[blockIdx.x * 32 + (i)] = __builtin_amdgcn_s_memrealtime()
-#elif defined(MGN_WALLX)
-// lighter diagnostic build: the wall stamps, the hardware ids and per block
-// the slowest iteration's phases ([12] generator store phase, [13] its
-// iteration, [14] ledger phase 1, [15] its iteration), no cycle accumulators
-__device__ unsigned long long g_duo_stamps[24];
-__device__ unsigned long long g_duo_wall[2048 * 32];
-#define MGN_T(v)
-#define MGN_WALL(i) if ((threadIdx.x & 255) == 0 && blockIdx.x < 2048) g_duo_wall[blockIdx.x * 32 + (i)] = __builtin_amdgcn_s_memrealtime()
-#else
-#define MGN_T(v)
-#define MGN_WALL(i)
-#endif
-#ifdef MGN_WALLX
-#define MGN_RT(v) v = __builtin_amdgcn_s_memrealtime()
-#define MGN_WALLV(i, val_) if ((threadIdx.x & 255) == 0 && blockIdx.x < 2048) g_duo_wall[blockIdx.x * 32 + (i)] = (val_)
-#else
-#define MGN_RT(v)
-#define MGN_WALLV(i, val_)
-#endif
 constexpr int DUO_HALF = DUO_BLOCK / 2;
 
 enum { REC_STEP = 1, REC_TICK = 2, REC_DONE = 4, REC_MCALL = 8 };
@@ -172,8 +140,6 @@ template <typename T>
 __device__ __forceinline__ void ost(MGN_G T* q, T v) {
 #if defined(MGN_ABL_NOSTORE)  // diagnostic timing build: outputs not stored
   (void)q; (void)v;
-#elif defined(MGN_X_NT)
-  __builtin_nontemporal_store(v, q);
 #else
   *q = v;
 #endif
@@ -185,15 +151,8 @@ struct GState {
 };
 
 // One-step shaping (DSR / DDR / PPC / naive, n = 1) runs on the ledger side,
-// right after the step's reward.  MGN_X_GEN_SHAPE moves it to the generator
-// side (the shaper state feeds only the shaped reward): measured slower at
-// C3 (2.79 -> 2.95 us per step at 256-step launches; the generator's store
-// phase then sets phase 2), kept as a diagnostic build.
-#ifdef MGN_X_GEN_SHAPE
-constexpr bool kGenShape = true;
-#else
-constexpr bool kGenShape = false;
-#endif
+// right after the step's reward (on the generator side it measured slower at
+// C3, 2.79 -> 2.95 us per step at 256-step launches, round 1).
 
 // The step finish is split between the roles.  The ledger lanes evaluate it
 // (ledger_finish: Env.h:211-229 reward, Portfolio.cpp:150-155
@@ -247,9 +206,8 @@ __device__ __forceinline__ void ledger_finish(DuoRec<S>& rc, const Lane<1>& s, c
     cos_term = p.cos_temp * (dot / (np_ * g.cos_qn));
   }
   double shaped_s = 0., rin_s = 0., shaped_v = 0.;
-  if constexpr (NST || kGenShape) {
-    // the generator side shapes (n = 1) or adds the column value to the
-    // NStepBuffer (n > 1)
+  if constexpr (NST) {
+    // the generator side adds the column value to the NStepBuffer
     if (D == 1) rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
   } else if (D == 1) {
     rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
@@ -348,10 +306,7 @@ __device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s,
       if (om & O_OPT) ost(out.obs_port + ((size_t)k * p.N * (A + 1) + (size_t)env * (A + 1) + 1 + s.asset[0]), portA);
       if (D != 1) {
         if (om & O_AREW) ost(out.agent_reward + (i), sh.rAr[l]);
-        if constexpr (!NST && kGenShape) {
-          const double v = shape(p.shaper, sh.rAr[l], ns.A, ns.B, p.eta, sh.rCos[el], p.sexp);
-          if (om & O_SHP) ost(out.shaped + (i), v);
-        } else if (!NST && (om & O_SHP)) {
+        if (!NST && (om & O_SHP)) {
           ost(out.shaped + (i), sh.rShv[l]);
         }
       }
@@ -367,24 +322,7 @@ __device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s,
       if (!NST && (om & O_NSH)) ost(out.n_shaped + (oN + env), (uint8_t)(1));
       if (D == 1) {
         if (om & O_AREW) ost(out.agent_reward + (oN + env), sh.rRin[el]);
-        if (!NST && !kGenShape && (om & O_SHP)) ost(out.shaped + (oN + env), sh.rShaped[el]);
-      }
-    }
-    if constexpr (!NST && kGenShape) {
-      if (D == 1) {
-        // every lane of the env evaluates the env's shaper (same operands)
-        const double r = sh.rRin[el];
-        double v;
-        if (p.shaper == MGN_SHAPER_DDR) {  // shape() for DDR (nstep_buffer.py:128-162)
-          v = clip1((0.0 + 1.0 * ddr_one_pre(r, ns.A, ns.B, ddr_pre(ns.A, ns.B))) / 1);
-          double m = r < 0. ? r : 0.;
-          if (r != r) m = r;
-          ns.A += p.eta * (r - ns.A);
-          ns.B += p.eta * (m * m - ns.B);
-        } else {
-          v = shape(p.shaper, r, ns.A, ns.B, p.eta, sh.rCos[el], p.sexp);
-        }
-        if (ls == 0 && (om & O_SHP)) ost(out.shaped + (oN + env), v);
+        if (!NST && (om & O_SHP)) ost(out.shaped + (oN + env), sh.rShaped[el]);
       }
     }
     if constexpr (NST) {
@@ -501,112 +439,17 @@ __device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s,
   }
 }
 
-#ifndef MGN_DUO_VAR
-#define MGN_DUO_VAR 0
-#endif
-// broker_spec's canonical trees over DPP in registers instead of every lane
-// reading every record's leaves from LDS
-#ifndef MGN_SPEC_DPP
-#define MGN_SPEC_DPP 1
-#endif
-// broker_spec's cash chain walked by one lane per env (published to LDS)
-// instead of by every lane of the env (each reading every record)
-#ifndef MGN_SPEC_CH1
-#define MGN_SPEC_CH1 1
-#endif
-// broker_spec: only the lanes whose check reads the sums (and the last lane)
-// walk the canonical tree (measured 6 % slower per step at C3: the branch
-// around the tree keeps its LDS reads from overlapping the cash chain;
-// profiles/r04_ab_tree_skip.txt)
-#ifndef MGN_SPEC_TREE_SKIP
-#define MGN_SPEC_TREE_SKIP 0
-#endif
-
-// Broker::handleTransaction(units) for a segment of S lanes, one asset per
-// lane, resolved speculatively.  The serial dependency between orders (each
-// risk check sees the cash and portfolio sums the earlier orders left,
-// Broker.cpp:149-155) is only a dependency on which earlier orders executed.
-// Guess that every nonzero order executes; then each lane checks ITS order
-// against the state the guess implies -- the cash chain c_i over the earlier
-// executed orders (the same (((c + X1) - y) - Z) sequence as the serial form)
-// and the canonical trees over the leaves (executed earlier orders: post-order
-// leaves, the rest: pre-order) -- all lanes in parallel.  The checks up to the
-// first order whose outcome contradicts the guess are exact; that order's
-// outcome is taken from its check, later ones are re-guessed, repeat.  Every
-// check that is kept was evaluated on exactly the operands the serial form
-// uses, so the ledger, responses and sums are bit-identical to XRounds; an
-// unrefused batch (the common case) costs one pass instead of S dependent
-// rounds.
-// The four canonical sums (L*P, mep*L, short L*mep, borrowed margin) of one
-// pass, as a streaming pairwise tree: leaves are read from LDS in order and
-// each subtree is summed before the next is read, so log2(S) partials per sum
-// are live instead of S leaves (S = 16 kept all 64 leaf doubles in VGPRs and
-// spilled).  The grouping is tree<S>'s, so the sums are bit-identical.  Leaf j
-// is post-order (executed order before this lane's) where bit j of `post`.
-// RP: the subtree is on the root's rightmost path; its left children are
-// recorded in sib[level] so the last leaf can be replaced afterwards.
-struct Q4 {
-  double a, b, c, d;
-};
-__device__ __forceinline__ Q4 q4add(const Q4& x, const Q4& y) {
-  return Q4{x.a + y.a, x.b + y.b, x.c + y.c, x.d + y.d};
-}
-template <int N>
-constexpr int ilog2() { return N <= 1 ? 0 : 1 + ilog2<N / 2>(); }
-// FENCE (the three-role kernel at S = 16): a scheduling fence between the
-// halves of every subtree of >= 8 leaves keeps the scheduler from hoisting the
-// right half's leaf loads above the left half's sums -- all 64 leaf doubles
-// live at once spilled its ledger waves (168 VGPRs + 37 spilled -> 134, none;
-// 16 TrendOU assets 7.7 -> 5.3 us/step).  The two-role kernel, at two waves
-// per SIMD either way, runs slower fenced (6.3 -> 6.8) and is not.
-template <int S, int LO, int N, bool RP, bool FENCE = false>
-__device__ __forceinline__ Q4 tree4(const EnvRecs<S>& er, uint32_t post, Q4 (&sib)[6]) {
-  if constexpr (N == 1) {
-    const d2* rv = reinterpret_cast<const d2*>(&er.r[LO]) + (((post >> LO) & 1u) ? 2 : 0);
-    const d2 a = rv[0], b = rv[1];
-    return Q4{a.x, a.y, b.x, b.y};
-  } else {
-    const Q4 l = tree4<S, LO, N / 2, false, FENCE>(er, post, sib);
-    if constexpr (FENCE && N >= 8) __builtin_amdgcn_sched_barrier(0);
-    const Q4 r = tree4<S, LO + N / 2, N / 2, RP, FENCE>(er, post, sib);
-    if constexpr (RP) sib[ilog2<N>() - 1] = l;
-    return q4add(l, r);
-  }
-}
-
 // One order of the Broker's cash chain (Broker.cpp:128-135): cash becomes
-// ((cash + X1) - y) - Z when the order executes.  MGN_SPEC_CHMASK: a skipped
-// order adds the identities of the same operations (c + -0.0 and c - +0.0 are
-// c, bit for bit, for every c), so the select of the terms leaves the chain's
-// dependency -- three dependent additions per order, no select behind them.
-// Measured slower (20-step 2.22-2.24 -> 2.29-2.30 us/step, 256-step 1.92-1.93
-// -> 2.02-2.03: profiles/r04_ab_chain_mask.txt): off
-#ifndef MGN_SPEC_CHMASK
-#define MGN_SPEC_CHMASK 0
-#endif
-// (MASK false at two slots per lane: 16 orders' masked terms formed ahead of
-// the chain spilled at the 168-register budget)
-template <bool MASK = MGN_SPEC_CHMASK != 0>
+// ((cash + X1) - y) - Z when the order executes.  (Tried and not kept, round
+// 4: the skipped orders' terms masked to the additions' identities, 2-5 %
+// slower, profiles/r04_ab_chain_mask.txt; a one-subtraction chain when no
+// order of the wave closes or settles, mixed, profiles/r04_ab_plain_chain.txt)
 __device__ __forceinline__ double chain_step(double c, double X1, double y, double Z, bool go) {
-  if (MASK) return ((c + (go ? X1 : -0.0)) - (go ? y : 0.0)) - (go ? Z : 0.0);
   const double ci = ((c + X1) - y) - Z;
   return go ? ci : c;
 }
 
-// MGN_SPEC_PLAIN: when no order of the wave closes a position or settles a
-// borrowed margin (X1 = -0.0 and Z = +0.0 bit for bit: every order at a
-// required margin of 1 that buys or closes exactly), the cash update of an
-// executed order is cash - y -- c + -0.0 and x - +0.0 are c and x for every
-// value -- one dependent subtraction per order on the chain instead of three
-// (a uniform branch on the wave's ballot).  Measured mixed
-// (profiles/r04_ab_plain_chain.txt: one-step launches -3 %, 16 assets -3 %,
-// 256-step C3 +2-4 %, C5 +10 % -- the second walk's registers spill at two
-// slots per lane): off
-#ifndef MGN_SPEC_PLAIN
-#define MGN_SPEC_PLAIN 0
-#endif
-
-// The canonical trees of broker_spec in registers (MGN_SPEC_DPP): every lane
+// The canonical trees of broker_spec in registers: every lane
 // holds its own order's four leaves before (pre) and after (post) the order;
 // the tree of lane ls's check has post leaves for the executed orders j < ls
 // and pre leaves elsewhere.  Level by level, a lane takes its sibling
@@ -649,7 +492,22 @@ __device__ __forceinline__ void dpp_tree4(const double (&pre)[4], const double (
   for (int q = 0; q < 4; ++q) rootP[q] = nP[q];
 }
 
-template <int S, bool RQ1, bool LOWREG>
+// Broker::handleTransaction(units) for a segment of S lanes, one asset per
+// lane, resolved speculatively.  The serial dependency between orders (each
+// risk check sees the cash and portfolio sums the earlier orders left,
+// Broker.cpp:149-155) is only a dependency on which earlier orders executed.
+// Guess that every nonzero order executes; then each lane checks ITS order
+// against the state the guess implies -- the cash chain c_i over the earlier
+// executed orders (the same (((c + X1) - y) - Z) sequence as the serial form)
+// and the canonical trees over the leaves (executed earlier orders: post-order
+// leaves, the rest: pre-order) -- all lanes in parallel.  The checks up to the
+// first order whose outcome contradicts the guess are exact; that order's
+// outcome is taken from its check, later ones are re-guessed, repeat.  Every
+// check that is kept was evaluated on exactly the operands the serial form
+// uses, so the ledger, responses and sums are bit-identical to XRounds; an
+// unrefused batch (the common case) costs one pass instead of S dependent
+// rounds.
+template <int S, bool RQ1>
 __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRecs<S>& er,
                                             double& cash, const double (&uc)[1], double (&tp)[1],
                                             double (&tu)[1], double (&tc)[1], int (&rk)[1], int ls,
@@ -658,90 +516,29 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
 #ifdef MGN_STAMPS
   const unsigned long long t_a = __builtin_amdgcn_s_memtime();
 #endif
-  double lf_pre[4], lf_post[4];  // MGN_SPEC_DPP: the own leaves and check operands, in registers
+  double lf_pre[4], lf_post[4];  // the own leaves and check operands, in registers
   OwnChk oc[1];
-  order_prep<1, S, !MGN_SPEC_DPP>(s, p, er, uc, ls, cu2, me2, bm3, tpr, tco, lf_pre, lf_post, oc);
+  order_prep<1, S, false>(s, p, er, uc, ls, cu2, me2, bm3, tpr, tco, lf_pre, lf_post, oc);
 #ifdef MGN_STAMPS
   const unsigned long long t_b = __builtin_amdgcn_s_memtime();
 #endif
-#if MGN_SPEC_DPP
   const OwnChk& own = oc[0];
-  // every order of the wave plain (MGN_SPEC_PLAIN): a uniform value
-  const bool wave_plain = __builtin_amdgcn_ballot_w64(!own.plain) == 0;
-#else
-  const OrderRec& own = er.r[ls];
-#endif
   const int act = uc[0] != 0. ? 1 : 0;
-  // the lanes whose risk check reads the sums before their order (an order
-  // that is checked at all: Portfolio.cpp:257-265 leaves an opposite-side
-  // order with u <= -cur unchecked), and the last lane, whose tree also
-  // yields the sums after every order: the others skip the tree's LDS reads
-  // (their lanes idle in its instructions)
-#if MGN_SPEC_TREE_SKIP
-  [[maybe_unused]] const bool need_tree = (act && (own.need_mc || own.need_insuff)) || ls == S - 1;
-#else
-  [[maybe_unused]] constexpr bool need_tree = true;
-#endif
   const uint32_t act_bits = (uint32_t)seg_or<S>(act << ls);
   uint32_t go_bits = act_bits;  // the guess
   const double cash0 = cash;
   int go = 0, mc = 0, insuff = 0;
   double cend = cash0;
-  // S <= 8: the leaves of the last (consistent) pass in registers (measured
-  // ~1 % faster at S = 8 than the streaming tree); S = 16 or LOWREG (the
-  // three-role kernel's 168-VGPR budget): the streaming tree, its
-  // rightmost-path left children kept
-  [[maybe_unused]] constexpr bool STREAM = LOWREG || S >= 16;
-#if !MGN_SPEC_DPP
-  Q4 sib[6];
-  double lv[4][STREAM ? 1 : S];
-#endif
-  double rootP[4];  // MGN_SPEC_DPP: the sums after the orders the pass took
+  double rootP[4];  // the sums after the orders the pass took
   for (int it = 0; it <= S; ++it) {
     // canonical sums before this lane's order: leaves of executed earlier
     // orders after the order, the others before
-    double r0 = 0., r1 = 0., r2 = 0., r3 = 0.;
-#if MGN_SPEC_DPP
-    {
-      double path[4];
-      dpp_tree4<S>(lf_pre, lf_post, ((go_bits >> ls) & 1) != 0, ls, path, rootP);
-      r0 = path[0];
-      r1 = path[1];
-      r2 = path[2];
-      r3 = path[3];
-    }
-#else
-    if constexpr (STREAM) {
-      if (need_tree) {
-        const Q4 rt = tree4<S, 0, S, true, LOWREG && S >= 16>(er, go_bits & ((1u << ls) - 1u), sib);
-        r0 = rt.a;
-        r1 = rt.b;
-        r2 = rt.c;
-        r3 = rt.d;
-      }
-    } else if (need_tree) {
-#pragma unroll
-      for (int j = 0; j < S; ++j) {
-        const bool post = (j < ls) && ((go_bits >> j) & 1);
-        const d2* rv = reinterpret_cast<const d2*>(&er.r[j]) + (post ? 2 : 0);
-        const d2 a = rv[0], b = rv[1];
-        lv[0][j] = a.x;
-        lv[1][j] = a.y;
-        lv[2][j] = b.x;
-        lv[3][j] = b.y;
-      }
-      r0 = tree<S>(lv[0]);
-      r1 = tree<S>(lv[1]);
-      r2 = tree<S>(lv[2]);
-      r3 = tree<S>(lv[3]);
-    }
-#endif
-    // cash before this lane's order, and after the last order, under the guess
-    double c_own = cash0;
-#if MGN_SPEC_CH1
-    // the chain is the env's, not the lane's: its first lane walks it (its
-    // records' cash terms read by one lane of the env, not all of them) and
-    // publishes the cash before every order and after the last
+    double r[4];
+    dpp_tree4<S>(lf_pre, lf_post, ((go_bits >> ls) & 1) != 0, ls, r, rootP);
+    // cash before this lane's order, and after the last order, under the
+    // guess: the chain is the env's, not the lane's, so its first lane walks
+    // it (one lane of the env reads the records' cash terms) and publishes
+    // the cash before every order and after the last
     if (ls == 0) {
       double c = cash0;
 #pragma unroll
@@ -749,43 +546,21 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
         er.cpre[i] = c;
         const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
         const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
-        if (MGN_SPEC_DPP && MGN_SPEC_PLAIN && wave_plain)
-          c = ((go_bits >> i) & 1) ? c - yz.x : c;
-        else
-          c = chain_step(c, xz.y, yz.x, yz.y, ((go_bits >> i) & 1) != 0);
+        c = chain_step(c, xz.y, yz.x, yz.y, ((go_bits >> i) & 1) != 0);
       }
       er.cpre[S] = c;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    c_own = er.cpre[ls];
+    const double c_own = er.cpre[ls];
     cend = er.cpre[S];
-#else
-    {
-      double c = cash0;
-#pragma unroll
-      for (int i = 0; i < S; ++i) {
-        // the three-role kernel at S = 16: records read four at a time (a
-        // scheduling fence per group, as tree4's FENCE)
-        if constexpr (LOWREG && S >= 16) {
-          if (i > 0 && i % 4 == 0) __builtin_amdgcn_sched_barrier(0);
-        }
-        if (i == ls) c_own = c;
-        const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
-        const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
-        const double ci = ((c + xz.y) - yz.x) - yz.y;
-        c = ((go_bits >> i) & 1) ? ci : c;
-      }
-      cend = c;
-    }
-#endif
     // Portfolio::checkRisk(i, u), Portfolio.cpp:254-279 (as XRounds)
-    const double pnl = r0 - r1;
-    const double balance = c_own + r2;
+    const double pnl = r[0] - r[1];
+    const double balance = c_own + r[2];
     const double bp = balance + pnl;
     const double availM = RQ1 ? bp : bp / p.reqM;
-    const double equity = (c_own + r0) - r3;
+    const double equity = (c_own + r[0]) - r[3];
     const double mr = p.mainM * pnl;
     mc = (own.need_mc != 0) & ((equity <= -mr) | (bp <= -mr));
     insuff = (own.need_insuff != 0) & ((availM <= own.aPX) | (balance <= 0.));
@@ -807,39 +582,12 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
   any_mc = seg_or<S>(act & mc) != 0;
   rk[0] = act ? (mc ? MGN_MARGIN_CALL : (insuff ? MGN_INSUFF_MARGIN : MGN_GREEN)) : rk[0];
   const bool go_own[1] = {go != 0};
-  // the post-transaction sums: the last lane's leaves are final but its own;
-  // settle that one (its leaf at the bottom of the rightmost path, the left
-  // children recorded) and broadcast its trees to the segment
-#if MGN_SPEC_DPP
-  // the root of the last pass's P tree: its guess held for every order
+  // the post-transaction sums: the root of the last pass's P tree (its guess
+  // held for every order)
   after.lp = rootP[0];
   after.ml = rootP[1];
   after.sh = rootP[2];
   after.b = rootP[3];
-#else
-  Q4 x;
-  if constexpr (STREAM) {
-    const d2* rv = reinterpret_cast<const d2*>(&er.r[S - 1]) + ((ls == S - 1 && go) ? 2 : 0);
-    const d2 la = rv[0], lb = rv[1];
-    x = Q4{la.x, la.y, lb.x, lb.y};
-#pragma unroll
-    for (int k = 0; k < ilog2<S>(); ++k) x = q4add(sib[k], x);
-  } else {
-    if (ls == S - 1 && go) {
-      const d2* rv = reinterpret_cast<const d2*>(&er.r[S - 1]) + 2;
-      const d2 a = rv[0], b = rv[1];
-      lv[0][S - 1] = a.x;
-      lv[1][S - 1] = a.y;
-      lv[2][S - 1] = b.x;
-      lv[3][S - 1] = b.y;
-    }
-    x = Q4{tree<S>(lv[0]), tree<S>(lv[1]), tree<S>(lv[2]), tree<S>(lv[3])};
-  }
-  after.lp = seg_bcast<S, S - 1>(x.a);
-  after.ml = seg_bcast<S, S - 1>(x.b);
-  after.sh = seg_bcast<S, S - 1>(x.c);
-  after.b = seg_bcast<S, S - 1>(x.d);
-#endif
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   apply_orders<1>(s, go_own, cu2, me2, bm3, tpr, tco, uc, tp, tu, tc);
@@ -860,8 +608,8 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
 // of slot 0 reads the pair pre + pre, slot 1 (post of slot 0 where it
 // executes) + pre, and the pair's P / Q versions go on to dpp_tree4's
 // cross-lane levels, which add the same sibling to both slots' paths.  The
-// cash chain is walked by the env's first lane over all 2 S orders, as
-// broker_spec's MGN_SPEC_CH1; the fix-up of a wrong guess is broker_spec's
+// cash chain is walked by the env's first lane over all 2 S orders, as in
+// broker_spec; the fix-up of a wrong guess is broker_spec's
 // (the first order whose check disagrees decides, the later ones are guessed
 // again), so the result is the sequential Broker's.
 template <int S, bool RQ1>
@@ -873,7 +621,6 @@ __device__ __forceinline__ void broker_spec_m2(Lane<2>& s, const KParams& p, Env
   double lf_pre[4 * M], lf_post[4 * M];
   OwnChk oc[M];
   order_prep<M, S, false>(s, p, er, uc, ls, cu2, me2, bm3, tpr, tco, lf_pre, lf_post, oc);
-  const bool wave_plain = __builtin_amdgcn_ballot_w64(!(oc[0].plain && oc[1].plain)) == 0;  // (MGN_SPEC_PLAIN)
   // the leaves are re-formed in every pass from the slot state the lane
   // holds anyway (ledger, price, and the order's outcome): the same products
   // (order_prep's), so the same bits, without 16 leaf registers live across
@@ -943,10 +690,7 @@ __device__ __forceinline__ void broker_spec_m2(Lane<2>& s, const KParams& p, Env
         er.cpre[i] = c;
         const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
         const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
-        if (MGN_SPEC_PLAIN && wave_plain)
-          c = ((go_bits >> i) & 1) ? c - yz.x : c;
-        else
-          c = chain_step<false>(c, xz.y, yz.x, yz.y, ((go_bits >> i) & 1) != 0);
+        c = chain_step(c, xz.y, yz.x, yz.y, ((go_bits >> i) & 1) != 0);
       }
       er.cpre[APAD] = c;
     }
@@ -1070,15 +814,14 @@ __device__ __forceinline__ void duo_replay_tick(Lane<1>& s, const KParams& p, ui
 // step per iteration, so every iteration j < K - 1 is followed by another and
 // the shared `more` flag (an LDS round trip on both roles' paths) is read only
 // from iteration K - 1 on
-#ifndef MGN_DUO_MORESKIP
-#define MGN_DUO_MORESKIP 1
-#endif
 template <int S, bool RQ1, bool ABL, bool DISC, bool RP, bool NST, int GK = -1>
 __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out, int in_kind_rt,
                                                         const double* __restrict__ units_in,
                                                         const int32_t* __restrict__ aidx_in,
                                                         const int8_t* __restrict__ act_in, int K) {
-  warm_kernargs<(int)(sizeof(KParams) + sizeof(mgn_traj) + 48)>();
+  // the argument segment: KParams, mgn_traj, in_kind_rt (padded to 8),
+  // units_in, aidx_in, act_in, K
+  warm_kernargs<(int)(sizeof(KParams) + sizeof(mgn_traj) + 8 + 24 + 4)>();
   const int in_kind = DISC ? IN_DISCRETE : in_kind_rt;
   MGN_WALL(threadIdx.x < DUO_HALF ? 0 : 1);
 #if defined(MGN_STAMPS) || defined(MGN_WALLX)
@@ -1142,7 +885,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       s.tlen[0] = p.tlen[li];
       s.tfl[0] = p.tfl[li];
     }
-    if constexpr (NST || kGenShape) {  // the generator side owns the shaper state
+    if constexpr (NST) {  // the generator side owns the shaper state
       if (p.D == 1) {
         nst.A = p.sA[envc];
         nst.B = p.sB[envc];
@@ -1305,7 +1048,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       acc[0] += T1 - T0; acc[1] += T2 - T1; acc[2] += T3 - T2; acc[3] += T4 - T3;
 #endif
       // a wave-uniform (scalar) exit test: the fin pass skips a barrier
-      if ((!MGN_DUO_MORESKIP || j + 1 >= K) && !__builtin_amdgcn_readfirstlane(sh.more[j % 3])) {
+      if (j + 1 >= K && !__builtin_amdgcn_readfirstlane(sh.more[j % 3])) {
         fin = true;
         MGN_WALL(4);
       }
@@ -1337,7 +1080,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
         p.nhead[env] = nst.head;
       }
     }
-    if constexpr (NST || kGenShape) {
+    if constexpr (NST) {
       if (p.D == 1) {
         if (ls == 0) {
           p.sA[env] = nst.A;
@@ -1453,7 +1196,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
       prevVal = s.L[0] * s.P[0];
       MGN_T(Ta);
       if (in_kind != IN_NONE && !(ABL && (p.ablate & 1))) {
-        broker_spec<S, RQ1, false>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, sa, any_mc);
+        broker_spec<S, RQ1>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, sa, any_mc);
         mcall = margin_call(sa, cash, p.mainM) ? 1 : 0;  // Broker.cpp:156-157
       }
       MGN_T(Tb);
@@ -1560,7 +1303,7 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
     if (j == 0) MGN_WALL(6);
     if (j == 2) MGN_WALL(7);
 #endif
-    if ((!MGN_DUO_MORESKIP || j + 1 >= K) && !__builtin_amdgcn_readfirstlane(sh.more[j % 3])) break;
+    if (j + 1 >= K && !__builtin_amdgcn_readfirstlane(sh.more[j % 3])) break;
   }
   MGN_WALL(3);
   MGN_WALLV(14, rmax);
@@ -1585,12 +1328,12 @@ __global__ __launch_bounds__(DUO_BLOCK) void k_step_duo(KParams p, mgn_traj out,
   }
   if (ls == 0) {
     p.cash[env] = cash;
-    if (!(NST || kGenShape) && D == 1) {  // else the generator side owns the shaper state
+    if (!(NST) && D == 1) {  // else the generator side owns the shaper state
       p.sA[env] = g.shA;
       p.sB[env] = g.shB;
     }
   }
-  if (!(NST || kGenShape) && D != 1 && s.valid[0]) {
+  if (!(NST) && D != 1 && s.valid[0]) {
     p.sA[(size_t)env * A + s.asset[0]] = g.shA;
     p.sB[(size_t)env * A + s.asset[0]] = g.shB;
   }

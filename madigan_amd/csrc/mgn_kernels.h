@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include "../../include/madigan_amd.h"
+#include "mgn_diag.h"
 #include "mgn_math.h"
 
 namespace mgn {
@@ -950,7 +951,6 @@ struct XRounds {
 struct OwnChk {
   double aPX;
   bool need_mc, need_insuff;
-  bool plain;  // X1 is -0.0 and Z +0.0 bit for bit: the cash update is cash - y
 };
 template <int M, int S, bool WPP = true>
 __device__ __forceinline__ void order_prep(const Lane<M>& s, const KParams& p, EnvRecs<M * S>& er,
@@ -1022,7 +1022,6 @@ __device__ __forceinline__ void order_prep(const Lane<M>& s, const KParams& p, E
       own[m].aPX = aPX;
       own[m].need_mc = !opp;
       own[m].need_insuff = !opp || rev;
-      own[m].plain = __double_as_longlong(X1v) == (long long)0x8000000000000000ULL && __double_as_longlong(Zv) == 0;
     }
   }
   // the segment's records are written by its own lanes: wave-scope ordering
@@ -1312,7 +1311,7 @@ __device__ __forceinline__ void nstep_column(const KParams& p, RingP ring, OutP 
 // RQ1: required_margin == 1.0, where x / required_margin == x exactly and the
 // divisions are skipped.  NST: n-step aggregation (nstep > 1) compiled in.
 // speculative Broker resolution for one asset per lane (defined in mgn_duo.h)
-template <int S, bool RQ1, bool LOWREG>
+template <int S, bool RQ1>
 __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRecs<S>& er,
                                             double& cash, const double (&uc)[1], double (&tp)[1],
                                             double (&tu)[1], double (&tc)[1], int (&rk)[1], int ls,
@@ -1487,7 +1486,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, mgn_traj out, int in_
             if constexpr (M == 1) {
               // one asset per lane: the speculative resolution of the two-role
               // kernel (mgn_duo.h) -- one pass when no order is refused
-              broker_spec<S, RQ1, false>(s, p, recs[tid / S], cash, uc, tp, tu, tc, rk, ls, sa, any_mc);
+              broker_spec<S, RQ1>(s, p, recs[tid / S], cash, uc, tp, tu, tc, rk, ls, sa, any_mc);
             } else {
               broker_x<M, S, RQ1>(s, p, recs[tid / S], cash, s0, uc, tp, tu, tc, rk, ls, sa, any_mc);
             }

@@ -53,11 +53,8 @@ constexpr size_t kTrioLdsMax = 160 * 1024;
 // the three-role kernel's two-slots-per-lane layout (launch_trio_m2): 9..16
 // assets at the 256-lane layout (N x 16 >= 256 x 256 lanes), discrete
 // actions, one-step rewards with a scalar shaper
-#ifndef MGN_TRIO_M2
-#define MGN_TRIO_M2 1
-#endif
 inline bool trio_m2_ok(long long n_envs, int A, int nstep, int D, int in_kind) {
-  return MGN_TRIO_M2 && A > 8 && A <= 16 && n_envs * 16 >= 65536 && nstep == 1 && D == 1 &&
+  return A > 8 && A <= 16 && n_envs * 16 >= 65536 && nstep == 1 && D == 1 &&
          in_kind == IN_DISCRETE;
 }
 void launch_trio_m2_a16(const StepArgs& a);

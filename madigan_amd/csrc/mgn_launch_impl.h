@@ -123,10 +123,7 @@ void launch_trio_nst(const StepArgs& a) {
   const int epb = (small ? 64 : TRIO_W) / S;
   const int grid = (a.p.N + epb - 1) / epb;
   const bool disc = a.in_kind == IN_DISCRETE;
-  // the kind-specialized instantiation keeps a third pad per env for the
-  // generator's prefix summands (MGN_NST_GPFX)
-  const bool gpfx = MGN_NST_GPFX && !small && disc && a.gkind == MGN_SRC_TRENDOU;
-  const size_t lds = trio_nst_dyn_lds(S, small ? 64 : TRIO_W, a.p.nstep, gpfx);
+  const size_t lds = trio_nst_dyn_lds(S, small ? 64 : TRIO_W, a.p.nstep);
   auto goN = [&](auto kern) {
     // a refused size is the caller's hipGetLastError (HIP records every
     // call's status); trio_eligible keeps static + dynamic LDS within 160 KiB

@@ -164,19 +164,16 @@ constexpr double TWO_M32 = 2.3283064365386962890625e-10;
 // IEEE operation.  The reward ratio curEq / prevEq stays IEEE: a small log
 // reward would carry its last-bit error at a large relative size.  Every step
 // kernel uses these helpers, so the schedules stay bit-identical.
-#ifndef MGN_FAST_RT
-#define MGN_FAST_RT 1
-#endif
 constexpr int kNormalClass = (1 << 3) | (1 << 8);  // v_cmp_class: -normal | +normal
 __device__ __forceinline__ double rt_div(double a, double b) {
-  if (!MGN_FAST_RT || !__builtin_amdgcn_class(b, kNormalClass)) return a / b;
+  if (!__builtin_amdgcn_class(b, kNormalClass)) return a / b;
   double r = __builtin_amdgcn_rcp(b);
   r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
   r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
   return a * r;
 }
 __device__ __forceinline__ double rt_sqrt(double x) {
-  if (!MGN_FAST_RT || !__builtin_amdgcn_class(x, 1 << 8)) return sqrt(x);
+  if (!__builtin_amdgcn_class(x, 1 << 8)) return sqrt(x);
   const double y = __builtin_amdgcn_rsq(x);
   double g = x * y, h = 0.5 * y;
   const double r = __builtin_fma(-g, h, 0.5);

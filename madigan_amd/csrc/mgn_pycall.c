@@ -8,6 +8,8 @@
  * way the reference's pybind11 Env.step binding calls Env::step.
  *
  *   rollout(env, actions, k, traj) -> int   (= mgn_rollout(env, actions, k, traj))
+ *   synchronize(env) -> int                 (= mgn_synchronize(env): the handle's
+ *                                            stream, not the whole device)
  *
  * env is the handle mgn_create returned, actions the (K, N, A) int8 device
  * actions, traj the mgn_traj the launcher validated -- the values the ctypes
@@ -37,9 +39,23 @@ static PyObject *rollout(PyObject *self, PyObject *const *args, Py_ssize_t nargs
   return PyLong_FromLong(mgn_rollout(env, actions, (int32_t)k, traj));
 }
 
+static PyObject *synchronize(PyObject *self, PyObject *arg) {
+  (void)self;
+  mgn_env *env = (mgn_env *)PyLong_AsVoidPtr(arg);
+  if (PyErr_Occurred()) return NULL;
+  if (env == NULL) {
+    PyErr_SetString(PyExc_ValueError, "synchronize: null handle");
+    return NULL;
+  }
+  int rc;
+  Py_BEGIN_ALLOW_THREADS rc = mgn_synchronize(env);
+  Py_END_ALLOW_THREADS return PyLong_FromLong(rc);
+}
+
 static PyMethodDef methods[] = {
     {"rollout", (PyCFunction)(void (*)(void))rollout, METH_FASTCALL,
      "mgn_rollout(env, actions, k, traj) -> int (MGN_OK = 0)"},
+    {"synchronize", (PyCFunction)synchronize, METH_O, "mgn_synchronize(env) -> int (MGN_OK = 0)"},
     {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_mgn_pycall", NULL, -1, methods};

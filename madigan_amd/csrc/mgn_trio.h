@@ -28,9 +28,9 @@
 // stands.  Every value is the same expression of the same operands as in
 // k_step, so every output is bit-identical to k_step / k_step_duo (and the
 // oracle).
-// Stores: F stores every output of the steps it confirms (MGN_TRIO_LST /
-// MGN_TRIO_GST move the BrokerResponse arrays to L, State.price and the
-// timestamp to G: measured slower); G and L write their state back at exit.
+// Stores: F stores every output of the steps it confirms (the BrokerResponse
+// arrays stored by L, or State.price and the timestamp by G, measured
+// slower, round 2); G and L write their state back at exit.
 // Scope: one asset slot per lane at APAD = S in {2, 4, 8, 16}, or two (MM = 2)
 // at S = 8 for 9..16 assets; generator sources or (16 assets) a replay tape;
 // n = 1 with or without a window (WIN: the finish role pushes the ring /
@@ -42,53 +42,15 @@
 
 namespace mgn {
 
-#ifdef MGN_ITERSTAMP
-// diagnostic build: s_memtime stamps of the first 256 blocks, 64 slots each --
-// [0] entry, [1] after the prologue barrier, [2 + j] generator lane 0 after
-// iteration j's barrier (j < 40), [44] generator / [45] ledger / [46] finish
-// lane 0 after its epilogue stores (with their completion wait); [47] G lane 0
-// once the kernel arguments arrived, [48] G lane 0 once its iteration-0 tick
-// is published to LDS, [49] L lane 0 once its iteration-0 records are
-// published, [50] F lane 0 once its iteration-1 outputs are issued
-__device__ unsigned long long g_iter[256 * 64];
-#define MGN_IT(slot, lane0)                                             \
-  if (threadIdx.x == (lane0) && blockIdx.x < 256 && (slot) < 64)        \
-    g_iter[blockIdx.x * 64 + (slot)] = __builtin_amdgcn_s_memtime()
-#define MGN_IT_DRAIN() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
-#else
-#define MGN_IT(slot, lane0)
-#define MGN_IT_DRAIN()
-#endif
-
 constexpr int TRIO_BLOCK = 768;
 constexpr int TRIO_W = 256;  // lanes per role
 // TW = 64 (one wave per role, 192-thread workgroups): small batches, whose
 // 256-lane workgroups would leave CUs idle (C2: 4096 envs x 4 assets fill 64
 // of 256 CUs at 256 lanes per role, all of them at 64)
 
-// which role stores what, and the roles' issue priorities (tuning switches;
-// the defaults are the measured best)
-#ifndef MGN_TRIO_LST
-#define MGN_TRIO_LST 0  // L stores the BrokerResponse arrays (else F)
-#endif
-#ifndef MGN_TRIO_GST
-#define MGN_TRIO_GST 0  // G stores State.price and timestamp (else F)
-#endif
-#ifndef MGN_TRIO_PG
-#define MGN_TRIO_PG 0
-#endif
-#ifndef MGN_TRIO_PL
-#define MGN_TRIO_PL 2
-#endif
-#ifndef MGN_TRIO_PF
-#define MGN_TRIO_PF 1
-#endif
-
-
-// generator lanes slot-major on handles of several source kinds (k_step_trio)
-#ifndef MGN_TRIO_GSLOT
-#define MGN_TRIO_GSLOT 1
-#endif
+// the roles' issue priorities (s_setprio; the ledger's orders are the
+// critical path -- equal priorities measured slower, round 2)
+constexpr int kPrioG = 0, kPrioL = 2, kPrioF = 1;
 
 // one-step launches (the agent loop): an auto-reset after the step absorbed
 // in the iteration that finds it (no window, generator sources): the
@@ -100,48 +62,23 @@ constexpr int TRIO_W = 256;  // lanes per role
 // candidate tick under the finish role's last iteration cost 1-2 %, so longer
 // launches run the reset in an iteration of its own
 // (profiles/r04_ab_tail_reset.txt)
-#ifndef MGN_TRIO_TAILRST
-#define MGN_TRIO_TAILRST 1
-#endif
-
+//
 // WIN with a log window: the generator role forms the window rows' log
-// prices (the finish role reads them from LDS)
-#ifndef MGN_TRIO_GLOG
-#define MGN_TRIO_GLOG 1
-#endif
-
-// NST (generator sources of one kind): the first pop's summands over the
-// entries already in the ring, and their ordered sum, formed by the generator
-// role at the start of the iteration while the finish role forms the step's
-// reward; the finish role waits for it (an LDS stamp) and adds the new
-// entry's summand -- the same operations in the same order.  Bit-identical
-// but neutral at n = 20 DDR (3.76-3.80 vs 3.80-3.81 us/step,
-// profiles/r04_ab_nst_prefix.txt): off
-#ifndef MGN_NST_GPFX
-#define MGN_NST_GPFX 0
-#endif
-
-// NST: the pop's ordered sum read back by the env's first lane only
-#ifndef MGN_NST_SUM1
-#define MGN_NST_SUM1 1
-#endif
-
+// prices (the finish role reads them from LDS; GLOG below)
+//
 // NST: rounds of a pop's summands evaluated together (the terms' chains
-// interleave; rounds past the buffer's are computed and dropped)
-#ifndef MGN_NST_U
-#define MGN_NST_U 3
-#endif
+// interleave; rounds past the buffer's are computed and dropped).  (Tried and
+// not kept, round 4: the generator role forming the first pop's prefix over
+// the entries already in the ring -- bit-identical, neutral at n = 20 DDR,
+// profiles/r04_ab_nst_prefix.txt)
+constexpr int kNstU = 3;
 
 // the loop's exit test after iteration j's barrier: iterations 0..K always
 // run (the K steps, one iteration behind for the finish role), so the shared
 // `more` flag -- an LDS read on every role's path out of the barrier -- is
-// consulted only from iteration K on (MGN_TRIO_MORESKIP; rollbacks and refill
-// ticks raise it)
-#ifndef MGN_TRIO_MORESKIP
-#define MGN_TRIO_MORESKIP 1
-#endif
+// consulted only from iteration K on (rollbacks and refill ticks raise it)
 __device__ __forceinline__ bool trio_exit(int j, int K, const int32_t& more) {
-  if (MGN_TRIO_MORESKIP && j < K) return false;
+  if (j < K) return false;
   return !__builtin_amdgcn_readfirstlane(more);
 }
 
@@ -184,14 +121,9 @@ struct TrioShared {
   int64_t row[2][EPB];
   uint32_t dend[2][EPB];
   double feat[2][NSL];
-  // WIN with a log window (MGN_TRIO_GLOG): the tick's log-normalised prices,
-  // formed by the generator role for the finish role's window rows
+  // WIN with a log window: the tick's log-normalised prices, formed by the
+  // generator role for the finish role's window rows
   double lprice[2][NSL];
-  // NST with the generator's prefix (MGN_NST_GPFX): the finish role's buffer
-  // state after its pops (F -> G, next iteration), the prefix sum (G -> F,
-  // same iteration) and the iteration that published it
-  double nA[2][EPB], nB[2][EPB], pfx[2][EPB];
-  int32_t nhd[2][EPB], nln[2][EPB], pfx_it[EPB];
 };
 
 // LDS of k_step_trio<S, ..., TW, NST, ..., M>: its static arrays (an upper
@@ -253,10 +185,9 @@ __device__ __forceinline__ void trio_replay_tick(Lane<M>& s, const KParams& p, u
   nx.dend = p.rp_end[s.rcur];
   s.pf_ok = true;
 }
-// per env: the ring, the finish role's pop summands and (gpfx, MGN_NST_GPFX)
-// the generator's prefix summands
-inline size_t trio_nst_dyn_lds(int S, int TW, int nstep, bool gpfx = MGN_NST_GPFX != 0) {
-  return (size_t)(TW / S) * (gpfx ? 3 : 2) * nst_pad(nstep, S) * sizeof(double);
+// per env: the ring and the finish role's pop summands
+inline size_t trio_nst_dyn_lds(int S, int TW, int nstep) {
+  return (size_t)(TW / S) * 2 * nst_pad(nstep, S) * sizeof(double);
 }
 
 // OMC: the output set when known at compile time (O_ALL, O_STD), else 0.
@@ -317,19 +248,17 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
                                                           const double* __restrict__ units_in,
                                                           const int32_t* __restrict__ aidx_in, int K) {
   MGN_IT(0, 0);
-  warm_kernargs<(int)(sizeof(KParams) + sizeof(mgn_traj) + 48)>();
+  // the argument segment: 6 leading pointers, KParams, mgn_traj, in_kind_rt
+  // (padded to 8), units_in, aidx_in, K
+  warm_kernargs<(int)(48 + sizeof(KParams) + sizeof(mgn_traj) + 8 + 16 + 4)>();
   MGN_IT(47, 0);
   const int in_kind = DISC ? IN_DISCRETE : in_kind_rt;
   constexpr int M = MM;
-  // (not at two slots per lane with a mixed-kind generator, nor beside the
-  // generator's n-step prefix: the candidate's copy of the generator state
-  // spilled at the 168-register budget)
-  constexpr bool TAIL = MGN_TRIO_TAILRST && !RP && !WIN && (MM == 1 || GK >= 0) && !(NST && MGN_NST_GPFX);
-  constexpr bool GLOG = MGN_TRIO_GLOG && WIN && !RP;
-  // NST: the generator role forms the first pop's prefix (env-major
-  // generator lanes: one source kind)
-  constexpr bool GPFX = MGN_NST_GPFX && NST && GK >= 0 && M == 1;
-  constexpr int NPADS = GPFX ? 3 : 2;
+  // (not at two slots per lane with a mixed-kind generator: the candidate's
+  // copy of the generator state spilled at the 168-register budget)
+  constexpr bool TAIL = !RP && !WIN && (MM == 1 || GK >= 0);
+  constexpr bool GLOG = WIN && !RP;
+  constexpr int NPADS = 2;  // NST: ring, pop summands
   static_assert(M == 1 || (M == 2 && !NST), "two slots per lane: one-step rewards");
   constexpr int APAD = S * M;
   constexpr int TRIO_W = TW;
@@ -350,7 +279,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   // few envs, each kind's branch executed by the waves that hold it (the
   // Composite's Sine, OU and TrendOU branches no longer run in every
   // generator wave).  Records stay env-major: the lane publishes at el S + ls.
-  constexpr bool GSLOT = MGN_TRIO_GSLOT && GK < 0 && !RP && TW / S > 1 && M == 1;
+  constexpr bool GSLOT = GK < 0 && !RP && TW / S > 1 && M == 1;
   const int el = (GSLOT && role == 0) ? l % EPB : l / S;
   const int ls = (GSLOT && role == 0) ? l / EPB : l % S;
   const int lx = (el * S + ls) * M;  // the lane's first (env, asset) slot record index
@@ -491,25 +420,23 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     sh.more[1] = 0;
     sh.more[2] = 0;
   }
-  if (GPFX && threadIdx.x < EPB) sh.pfx_it[threadIdx.x] = -1;  // (read from iteration 1 on)
 #ifdef MGN_STAMPS
   if (threadIdx.x < 8) s_duo_sub[threadIdx.x] = 0;
 #endif
-  if (!QREG || K == 0 || !MGN_TRIO_MORESKIP) __syncthreads();
+  if (!QREG || K == 0) __syncthreads();
   MGN_IT(1, 0);
 #pragma unroll
   for (int m = 0; m < M; ++m) s.kind[m] = s.valid[m] ? (QREG ? GK : s_src[s.asset[m]].kind) : -1;
 
   // NST: a pop's summands (nstep_column's operands: summand kk of the entries
-  // [head, head + len) on lane kk mod S, MGN_NST_U rounds evaluated together
+  // [head, head + len) on lane kk mod S, kNstU rounds evaluated together
   // on clamped operands so their chains interleave, slots [len, R S) +0.0)
   // into scr, and their ordered sum in kk order (S per chunk, the next
   // chunk's reads issued before this chunk's adds; +0.0 slots leave it
   // unchanged: acc starts at +0.0 and is never -0.0)
-  // (U: rounds per pass, a std::integral_constant)
-  const auto nst_summands = [&](auto Uc, const double* ring, double* scr, int head, int len, double A, double B,
+  const auto nst_summands = [&](const double* ring, double* scr, int head, int len, double A, double B,
                                 const PopPre& c) {
-    constexpr int U = decltype(Uc)::value;
+    constexpr int U = kNstU;
     const int n = p.nstep;
     const int R = (len + S - 1) / S;
     for (int j = 0; j < R; j += U) {
@@ -564,8 +491,6 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 
   if (role == 0) {
     // ---------------- generator waves: tick of step j, State.price / timestamp
-    const uint32_t om = OMC ? OMC : traj_mask(out);
-    const GTraj ov = traj_vgpr<MGN_TRIO_GST ? OMC : O_REW>(out);
     p.seed = in_vgpr(p.seed);
     p.env_offset = in_vgpr(p.env_offset);
     drain_vmem();
@@ -592,7 +517,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     uint64_t ts2 = 0;
     bool shadow = false;
     int jlast = 0;
-    __builtin_amdgcn_s_setprio(MGN_TRIO_PG);
+    __builtin_amdgcn_s_setprio(kPrioG);
 #ifdef MGN_STAMPS
     unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0;
     int jn = 0;
@@ -654,31 +579,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         }
         const bool rst = j > 0 && sh.reset[prv][el] != 0;
         const bool prev_step = j > 0 && (sh.rFlags[prv][el] & TR_STEP) != 0;
-        if constexpr (GPFX) {
-          // the finish role evaluates the env's step of the last iteration in
-          // this one (the same test as its own): the first pop's summands
-          // over the entries already in its ring and their ordered sum, with
-          // the shaper state after its last pops (MGN_NST_GPFX)
-          if (prev_step && !rst) {
-            const int pad = nst_pad(p.nstep, S);
-            const double* ring = s_nst + (size_t)el * NPADS * pad;
-            double* gscr = s_nst + (size_t)el * NPADS * pad + 2 * pad;
-            const double A = sh.nA[prv][el], B = sh.nB[prv][el];
-            const int len0 = sh.nln[prv][el];
-            nst_summands(std::integral_constant<int, MGN_NST_U>{}, ring, gscr, sh.nhd[prv][el], len0, A, B,
-                         pop_pre(p.shaper, A, B));
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (ls == 0) {
-              sh.pfx[cur][el] = nst_sum(gscr, len0);
-              __hip_atomic_store(&sh.pfx_it[el], j, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-          }
-        }
         // every branch's tick is the one call below (one copy of the
         // generator's code: the kind dispatch of every slot, inlined once)
-        bool tk = false, stepk = false;
+        bool tk = false;
         if (WIN && !rst && gpend > 0) {
           // a refill tick (not speculative: the reset is confirmed)
           tk = true;
@@ -727,7 +630,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #else
           ts = ts + 1;
 #endif
-          stepk = true;
+          k += 1;
         } else if (TAIL && K == 1) {
           // idle (the launch's ticks done, no reset pending): the candidate of
           // a reset the finish role may find in this iteration -- Env::reset's
@@ -739,17 +642,6 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           tk = true;
         }
         if (tk) tick();
-        if (stepk) {
-          // State.price and timestamp of step k (overwritten if rolled back)
-          if (MGN_TRIO_GST) {
-            const size_t oN = (size_t)k * p.N;
-#pragma unroll
-            for (int m = 0; m < M; ++m)
-              if (s.valid[m] && (om & O_OPR)) ost(ov.obs_price + ((oN + env) * (size_t)p.F + s.asset[m]), s.P[m]);
-            if (ls == 0 && (om & O_TS)) ost(ov.timestamp + (oN + env), (uint64_t)ts);
-          }
-          k += 1;
-        }
       }
 #pragma unroll
       for (int m = 0; m < M; ++m) sh.price[cur][lx + m] = s.P[m];
@@ -761,7 +653,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           for (int m = 0; m < M; ++m) sh.lprice[cur][lx + m] = log_norm(s.P[m]);
         }
       }
-      if (!MGN_TRIO_GST && ls == 0) sh.ts[cur][el] = ts;
+      if (ls == 0) sh.ts[cur][el] = ts;
       if constexpr (RP) {
         if (ls == 0) {
           sh.row[cur][el] = rp.row;
@@ -814,7 +706,6 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   if (role == 1) {
     // ---------------- ledger waves: Broker orders of step j
     const uint32_t om = OMC ? OMC : traj_mask(out);
-    const GTraj ov = traj_vgpr<MGN_TRIO_LST ? OMC : O_REW>(out);
     const MGN_G double* gunits = vptr(units_in);
     const MGN_G int32_t* gaidx = vptr(aidx_in);
     p.init_cash = in_vgpr(p.init_cash);
@@ -843,7 +734,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       }
       if (ls == 0) p.cash[env] = cash;
     };
-    __builtin_amdgcn_s_setprio(MGN_TRIO_PL);  // the orders are the critical path
+    __builtin_amdgcn_s_setprio(kPrioL);  // the orders are the critical path
 #ifdef MGN_STAMPS
     unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0;
 #endif
@@ -952,7 +843,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #endif
           if (j == 0) MGN_IT(52, TRIO_W);
           if constexpr (M == 1)
-            broker_spec<S, RQ1, true>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, after, any_mc);
+            broker_spec<S, RQ1>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, after, any_mc);
           else
             broker_spec_m2<S, RQ1>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, after, any_mc);
           if (j == 0) MGN_IT(53, TRIO_W);
@@ -960,14 +851,6 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         sa = after;
 #pragma unroll
         for (int m = 0; m < M; ++m) {
-          // BrokerResponse of step k (overwritten if rolled back)
-          if (MGN_TRIO_LST && s.valid[m]) {
-            const size_t i = oNA + (size_t)env * A + s.asset[m];
-            if (om & O_TP) ost(ov.tprice + i, tp[m]);
-            if (om & O_TU) ost(ov.tunits + i, tu[m]);
-            if (om & O_TC) ost(ov.tcost + i, tc[m]);
-            if (om & O_RISK) ost(ov.risk + i, (uint8_t)rk[m]);
-          }
           sh.rL[cur][lx + m] = s.L[m];
           sh.rTp[cur][lx + m] = tp[m];
           sh.rTu[cur][lx + m] = tu[m];
@@ -1166,7 +1049,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     }
   };
   drain_vmem();
-  __builtin_amdgcn_s_setprio(MGN_TRIO_PF);
+  __builtin_amdgcn_s_setprio(kPrioF);
 #ifdef MGN_STAMPS
   unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0;
 #endif
@@ -1269,24 +1152,13 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           const PopPre c = pop_pre(p.shaper, g.shA, g.shB);
           double acc = 0.0;
-          if (GPFX && pj == 0) {
-            // the generator role's ordered sum of the summands of the
-            // entries before this step's (published in this iteration), plus
-            // this step's: the same additions in the same order
-            if (!MGN_NST_SUM1 || ls == 0) {
-              while (__hip_atomic_load(&sh.pfx_it[el], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != j)
-                __builtin_amdgcn_s_sleep(1);
-              acc = sh.pfx[cur][el] + pop_term(p.shaper, v, g.shA, g.shB, c, s_disc[len - 1]);
-            }
-          } else {
-            nst_summands(std::integral_constant<int, MGN_NST_U>{}, ring, scr, head, len, g.shA, g.shB, c);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // the ordered sum only feeds the popped value the env's first lane
-            // stores: only that lane reads the summands back (MGN_NST_SUM1)
-            if (!MGN_NST_SUM1 || ls == 0) acc = nst_sum(scr, len);
-          }
+          nst_summands(ring, scr, head, len, g.shA, g.shB, c);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          // the ordered sum only feeds the popped value the env's first lane
+          // stores: only that lane reads the summands back
+          if (ls == 0) acc = nst_sum(scr, len);
           double res = acc;
           if (p.shaper == MGN_SHAPER_DSR || p.shaper == MGN_SHAPER_DDR) {
             res = clip1(acc / len);
@@ -1333,13 +1205,11 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         if (f.valid[m]) {
           const size_t i = kidx(k, sNA, bA) + m;
           const int x = lx + m;
-          if (!MGN_TRIO_LST) {
-            if (om & O_TP) ost(ov.tprice + i, sh.rTp[prv][x]);
-            if (om & O_TU) ost(ov.tunits + i, sh.rTu[prv][x]);
-            if (om & O_TC) ost(ov.tcost + i, sh.rTc[prv][x]);
-            if (om & O_RISK) ost(ov.risk + i, (uint8_t)sh.rRk[prv][x]);
-          }
-          if (!RP && !MGN_TRIO_GST && (om & O_OPR)) ost(ov.obs_price + (kidx(k, sNF, bP) + m), f.P[m]);
+          if (om & O_TP) ost(ov.tprice + i, sh.rTp[prv][x]);
+          if (om & O_TU) ost(ov.tunits + i, sh.rTu[prv][x]);
+          if (om & O_TC) ost(ov.tcost + i, sh.rTc[prv][x]);
+          if (om & O_RISK) ost(ov.risk + i, (uint8_t)sh.rRk[prv][x]);
+          if (!RP && (om & O_OPR)) ost(ov.obs_price + (kidx(k, sNF, bP) + m), f.P[m]);
           if (om & O_OPT) ost(ov.obs_port + (kidx(k, sNA1, bO) + 1 + f.asset[m]), portA[m]);
           if (D != 1) {
             if (om & O_AREW) ost(ov.agent_reward + i, ar[m]);
@@ -1363,7 +1233,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         if (om & O_DEND) ost(ov.data_end + ie, (uint8_t)(RP ? sh.dend[prv][el] : 0u));
         if (om & O_REW) ost(ov.reward + ie, reward);
         if (om & O_NSH) ost(ov.n_shaped + ie, (uint8_t)pops);
-        if (!MGN_TRIO_GST && (om & O_TS)) ost(ov.timestamp + ie, (uint64_t)sh.ts[prv][el]);
+        if (om & O_TS) ost(ov.timestamp + ie, (uint64_t)sh.ts[prv][el]);
         if (D == 1) {
           if (om & O_AREW) ost(ov.agent_reward + ie, rin_s);
           if (!NST && (om & O_SHP)) ost(ov.shaped + ie, shaped_s);
@@ -1412,16 +1282,6 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #pragma unroll
       for (int m = 0; m < M; ++m) pa[m] = (Lf[m] * Pf[m]) / eq;
       push_row(Pf, pa, (cashf - bf) / eq, (uint64_t)sh.ts[prv][el], klast, prv);
-    }
-    if constexpr (GPFX) {
-      // the n-step buffer after this iteration's pops, for the generator's
-      // prefix of the next iteration's first pop
-      if (ls == 0) {
-        sh.nA[cur][el] = g.shA;
-        sh.nB[cur][el] = g.shB;
-        sh.nhd[cur][el] = nhead;
-        sh.nln[cur][el] = nlen;
-      }
     }
     if (ls == 0) sh.reset[cur][el] = rst_out;
     // the reset tick runs next iteration -- a tail reset's in this one, by the

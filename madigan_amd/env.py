@@ -500,27 +500,61 @@ class BatchedEnv:
         L.check(self.lib.mgn_rollout(self.h, C.c_void_p(actions.data_ptr()), K, C.byref(t)), self.h)
         return out
 
-    def rollout_launcher(self, out: dict, k_steps: int):
-        """A launcher for repeated K-step rollouts into the same output buffers:
-        ``launch(actions_ptr)`` runs mgn_rollout on (K,N,A) int8 device actions
-        at that address, with the mgn_traj validated once here (the per-launch
-        host work is the ctypes call).  The caller keeps ``out`` alive."""
+    def rollout_launcher(self, out: dict, k_steps: int, actions=None):
+        """A launcher for repeated K-step rollouts into the same output buffers,
+        with the mgn_traj validated once here (the per-launch host work is the
+        call itself).  The caller keeps ``out`` (and ``actions``) alive.
+
+        With ``actions`` -- a (T, N, A) int8 device tensor, T >= K -- the
+        launcher is ``launch(t)``: K steps from rows [t, t + K) of it, t checked
+        against T - K on every call.  Without it, ``launch(actions_ptr)`` reads
+        (K, N, A) int8 at a raw device address the caller vouches for (an
+        address whose buffer holds fewer than K steps is read past its end:
+        round 4's bench fault)."""
+        torch = _torch()
         K = int(k_steps)
         t = self._traj_for(out, K)
         pc = L.pycall()
         if pc is not None:  # the CPython binding: no ctypes conversion per call
             f, hv, tv = pc.rollout, self.h.value, C.addressof(t)
 
-            def launch(actions_ptr: int) -> int:
+            def raw(actions_ptr: int) -> int:
                 return f(hv, actions_ptr, K, tv)
-            launch._keep = t  # the mgn_traj the address points at
-            return launch
-        ref = C.byref(t)
-        fn, h = self.lib.mgn_rollout, self.h
+        else:
+            ref = C.byref(t)
+            fn, h = self.lib.mgn_rollout, self.h
 
-        def launch(actions_ptr: int) -> int:
-            return fn(h, actions_ptr, K, ref)
+            def raw(actions_ptr: int) -> int:
+                return fn(h, actions_ptr, K, ref)
+        if actions is None:
+            raw._keep = t  # the mgn_traj the address points at
+            return raw
+        if not (isinstance(actions, torch.Tensor) and actions.device == self.device
+                and actions.dtype == torch.int8 and actions.is_contiguous() and actions.dim() == 3
+                and actions.shape[1] == self.N and actions.shape[2] == self.A):
+            raise ValueError(f"actions must be a contiguous (T, {self.N}, {self.A}) int8 tensor on {self.device}")
+        T = int(actions.shape[0])
+        if T < K:
+            raise ValueError(f"actions hold {T} steps, a launch reads {K}")
+        base, row, tmax = actions.data_ptr(), self.N * self.A, T - K
+
+        def launch(t0: int) -> int:
+            if not 0 <= t0 <= tmax:
+                raise IndexError(f"launch at step {t0}: rows [{t0}, {t0 + K}) outside the {T} action steps")
+            return raw(base + t0 * row)
+        launch._keep = (t, actions)
         return launch
+
+    def stream_synchronizer(self):
+        """A zero-argument callable that waits for the handle's stream
+        (mgn_synchronize) -- every launch of the handle is on it -- rather than
+        the whole device (torch.cuda.synchronize); returns the status code."""
+        pc = L.pycall()
+        if pc is not None and hasattr(pc, "synchronize"):
+            f, hv = pc.synchronize, self.h.value
+            return lambda: f(hv)
+        fn, h = self.lib.mgn_synchronize, self.h
+        return lambda: fn(h)
 
     # ---- Env::setDataSource / checkpoint --------------------------------------------
     def set_sources(self, spec: SourceSpec, prices=None):

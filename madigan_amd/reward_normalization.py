@@ -300,14 +300,33 @@ class SharpeEWMA(RewardShaper):
         if r.shape != (self.N,):
             raise ValueError(f"reward must be ({self.N},), got {r.shape}")
         self._update(r)
-        # the .pyx divides by sqrt(ewssq) with Cython's checked division: a
-        # zero variance (a constant reward stream) raises ZeroDivisionError
-        # there, never a nan / inf into the caller's data
-        if np.any((self.count > 1) & (self.ewssq == 0.)):
-            raise ZeroDivisionError("float division by zero (SharpeEWMA: zero reward variance)")
         with np.errstate(divide="ignore", invalid="ignore"):
             out = np.where(self.count <= 1, 0., r / np.sqrt(self.ewssq))
+        # the .pyx divides by sqrt(ewssq) with Cython's checked division: a
+        # zero variance (a constant reward stream) raises ZeroDivisionError
+        # there, after _update advanced the statistics, never a nan / inf into
+        # the caller's data.  Batched, each env behaves as its own shaper: every
+        # env's statistics advance, and the error names the envs whose call
+        # would have raised, carrying the other envs' values (nan at the named
+        # ones) -- a caller that catches it has the batch's step, not a retry
+        bad = (self.count > 1) & (self.ewssq == 0.)
+        if np.any(bad):
+            err = ZeroVarianceError("float division by zero (SharpeEWMA: zero reward variance"
+                                    + ("" if self.scalar else f" in envs {np.flatnonzero(bad).tolist()[:8]}") + ")")
+            err.envs = np.flatnonzero(bad)
+            err.out = np.where(bad, np.nan, out)
+            raise err
         return float(out[0]) if self.scalar else out
+
+
+class ZeroVarianceError(ZeroDivisionError):
+    """SharpeEWMA.stream on a zero-variance reward stream (the reference's
+    ZeroDivisionError).  ``envs``: the envs whose shaper raised (batched mode;
+    [0] in scalar mode); ``out``: the batch's values, nan at those envs.  Every
+    env's statistics have advanced, as the reference's _update runs before its
+    division."""
+    envs: np.ndarray
+    out: np.ndarray
 
 
 _CLASSES = {c.__name__: c for c in (SharpeFixedWindow, SortinoFixedWindowA, SortinoFixedWindowB,

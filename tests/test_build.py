@@ -1,0 +1,80 @@
+"""CPU checks of the product build (madigan_amd/build.py): the library is
+rebuilt when only its flags change, and the step kernels the automatic
+schedule runs at the benchmarked shapes keep their registers -- no spill to
+scratch -- as the compiler reports them (-Rpass-analysis=kernel-resource-usage,
+recorded by every build in madigan_amd/_obj/resource_usage.json).  Two units
+are built without machine LICM (build.UNIT_FLAGS), which kept their math
+constants from being hoisted out of the step loop and spilled; a compiler
+update that re-spills them fails here rather than only measuring slower."""
+import json
+import os
+import re
+
+import pytest
+
+from madigan_amd import build as B
+
+
+@pytest.fixture(scope="module")
+def usage():
+    if not os.path.exists(B.RESOURCE_USAGE):
+        pytest.fail(f"{B.RESOURCE_USAGE} missing: build the library (python -m madigan_amd.build)")
+    with open(B.RESOURCE_USAGE) as f:
+        return json.load(f)
+
+
+def _kernels(usage, unit, pattern):
+    rx = re.compile(pattern)
+    return {k: v for k, v in usage[unit].items() if rx.search(k)}
+
+
+# (unit, mangled-name pattern, the most VGPRs the kernels may spill, why)
+CASES = [
+    # k_step_trio<S, RQ1, DISC=true, OMC in {O_STD = 4093, O_ALL = 16383}, ...>: the
+    # agent loop's instantiations, the C3 headline among them (S = 8, GK = TrendOU)
+    ("mgn_launch_a8.hip", r"k_step_trioILi8ELb[01]ELb1ELj(4093|16383)E", 0, "C3 headline"),
+    ("mgn_launch_a4.hip", r"k_step_trioILi4ELb[01]ELb1ELj(4093|16383)E", 0, "4-asset agent loop"),
+    ("mgn_launch_a2.hip", r"k_step_trioILi2ELb[01]ELb1ELj(4093|16383)E", 0, "2-asset agent loop"),
+    # the windowed one-wave-per-role instantiations (C2's OU windows)
+    ("mgn_launch_a4.hip", r"k_step_trioILi4ELb[01]ELb1ELj0ELb1ELi64E", 0, "C2"),
+    # n-step at APAD 8, built without machine LICM (n = 20 DDR)
+    ("mgn_launch_a8nst.hip", r"k_step_trio", 0, "n-step, -disable-machine-licm"),
+    # two slots per lane (C5, 16 assets), built without machine LICM: 48 -> 4
+    # spilled VGPRs in round 4; more is a regression
+    ("mgn_launch_a16m2.hip", r"k_step_trio", 4, "two slots per lane, -disable-machine-licm"),
+]
+
+
+@pytest.mark.parametrize("unit,pattern,max_spill,what", CASES)
+def test_step_kernels_do_not_spill(usage, unit, pattern, max_spill, what):
+    ks = _kernels(usage, unit, pattern)
+    assert ks, f"{what}: no kernel matching {pattern} in {unit}"
+    for name, v in ks.items():
+        assert v["VGPRs Spill"] <= max_spill, f"{what}: {name} spills {v['VGPRs Spill']} VGPRs"
+        # three waves per SIMD: the three-role kernel's 768-thread workgroup
+        if "Li256E" in name:
+            assert v["Occupancy"] >= 3, f"{what}: {name} occupancy {v['Occupancy']}"
+
+
+def test_flag_change_rebuilds(monkeypatch):
+    assert os.path.exists(B.FLAGS_STAMP)
+    if B.needs_build():
+        pytest.skip("the library is out of date (sources newer than the build)")
+    monkeypatch.setattr(B, "FLAGS", B.FLAGS + ["-DMGN_UNUSED_FLAG"])
+    assert B.needs_build(), "a flag change alone must rebuild"
+    monkeypatch.setattr(B, "UNIT_FLAGS", {})
+    monkeypatch.setattr(B, "FLAGS", [f for f in B.FLAGS if f != "-DMGN_UNUSED_FLAG"])
+    assert B.needs_build(), "a unit-flag change alone must rebuild"
+
+
+def test_diag_switches_refused_without_diag(tmp_path):
+    """Stamp / ablation switches compile only in diagnostic builds (mgn_diag.h)."""
+    import subprocess
+    src = tmp_path / "t.hip"
+    src.write_text('#include "mgn_diag.h"\n')
+    r = subprocess.run([B.hipcc(), "--offload-arch=gfx950", "-fsyntax-only", "-DMGN_TRIO_ABL_G",
+                        f"-I{B.CSRC}", str(src)], capture_output=True, text=True)
+    assert r.returncode != 0 and "diagnostic builds" in r.stderr
+    r = subprocess.run([B.hipcc(), "--offload-arch=gfx950", "-fsyntax-only", "-DMGN_TRIO_ABL_G", "-DMGN_DIAG",
+                        f"-I{B.CSRC}", str(src)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

@@ -21,7 +21,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
-from tests.configs import trendou_sources
+from tests.configs import ou_sources, trendou_sources
 from tests.test_gpu_parity import assert_bits, close, gen_state_check, make_pair, out_check, state_check
 
 pytestmark = pytest.mark.gpu
@@ -71,9 +71,92 @@ def test_c3_full_grid_forced_resets(gpu):
         k0 += K
         state_check(g, orc, f"after K={K}")
     gen_state_check(g, orc, "C3 forced")
+    # one-step launches (the agent loop's K = 1) on the same grid: an episode
+    # that ends at a launch's only step is a tail reset -- the generator's
+    # candidate reset tick and the fresh Broker adopted after the loop
+    # (mgn_trio.h TAIL) -- checked against the oracle after every launch
+    n1 = 24
+    acts1 = g.generate_actions(n1, seed=0x6D6164 + 11)
+    a1 = acts1.cpu().numpy()
+    out1 = g.alloc_traj(1, fields=STD_FIELDS)
+    launch = g.rollout_launcher(out1, 1, acts1)
+    tail_launches = 0
+    for i in range(n1):
+        assert launch(i) == 0
+        o = _host(out1)
+        ref = orc.rollout(a1[i:i + 1], threads=THREADS)
+        for k in ("obs_price", "obs_port", "tprice", "tunits", "tcost"):
+            assert_bits(o[k], ref[k], f"K=1 launch {i} {k}")
+        for k in ("risk", "done", "margin_call"):
+            assert np.array_equal(o[k], ref[k]), f"K=1 launch {i} {k}"
+        assert np.array_equal(o["timestamp"].astype(np.uint64), ref["timestamp"]), f"K=1 launch {i} ts"
+        close(o["reward"], ref["reward"], f"K=1 launch {i} reward")
+        close(o["shaped"], ref["shaped"], f"K=1 launch {i} shaped", rtol=1e-10)
+        state_check(g, orc, f"after K=1 launch {i}")
+        gen_state_check(g, orc, f"after K=1 launch {i}")
+        tail_launches += int(o["done"].any())
+    assert tail_launches >= n1 - 2, f"only {tail_launches} of {n1} one-step launches ended an episode"
     st = g.episode_stats.cpu().numpy()
     for j, name in enumerate(("last_ret", "last_len", "last_equity", "n_done")):
         close(st[:, j], orc.scalar(name), name)
+
+
+def test_c3_sliced_launcher_sequence_vs_oracle(gpu):
+    """The bench's launch-length sweep on one handle at C3's shape: one-step
+    launches through a launcher on [:1] views of a 256-step trajectory, then
+    16- and 256-step launches on views of the same trajectory, each on fresh
+    rows of one bound action tensor -- every output and the state against the
+    oracle.  The launcher refuses action rows outside its tensor (round 4's
+    bench fault: a K = 256 launch given a 25-step action buffer read past it)."""
+    N, A = 8192, 8
+    g, orc = make_pair(trendou_sources(A, [0.001, 100, 500, 0.001, 0.005, 5.0, 0.15, 0.04, 0.001, 0.99]), N,
+                       seed=0x6D6164 + 3, required_margin=1.0, maintenance_margin=0.25, slippage_rel=1e-4,
+                       transaction_cost_rel=0.02, reward_shaper="DDR", adaptation_rate=0.001,
+                       unit_size=0.05, auto_reset=1, init_cash=1_000_000.0)
+    T = 512
+    acts = g.generate_actions(T, seed=0x6D6165)
+    a = acts.cpu().numpy()
+    big = g.alloc_traj(256, fields=STD_FIELDS)
+    row = 0
+    for K, n in ((1, 6), (16, 2), (256, 1)):
+        view = {k: v[:K] for k, v in big.items()}
+        launch = g.rollout_launcher(view, K, acts)
+        with pytest.raises(IndexError):
+            launch(T - K + 1)
+        with pytest.raises(IndexError):
+            launch(-1)
+        for i in range(n):
+            assert launch(row) == 0
+            o = _host(view)
+            ref = orc.rollout(a[row:row + K], threads=THREADS)
+            out_check({**o, "agent_reward": ref["agent_reward"]}, ref, f"K={K} launch {i}")
+            state_check(g, orc, f"K={K} launch {i}")
+            row += K
+    gen_state_check(g, orc, "sliced launcher")
+    with pytest.raises(ValueError):
+        g.rollout_launcher({k: v[:256] for k, v in big.items()}, 256, acts[:25])
+
+
+def test_sixteen_assets_ou_window64_two_slots_vs_oracle(gpu):
+    """16 OU assets with a W = 64 window at 4096 envs: the three-role kernel's
+    two-slots-per-lane layout (trio_m2_ok: 4096 x 16 lanes) -- the automatic
+    schedule since round 4 -- against the oracle: every output and every
+    step's window over two 32-step launches, with a leveraged broker ending
+    episodes inside them (the refill rows after each auto-reset)."""
+    from madigan_amd import _lib as L
+    from tests.test_gpu_configs import _check_windows
+    N, A, W, K = 4096, 16, 64, 32
+    g, orc = make_pair(ou_sources(A), N, seed=0x6D6164 + 12, required_margin=0.02, maintenance_margin=0.25,
+                       slippage_rel=1e-4, transaction_cost_rel=0.02, unit_size=0.9, auto_reset=1,
+                       init_cash=1e5, window=W, adaptation_rate=0.001, reward_shaper="DDR")
+    assert g.lib.mgn_get_schedule(g.h) == L.SCHED_TRIO
+    acts = g.generate_actions(2 * K, seed=0x6D6164 + 13)
+    _check_windows(g, orc, acts[:K], K, None, "A16 W64 launch 0")
+    _check_windows(g, orc, acts[K:], K, None, "A16 W64 launch 1")
+    state_check(g, orc, "A16 W64")
+    st = g.episode_stats.cpu().numpy()
+    assert st[:, 3].sum() > N // 10, "too few episode ends"
+    close(st[:, 3], orc.scalar("n_done"), "n_done")
 
 
 @pytest.mark.parametrize("sched", ["auto", "duo"])

@@ -296,10 +296,11 @@ def test_nstep_rollout(gpu, shaper, mode, n):
 @pytest.mark.parametrize("A,N,n,shaper", [(8, 8192, 20, "DDR"), (16, 4096, 5, "DSR"), (4, 16384, 3, "DDR")])
 def test_nstep_generator_prefix_vs_oracle(gpu, A, N, n, shaper):
     """n-step aggregation on the 256-lane three-role kernel with one source
-    kind (the n = 20 DDR bench shape's instantiation): the generator role forms
-    each step's first-pop prefix (MGN_NST_GPFX) and the finish role adds the
-    new entry's summand -- against the oracle over two launches (the buffer
-    carries across them), auto-resets flushing buffers inside the launches."""
+    kind (the n = 20 DDR bench shape's instantiation): the finish role's ring
+    and pops (every lane of the env evaluates part of a pop's summands, the
+    env's first lane sums them in order) against the oracle over two launches
+    (the buffer carries across them), auto-resets flushing buffers inside the
+    launches."""
     from madigan_amd import _lib as L
     K = 24
     kw = dict(required_margin=0.02, maintenance_margin=0.25, transaction_cost_rel=0.02,

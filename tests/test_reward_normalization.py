@@ -61,3 +61,39 @@ def test_make_reward_normalizer_dispatch():
     with pytest.raises(NotImplementedError):
         RN.make_reward_normalizer({"reward_shaper_config": {"reward_shaper": "Nope"}})
     assert RN.NullShaper().stream(0.25) == 0.25
+
+
+def test_sharpe_ewma_zero_variance_per_env():
+    """A constant reward stream (an agent holding cash) has zero variance:
+    the reference's checked division raises ZeroDivisionError for that env's
+    shaper.  Batched, only that env's value is void: the error names it and
+    carries the other envs' values, which equal independent scalar shapers'
+    -- and every env's statistics have advanced, as the scalar shapers' have."""
+    rng = np.random.default_rng(3)
+    T, N = 6, 4
+    r = rng.normal(0, 0.01, (T, N))
+    r[:, 2] = 0.25  # env 2: constant
+    batched = RN.SharpeEWMA(5, n_envs=N)
+    scal = [RN.SharpeEWMA(5) for _ in range(N)]
+    for t in range(T):
+        want, raised = np.empty(N), []
+        for e in range(N):
+            try:
+                want[e] = scal[e].stream(float(r[t, e]))
+            except ZeroDivisionError:
+                want[e] = np.nan
+                raised.append(e)
+        if raised:
+            with pytest.raises(RN.ZeroVarianceError) as ei:
+                batched.stream(r[t])
+            assert isinstance(ei.value, ZeroDivisionError)
+            assert ei.value.envs.tolist() == raised == [2]
+            got = ei.value.out
+        else:
+            got = batched.stream(r[t])
+        np.testing.assert_array_equal(np.isnan(got), np.isnan(want))
+        ok = ~np.isnan(want)
+        np.testing.assert_array_equal(got[ok].view(np.int64), want[ok].view(np.int64))
+    for e in range(N):
+        assert batched.count[e] == scal[e].count[0] == T
+        assert batched.ewssq[e] == scal[e].ewssq[0]

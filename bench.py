@@ -30,6 +30,10 @@ mgn_window_hist):
   C5  8192 envs/GPU x 16 HDF replay (synthetic OU paths written to an HDF5
       file in the HDFSourceSingle layout generalised to (T, 16), staged to HBM
       once, per-env start stride), 2% cost, DDR, norm none
+  R1  the reference's own experiment shape (scripts/ou_ddr_.001_nstep20.yaml):
+      --n-envs envs x 1 OU (mu 10, theta .08, phi .04), W = 64 (norm false:
+      raw prices), n = 20 step returns (discount .99) of the summed agent
+      reward, DDR eta .001 (--shaper sortino_shaperB: sortino_exp 1.1), 2% cost
 """
 from __future__ import annotations
 
@@ -269,6 +273,15 @@ def workload_env(name, N, A, rank, dev, **extra):
                            norm_type="log", **base),
                 "C4: Composite Synth(2)+OU(3)+TrendOU(3), 2% cost, PPC alpha=.01 target [1,0..0] "
                 "over the env log reward, W=64 window (norm log) gathered every step, auto-reset", 64)
+    if name == "R1":
+        shaper = extra.pop("shaper", "DDR")
+        sx = {"sortino_exp": 1.1} if shaper.startswith("sortino") else {}
+        spec = ou_spec([10.0], [0.08], [0.04])
+        return (BatchedEnv(spec, N, device=dev, seed=seed, env_offset=off, reward_shaper=shaper,
+                           nstep_return=20, discount=0.99, reward_mode="agent_sum", **sx, **base),
+                f"R1: OU x1 (mu 10, theta .08, phi .04), W=64 window (norm none), n=20 returns "
+                f"(discount .99) of the summed agent reward, {shaper} eta=.001{' exp 1.1' if sx else ''}, "
+                "2% cost, unit .05 avM, auto-reset (scripts/ou_ddr_.001_nstep20.yaml)", 64)
     if name == "C5":
         import tempfile
         T = 200_000
@@ -347,7 +360,8 @@ def main():
                     help="also time 1/16/64/256 steps per launch (separate launches; keep it off "
                          "when profiling, so the kernel's rocprof average is the headline's)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--workload", default="C3", choices=["C1", "C2", "C3", "C4", "C5"])
+    ap.add_argument("--workload", default="C3", choices=["C1", "C2", "C3", "C4", "C5", "R1"])
+    ap.add_argument("--shaper", default="DDR", help="R1: DDR or sortino_shaperB")
     ap.add_argument("--dump-stats", default=None,
                     help="rank 0 saves the gathered (n_total, 4) episode statistics (.npy)")
     ap.add_argument("--no-probe", dest="probe", action="store_false",
@@ -721,11 +735,11 @@ def windowed(args, world, rank, dev):
     import torch.distributed as dist
     wl = args.workload
     N = {"C2": 4096}.get(wl, args.n_envs)
-    A = {"C2": 4, "C4": 8, "C5": 16}[wl]
+    A = {"C2": 4, "C4": 8, "C5": 16, "R1": 1}[wl]
     if wl == "C2" and args.win_assets:
         # diagnostic: OU windows at another asset count, at --n-envs envs
         N, A = args.n_envs, args.win_assets
-    env, desc, W = workload_env(wl, N, A, rank, dev)
+    env, desc, W = workload_env(wl, N, A, rank, dev, **({"shaper": args.shaper} if wl == "R1" else {}))
     Kf = max(1, min(args.fuse, args.win_fuse))
     n_warm = max(1, -(-args.warmup // Kf))
     n_time = max(1, -(-args.steps // Kf))
@@ -734,7 +748,7 @@ def windowed(args, world, rank, dev):
     actions = env.generate_actions(total, seed=0x6D6164)
     traj = env.alloc_traj(Kf, fields=["reward", "shaped", "done", "obs_price", "obs_port",
                                       "timestamp", "tprice", "tunits", "tcost", "risk",
-                                      "margin_call", "data_end"])
+                                      "margin_call", "data_end"] + (["n_shaped"] if env.nstep > 1 else []))
     wp = torch.empty((Kf, N, W, env.F), dtype=torch.float64, device=dev)
     wo = torch.empty((Kf, N, W, A + 1), dtype=torch.float64, device=dev)
     wt = torch.empty((Kf, N, W), dtype=torch.int64, device=dev)
@@ -830,7 +844,7 @@ def windowed(args, world, rank, dev):
             "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": desc, "n_envs_per_gpu": N, "n_assets": A, "n_feats": env.F,
-                       "window": W, "steps_per_launch": Kf,
+                       "window": W, "steps_per_launch": Kf, "nstep": env.nstep,
                        "schedule": SCHED_NAMES[int(lib.mgn_get_schedule(h))],
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,

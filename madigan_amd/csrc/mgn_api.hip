@@ -333,30 +333,40 @@ bool duo_eligible(const mgn_env* e) {
   }
   return true;
 }
-// the three-role kernel: 2..16 assets, generator sources (replay tapes at 16
-// assets on the 256-lane layout); one-step rewards
-// (windows included: the confirmed steps' rows are pushed by its finish role)
-// or n-step aggregation of a scalar reward without a window (the finish
-// role's rings in dynamic LDS)
+// the three-role kernel: 1..16 assets (one asset on two lanes per role, the
+// second a pad), generator sources (replay tapes at 16 assets on the 256-lane
+// layout); one-step rewards or n-step aggregation of a scalar reward (the
+// finish role's rings in dynamic LDS), with or without a window (the
+// confirmed steps' rows are pushed by its finish role).  Some launches of an
+// eligible handle have no instantiation (trio_launchable) and run another
+// kernel -- every kernel reads and writes the same state, bit-identically
 bool trio_eligible(const mgn_env* e) {
   // (its output indices are k x a 32-bit stride: N (A + 1), N F and N n fit 32 bits)
   const uint64_t row = (uint64_t)(e->A + 1 > e->F ? e->A + 1 : e->F);
-  const bool nst_ok = e->cfg.nstep == 1 || (e->D == 1 && e->W == 0 && e->cfg.shaper < MGN_SHAPER_SHARPE);
+  const bool nst_ok = e->cfg.nstep == 1 || e->D == 1;
   // replay tapes: 16 assets at the 256-lane layout (N * 16 >= 256 * 256), n = 1
   const bool rp_ok = !e->replay || (e->apad == 16 && e->cfg.nstep == 1 && (uint64_t)e->N * 16 >= 65536);
-  if (!(e->apad >= 2 && e->apad <= 16 && !e->cfg.aux && rp_ok && nst_ok &&
+  if (!(e->apad >= 1 && e->apad <= 16 && !e->cfg.aux && rp_ok && nst_ok &&
         (uint64_t)e->N * row < (1ull << 32) && (uint64_t)e->N * (uint64_t)e->cfg.nstep < (1ull << 32)))
     return false;
   // n-step: the static arrays plus the envs' rings in dynamic LDS within a
   // workgroup's 160 KiB (2 assets at n = 64 would need more: the two-role /
   // single-role kernels run those)
   if (e->cfg.nstep > 1) {
-    static size_t (*const lds_of[5])(long long, int) = {nullptr, mgn::trio_nst_lds_a2, mgn::trio_nst_lds_a4,
-                                                        mgn::trio_nst_lds_a8, mgn::trio_nst_lds_a16};
+    // (one asset: the two-lane layout's, APAD 2)
+    static size_t (*const lds_of[5])(long long, int, bool) = {nullptr, mgn::trio_nst_lds_a2, mgn::trio_nst_lds_a4,
+                                                              mgn::trio_nst_lds_a8, mgn::trio_nst_lds_a16};
     const int idx = e->apad <= 2 ? 1 : e->apad <= 4 ? 2 : e->apad <= 8 ? 3 : 4;
-    if (lds_of[idx](e->N, e->cfg.nstep) > mgn::kTrioLdsMax) return false;
+    if (lds_of[idx](e->N, e->cfg.nstep, e->W > 0) > mgn::kTrioLdsMax) return false;
   }
   return true;
+}
+// the launches of a three-role handle with an instantiation: discrete steps
+// (the agent loop) always; units / single orders unless the env has one asset
+// or keeps a window with n-step rings
+bool trio_launchable(const mgn_env* e, int in_kind) {
+  if (in_kind == mgn::IN_DISCRETE) return true;
+  return e->apad > 1 && !(e->W > 0 && e->cfg.nstep > 1);
 }
 // automatic: where the single-role kernel would run one lane per asset (small
 // batches: one wave per SIMD), give every asset a second (and a third) lane
@@ -420,6 +430,16 @@ void launch_step(const mgn_env* e, const mgn_traj& out, int in_kind, const doubl
   if (trio && e->sched == MGN_SCHED_AUTO && e->apad > 8 && e->W > 0 && !e->replay &&
       !mgn::trio_m2_ok(e->N, e->A, e->cfg.nstep, e->D, in_kind) && duo_eligible(e)) {
     kDuo[4](a);
+    return;
+  }
+  if (trio && !trio_launchable(e, in_kind)) {
+    // no three-role instantiation for this launch: the two-role kernel where
+    // eligible, else the single-role one (same state, same bits)
+    if (duo_eligible(e)) {
+      kDuo[e->apad <= 2 ? 1 : e->apad <= 4 ? 2 : e->apad <= 8 ? 3 : 4](a);
+      return;
+    }
+    launch(kStep, e->apad, e->m, a);
     return;
   }
   if (trio) {

@@ -461,7 +461,10 @@ __device__ __forceinline__ double chain_step(double c, double X1, double y, doub
 // node is the sum of the same two children as the heap tree's (IEEE addition
 // commutes), so the sums are bit-identical to the LDS form; the root of P is
 // the sums after every executed order.
-template <int S>
+// ONE (a one-asset env on S = 2 lanes): the tree is lane 0's one leaf; every
+// lane of the segment takes lane 0's root (its path is only read by lane 0,
+// whose order is the only one)
+template <int S, bool ONE = false>
 __device__ __forceinline__ void dpp_tree4(const double (&pre)[4], const double (&post)[4], bool go_own, int ls,
                                           double (&path)[4], double (&rootP)[4]) {
   double nP[4], nQ[4];
@@ -470,6 +473,11 @@ __device__ __forceinline__ void dpp_tree4(const double (&pre)[4], const double (
     path[q] = pre[q];
     nQ[q] = pre[q];
     nP[q] = go_own ? post[q] : pre[q];
+  }
+  if constexpr (ONE) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rootP[q] = seg_bcast<S, 0>(nP[q]);
+    return;
   }
   auto level = [&](auto sibP, auto sibQ, bool right) {
 #pragma unroll
@@ -507,7 +515,7 @@ __device__ __forceinline__ void dpp_tree4(const double (&pre)[4], const double (
 // uses, so the ledger, responses and sums are bit-identical to XRounds; an
 // unrefused batch (the common case) costs one pass instead of S dependent
 // rounds.
-template <int S, bool RQ1>
+template <int S, bool RQ1, bool ONE>
 __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRecs<S>& er,
                                             double& cash, const double (&uc)[1], double (&tp)[1],
                                             double (&tu)[1], double (&tc)[1], int (&rk)[1], int ls,
@@ -534,7 +542,7 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
     // canonical sums before this lane's order: leaves of executed earlier
     // orders after the order, the others before
     double r[4];
-    dpp_tree4<S>(lf_pre, lf_post, ((go_bits >> ls) & 1) != 0, ls, r, rootP);
+    dpp_tree4<S, ONE>(lf_pre, lf_post, ((go_bits >> ls) & 1) != 0, ls, r, rootP);
     // cash before this lane's order, and after the last order, under the
     // guess: the chain is the env's, not the lane's, so its first lane walks
     // it (one lane of the env reads the records' cash terms) and publishes

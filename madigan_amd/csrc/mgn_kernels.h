@@ -160,8 +160,12 @@ __device__ __forceinline__ double seg_bcast(double v) {
   }
 }
 
-template <int M, int S>
+// ONE: a one-asset env on an S = 2 lane segment (the pipelined kernels'
+// narrowest layout): its canonical sum is the one leaf itself -- lane 0's --
+// not leaf + (+0.0), which differs from it in the sign of a -0.0 leaf
+template <int M, int S, bool ONE = false>
 __device__ __forceinline__ double canon(const double (&v)[M]) {
+  if constexpr (ONE) return seg_bcast<S, 0>(tree<M>(v));
   return seg_sum<S>(tree<M>(v));
 }
 
@@ -170,7 +174,7 @@ struct Sums {
 };
 
 // Portfolio.cpp:180-209 -- the four sums every valuation is built from
-template <int M, int S>
+template <int M, int S, bool ONE = false>
 __device__ __forceinline__ Sums port_sums(const double (&L)[M], const double (&mep)[M],
                                           const double (&Bm)[M], const double (&P)[M]) {
   double tlp[M], tml[M], tsh[M], tb[M];
@@ -183,10 +187,10 @@ __device__ __forceinline__ Sums port_sums(const double (&L)[M], const double (&m
     tb[m] = Bm[m];
   }
   Sums s;
-  s.lp = canon<M, S>(tlp);
-  s.ml = canon<M, S>(tml);
-  s.sh = canon<M, S>(tsh);
-  s.b = canon<M, S>(tb);
+  s.lp = canon<M, S, ONE>(tlp);
+  s.ml = canon<M, S, ONE>(tml);
+  s.sh = canon<M, S, ONE>(tsh);
+  s.b = canon<M, S, ONE>(tb);
   return s;
 }
 
@@ -1311,7 +1315,7 @@ __device__ __forceinline__ void nstep_column(const KParams& p, RingP ring, OutP 
 // RQ1: required_margin == 1.0, where x / required_margin == x exactly and the
 // divisions are skipped.  NST: n-step aggregation (nstep > 1) compiled in.
 // speculative Broker resolution for one asset per lane (defined in mgn_duo.h)
-template <int S, bool RQ1>
+template <int S, bool RQ1, bool ONE = false>
 __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRecs<S>& er,
                                             double& cash, const double (&uc)[1], double (&tp)[1],
                                             double (&tu)[1], double (&tc)[1], int (&rk)[1], int ls,

@@ -60,6 +60,9 @@ inline bool trio_m2_ok(long long n_envs, int A, int nstep, int D, int in_kind) {
 void launch_trio_m2_a16(const StepArgs& a);
 // the n-step three-role launches at APAD = 8, in their own unit (mgn_launch_a8nst.hip)
 void launch_trio_nst_a8(const StepArgs& a);
+// the three-role kernel for one-asset envs (ONE: S = 2 lanes, the second a
+// pad), in its own unit (mgn_launch_a1t.hip): discrete steps (the agent loop)
+void launch_trio_one(const StepArgs& a);
 
 // smallest assets-per-lane with at most 16 lanes per env (DPP-only reductions)
 constexpr int min_m(int apad) { return apad > 16 ? apad / 16 : 1; }
@@ -67,7 +70,7 @@ constexpr int min_m(int apad) { return apad > 16 ? apad / 16 : 1; }
 #define MGN_DECLARE_APAD(A)                          \
   void launch_duo_a##A(const StepArgs& a);           \
   void launch_trio_a##A(const StepArgs& a);          \
-  size_t trio_nst_lds_a##A(long long n_envs, int nstep); \
+  size_t trio_nst_lds_a##A(long long n_envs, int nstep, bool win); \
   void launch_step_a##A(int m, const StepArgs& a);   \
   void launch_init_a##A(int m, const InitArgs& a);   \
   void launch_val_a##A(int m, const ValArgs& a);

@@ -2,6 +2,8 @@
 // mgn_launch_a<APAD>.hip).
 #pragma once
 
+#include <type_traits>
+
 #include "mgn_launch.h"
 #include "mgn_trio.h"
 
@@ -114,25 +116,46 @@ void launch_trio_m2(const StepArgs& a) {
   }
 }
 
-// three-role pipelined step kernel (mgn_trio.h): S = APAD lanes per env per role
-// NST: the finish role's NStepBuffer rings in dynamic LDS (no window, D = 1).
-// APAD 8 instantiates it in its own unit (mgn_launch_a8nst.hip, UNIT_FLAGS)
+// the launch of a three-role instantiation: grid over the envs, the n-step
+// rings (NST) in dynamic LDS
 template <int S>
-void launch_trio_nst(const StepArgs& a) {
-  const bool small = (long long)a.p.N * S < 256LL * TRIO_W;
-  const int epb = (small ? 64 : TRIO_W) / S;
-  const int grid = (a.p.N + epb - 1) / epb;
-  const bool disc = a.in_kind == IN_DISCRETE;
-  const size_t lds = trio_nst_dyn_lds(S, small ? 64 : TRIO_W, a.p.nstep);
-  auto goN = [&](auto kern) {
+struct TrioGo {
+  const StepArgs& a;
+  bool small;
+  template <typename Kern>
+  void operator()(Kern kern, bool nst) const {
+    const int epb = (small ? 64 : TRIO_W) / S;
+    const int grid = (a.p.N + epb - 1) / epb;
+    const size_t lds = nst ? trio_nst_dyn_lds(S, small ? 64 : TRIO_W, a.p.nstep) : 0;
     // a refused size is the caller's hipGetLastError (HIP records every
     // call's status); trio_eligible keeps static + dynamic LDS within 160 KiB
-    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-        hipSuccess)
+    if (lds && hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+                   hipSuccess)
       return;
     launch_timed(a.ev0, a.ev1, kern, dim3(grid), dim3(small ? 192 : TRIO_BLOCK), (uint32_t)lds, a.stream,
                  a.p.L, a.p.mep, a.p.Bm, a.p.P, a.p.cash, a.act, a.p, a.out, a.in_kind, a.units, a.aidx, a.K);
-  };
+  }
+};
+
+// three-role pipelined step kernel (mgn_trio.h): S = APAD lanes per env per role
+// NST: the finish role's NStepBuffer rings in dynamic LDS (D = 1), with a
+// window for discrete steps (trio_launchable).  APAD 8 instantiates it in its
+// own unit (mgn_launch_a8nst.hip, UNIT_FLAGS)
+template <int S>
+void launch_trio_nst(const StepArgs& a) {
+  const bool small = (long long)a.p.N * S < 256LL * TRIO_W;
+  const bool disc = a.in_kind == IN_DISCRETE;
+  const TrioGo<S> go{a, small};
+  auto goN = [&](auto kern) { go(kern, true); };
+  if (a.p.W > 0) {
+    // windows: discrete steps only (trio_launchable), one wave per role at
+    // every batch -- the finish role's window rows and n-step pops need more
+    // than the 256-lane layout's 168 registers (it spilled 8)
+    const TrioGo<S> go64{a, true};
+    if (a.p.reqm_one) go64(k_step_trio<S, true, true, 0, true, 64, true>, true);
+    else go64(k_step_trio<S, false, true, 0, true, 64, true>, true);
+    return;
+  }
   if (small) {
     if (disc) {
       if (a.p.reqm_one) goN(k_step_trio<S, true, true, 0, false, 64, true>);
@@ -153,8 +176,45 @@ void launch_trio_nst(const StepArgs& a) {
   }
 }
 
+// the one-asset envs (ONE, S = 2: the second lane of every env a pad; its
+// sums are lane 0's one leaf), discrete steps (trio_launchable): window or
+// not, n = 1 or n-step (generator sources, any source kind); window handles
+// at one wave per role (the finish role's rows and pops need > 168 registers)
+// (a template: instantiated only by mgn_launch_a1t.hip)
+template <int S = 2>
+void launch_trio_one_impl(const StepArgs& a) {
+  static_assert(S == 2, "one asset on two lanes per role");
+  const bool win = a.p.W > 0, nst = a.p.nstep > 1;
+  const bool small = win || (long long)a.p.N * S < 256LL * TRIO_W;
+  const TrioGo<S> go{a, small};
+  auto pick = [&](auto rq1, auto winc, auto nstc) {
+    constexpr bool R = decltype(rq1)::value, W = decltype(winc)::value, NS = decltype(nstc)::value;
+    if constexpr (W) {
+      go(k_step_trio<S, R, true, 0, W, 64, NS, -1, false, 1, true>, NS);
+    } else {
+      if (small) go(k_step_trio<S, R, true, 0, W, 64, NS, -1, false, 1, true>, NS);
+      else go(k_step_trio<S, R, true, 0, W, TRIO_W, NS, -1, false, 1, true>, NS);
+    }
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  if (a.p.reqm_one) {
+    if (win) nst ? pick(T{}, T{}, T{}) : pick(T{}, T{}, F{});
+    else nst ? pick(T{}, F{}, T{}) : pick(T{}, F{}, F{});
+  } else {
+    if (win) nst ? pick(F{}, T{}, T{}) : pick(F{}, T{}, F{});
+    else nst ? pick(F{}, F{}, T{}) : pick(F{}, F{}, F{});
+  }
+}
+
 template <int S>
 void launch_trio(const StepArgs& a) {
+  if constexpr (S == 2) {
+    if (a.p.A == 1) {
+      launch_trio_one(a);  // mgn_launch_a1t.hip
+      return;
+    }
+  }
   if constexpr (S == 16) {
     if (trio_m2_ok(a.p.N, a.p.A, a.p.nstep, a.p.D, a.in_kind)) {
       launch_trio_m2_a16(a);  // mgn_launch_a16m2.hip
@@ -293,9 +353,9 @@ void dispatch_m(int m, const Arg& a) {
   void launch_trio_a##A(const StepArgs& a) {                                                 \
     if constexpr (A >= 2 && A <= 16) launch_trio<A>(a);                                       \
   }                                                                                          \
-  size_t trio_nst_lds_a##A(long long n_envs, int nstep) {                                    \
+  size_t trio_nst_lds_a##A(long long n_envs, int nstep, bool win) {                          \
     if constexpr (A >= 2 && A <= 16) {                                                       \
-      const bool small = n_envs * A < 256LL * TRIO_W;                                        \
+      const bool small = win || n_envs * A < 256LL * TRIO_W;                                 \
       return (small ? trio_static_lds<A, 64, true>() : trio_static_lds<A, TRIO_W, true>()) +   \
              trio_nst_dyn_lds(A, small ? 64 : TRIO_W, nstep);                                \
     }                                                                                        \

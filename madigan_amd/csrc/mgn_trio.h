@@ -32,10 +32,12 @@
 // arrays stored by L, or State.price and the timestamp by G, measured
 // slower, round 2); G and L write their state back at exit.
 // Scope: one asset slot per lane at APAD = S in {2, 4, 8, 16}, or two (MM = 2)
-// at S = 8 for 9..16 assets; generator sources or (16 assets) a replay tape;
-// n = 1 with or without a window (WIN: the finish role pushes the ring /
-// launch-history row of every step it confirms, and the refill rows after an
-// auto-reset), or n-step (NST, no window); k_step_duo / k_step run the rest.
+// at S = 8 for 9..16 assets, or a one-asset env on S = 2 lanes (ONE: its sums
+// are lane 0's one leaf); generator sources or (16 assets) a replay tape;
+// n = 1 or n-step of a scalar reward (NST: DSR / DDR / PPC / none, and the
+// naive shapers), with or without a window (WIN: the finish role pushes the
+// ring / launch-history row of every step it confirms, and the refill rows
+// after an auto-reset); k_step_duo / k_step run the rest.
 #pragma once
 
 #include "mgn_duo.h"
@@ -233,7 +235,7 @@ __device__ __forceinline__ void gen_state_copy(Lane<M>& d, const Lane<M>& s) {
 // envs fit one workgroup per CU; slots ls MM + m in the canonical order, the
 // ledger's broker_spec_m2; one-step rewards with a scalar shaper, D = 1)
 template <int S, bool RQ1, bool DISC, uint32_t OMC = 0, bool WIN = false, int TW = TRIO_W, bool NST = false,
-          int GK = -1, bool RP = false, int MM = 1>
+          int GK = -1, bool RP = false, int MM = 1, bool ONE = false>
 // The leading pointer arguments are the ledger role's state and actions:
 // built with -amdgpu-kernarg-preload-count (madigan_amd/build.py) they arrive
 // in SGPRs with the wave, so the orders' loads issue without waiting for the
@@ -260,6 +262,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   constexpr bool GLOG = WIN && !RP;
   constexpr int NPADS = 2;  // NST: ring, pop summands
   static_assert(M == 1 || (M == 2 && !NST), "two slots per lane: one-step rewards");
+  static_assert(!ONE || (S == 2 && M == 1), "a one-asset env on two lanes per role");
   constexpr int APAD = S * M;
   constexpr int TRIO_W = TW;
   constexpr int TRIO_BLOCK = 3 * TW;
@@ -715,7 +718,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     const bool need_ar = (p.reward_mode != MGN_REWARD_ENV_LOG) || (om & O_AREW);  // as the finish role's
     // sums of the ledger (canonical trees): ml, sh, b change only with the
     // orders, lp with the prices; `fresh` = recompute all four (start, reset)
-    Sums sa = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
+    Sums sa = port_sums<M, S, ONE>(s.L, s.mep, s.Bm, s.P);
     drain_vmem();
     MGN_IT(51, TRIO_W);
     int k = 0;
@@ -783,14 +786,14 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         const bool after_reset = prev_step ? false : true;
         Sums s0;
         if (after_reset && j > 0) {
-          s0 = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);  // after a reset tick
+          s0 = port_sums<M, S, ONE>(s.L, s.mep, s.Bm, s.P);  // after a reset tick
         } else {
           double tlp[M];
 #pragma unroll
           for (int m = 0; m < M; ++m) tlp[m] = s.L[m] * s.P[m];
           s0 = sa;
-          s0.lp = canon<M, S>(tlp);
-          if (j == 0) s0 = port_sums<M, S>(s.L, s.mep, s.Bm, s.P);
+          s0.lp = canon<M, S, ONE>(tlp);
+          if (j == 0) s0 = port_sums<M, S, ONE>(s.L, s.mep, s.Bm, s.P);
         }
         const double prevEq = (cash + s0.lp) - s0.b;  // Env.h:208
         double uc[M], tp[M], tu[M], tc[M], prevVal[M];
@@ -843,7 +846,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #endif
           if (j == 0) MGN_IT(52, TRIO_W);
           if constexpr (M == 1)
-            broker_spec<S, RQ1>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, after, any_mc);
+            broker_spec<S, RQ1, ONE>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, after, any_mc);
           else
             broker_spec_m2<S, RQ1>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, after, any_mc);
           if (j == 0) MGN_IT(53, TRIO_W);
@@ -962,7 +965,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       const double q = s.valid[m] ? tgt_g[1 + s.asset[m]] : 0.;
       qq[m] = q * q;
     }
-    g.cos_qn = sqrt(tgt_g[0] * tgt_g[0] + canon<M, S>(qq));
+    g.cos_qn = sqrt(tgt_g[0] * tgt_g[0] + canon<M, S, ONE>(qq));
   }
   const bool need_ar = (p.reward_mode != MGN_REWARD_ENV_LOG) || (om & O_AREW);
   // output element strides per step (32-bit: checked on the host) and the
@@ -1080,7 +1083,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         double tlp[M];
 #pragma unroll
         for (int m = 0; m < M; ++m) tlp[m] = f.L[m] * f.P[m];
-        q.lp = canon<M, S>(tlp);
+        q.lp = canon<M, S, ONE>(tlp);
       }
       q.ml = sh.rMl[prv][el];
       q.sh = sh.rSh[prv][el];
@@ -1116,8 +1119,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           pp[m] = pv * pv;
           pq[m] = pv * qv;
         }
-        const double np_ = sqrt(port0 * port0 + canon<M, S>(pp));
-        const double dot = port0 * s_tgt[0] + canon<M, S>(pq);
+        const double np_ = sqrt(port0 * port0 + canon<M, S, ONE>(pp));
+        const double dot = port0 * s_tgt[0] + canon<M, S, ONE>(pq);
         cos_term = p.cos_temp * (dot / (np_ * g.cos_qn));
       }
       double shaped_s = 0., rin_s = 0., shaped_v = 0.;
@@ -1127,7 +1130,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         // replay_buffer.py:68-80) for the env's scalar column: append, pop once
         // when full, every entry on done; the row of step k (n entries, zero
         // after the pops) is stored here
-        rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
+        rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S, ONE>(ar) : reward;
         const int n = p.nstep;
         double* ring = s_nst + (size_t)el * NPADS * nst_pad(n, S);  // ring, then the pop's summands
         double* scr = ring + nst_pad(n, S);
@@ -1150,6 +1153,20 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          if (p.shaper >= MGN_SHAPER_SHARPE) {
+            // the naive shapers (sharpe_shaper, sortino_shaperA / B,
+            // nstep_buffer.py:207-312) over the ring by the env's first lane,
+            // nstep_column's evaluation: the single-entry heuristic or the
+            // discounted sums in entry order
+            if (ls == 0) {
+              const double res = (len == 1) ? naive1(p.shaper, ring[head], p.sexp)
+                                            : naive_n(p.shaper, ring, n, 1, 0, head, len, s_disc, p.sexp);
+              if (row) ost(row + pj, res);
+            }
+            head = (head + 1 == n) ? 0 : head + 1;
+            len -= 1;
+            continue;
+          }
           const PopPre c = pop_pre(p.shaper, g.shA, g.shB);
           double acc = 0.0;
           nst_summands(ring, scr, head, len, g.shA, g.shB, c);
@@ -1184,7 +1201,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         while (nhead >= n) nhead -= n;
         nlen = L1 - pops;
       } else if (D == 1) {
-        rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S>(ar) : reward;
+        rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S, ONE>(ar) : reward;
         if (p.shaper == MGN_SHAPER_DDR) {  // shape() for DDR (nstep_buffer.py:128-162)
           const double r = rin_s;
           shaped_s = clip1((0.0 + 1.0 * ddr_one_pre(r, g.shA, g.shB, ddr_pre(g.shA, g.shB))) / 1);
@@ -1278,7 +1295,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         tlp[m] = Lf[m] * Pf[m];
       }
       const double cashf = sh.rCash[prv][el], bf = sh.rB[prv][el];
-      const double eq = (cashf + canon<M, S>(tlp)) - bf;
+      const double eq = (cashf + canon<M, S, ONE>(tlp)) - bf;
 #pragma unroll
       for (int m = 0; m < M; ++m) pa[m] = (Lf[m] * Pf[m]) / eq;
       push_row(Pf, pa, (cashf - bf) / eq, (uint64_t)sh.ts[prv][el], klast, prv);

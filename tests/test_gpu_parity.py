@@ -367,6 +367,18 @@ def test_nstep64_two_assets_auto_schedule(gpu):
     # rounds of 16 summands (nst_pad rounds n up to a multiple of 16)
     (16, dict(reward_shaper="DDR", nstep_return=3, discount=0.9)),
     (16, dict(reward_shaper="DSR", nstep_return=20, discount=0.99)),
+    # n-step rings beside a window, and the naive shapers, on the three-role
+    # kernel (round 5); one-asset envs on two lanes per role (ONE)
+    (4, dict(reward_shaper="DDR", nstep_return=6, discount=0.95, window=7)),
+    (2, dict(reward_shaper="sortino_shaperB", sortino_exp=1.1, nstep_return=5, reward_mode="agent_sum",
+             window=5)),
+    (8, dict(reward_shaper="sortino_shaperA", sortino_exp=2, nstep_return=4)),
+    (1, dict(reward_shaper="DDR")),
+    (1, dict(reward_shaper="DDR", nstep_return=20, discount=0.99, window=8, reward_mode="agent_sum")),
+    (1, dict(reward_shaper="sortino_shaperB", sortino_exp=1.1, nstep_return=5, window=6,
+             reward_mode="agent_sum")),
+    (1, dict(reward_shaper="PPC", cosine_temp=0.05, window=4, norm_type="log")),
+    (1, dict(reward_shaper="sharpe_shaper", nstep_return=3)),
 ])
 def test_schedules_bit_identical(gpu, A, kw):
     """The two-role kernel (k_step_duo: generator waves + ledger waves), the
@@ -382,12 +394,12 @@ def test_schedules_bit_identical(gpu, A, kw):
     rng = np.random.default_rng(A)
     units = rng.normal(0, 3e3, (N, A))
     res = []
-    # trio_eligible (mgn_api.hip): 2..16 assets; n-step only for a scalar reward
-    # without a window and a non-naive shaper (DSR / DDR / PPC / none)
+    # trio_eligible (mgn_api.hip): 1..16 assets; n-step for a scalar reward;
+    # the two-role kernel: 2..16 assets
     nst = kw.get("nstep_return", 1) > 1
-    trio_ok = 2 <= A <= 16 and (not nst or (kw.get("reward_mode") != "agent_per_asset" and not kw.get("window")
-                                          and kw.get("reward_shaper") in (None, "DSR", "DDR", "PPC")))
-    for sched in (L.SCHED_SINGLE, L.SCHED_DUO) + ((L.SCHED_TRIO,) if trio_ok else ()):
+    trio_ok = 1 <= A <= 16 and (not nst or kw.get("reward_mode") != "agent_per_asset")
+    duo_ok = A >= 2
+    for sched in (L.SCHED_SINGLE,) + ((L.SCHED_DUO,) if duo_ok else ()) + ((L.SCHED_TRIO,) if trio_ok else ()):
         g = BatchedEnv(spec, N, **base, **kw)
         L.check(g.lib.mgn_set_schedule(g.h, sched), g.h)
         assert g.lib.mgn_get_schedule(g.h) == sched
@@ -405,7 +417,7 @@ def test_schedules_bit_identical(gpu, A, kw):
             out.update({"w_" + str(i): t.cpu().numpy() for i, t in enumerate(g.window())})
         res.append(out)
     assert res[0]["done"].sum() > 0
-    for other, name in zip(res[1:], ("duo", "trio")):
+    for other, name in zip(res[1:], (("duo", "trio") if duo_ok else ("trio",))):
         for k, v in res[0].items():
             w = other[k]
             if np.asarray(v).dtype == np.float64:

@@ -538,11 +538,17 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
   int go = 0, mc = 0, insuff = 0;
   double cend = cash0;
   double rootP[4];  // the sums after the orders the pass took
+#ifdef MGN_STAMPS
+  unsigned long long t_tr = 0, t_ch = 0;
+#endif
   for (int it = 0; it <= S; ++it) {
     // canonical sums before this lane's order: leaves of executed earlier
     // orders after the order, the others before
     double r[4];
     dpp_tree4<S, ONE>(lf_pre, lf_post, ((go_bits >> ls) & 1) != 0, ls, r, rootP);
+#ifdef MGN_STAMPS
+    if (it == 0) t_tr = __builtin_amdgcn_s_memtime();
+#endif
     // cash before this lane's order, and after the last order, under the
     // guess: the chain is the env's, not the lane's, so its first lane walks
     // it (one lane of the env reads the records' cash terms) and publishes
@@ -563,6 +569,9 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const double c_own = er.cpre[ls];
     cend = er.cpre[S];
+#ifdef MGN_STAMPS
+    if (it == 0) t_ch = __builtin_amdgcn_s_memtime();
+#endif
     // Portfolio::checkRisk(i, u), Portfolio.cpp:254-279 (as XRounds)
     const double pnl = r[0] - r[1];
     const double balance = c_own + r[2];
@@ -605,6 +614,9 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
     s_duo_sub[0] += t_b - t_a;
     s_duo_sub[1] += t_c - t_b;
     s_duo_sub[2] += t_d - t_c;
+    s_duo_sub[3] += t_tr - t_b;   // first pass: the DPP trees
+    s_duo_sub[4] += t_ch - t_tr;  // first pass: the cash chain, published and read back
+    s_duo_sub[7] += t_c - t_ch;   // the checks and the remaining passes
     s_duo_sub[5] += 1;  // broker calls
   }
 #endif

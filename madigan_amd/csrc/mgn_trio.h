@@ -740,10 +740,15 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     __builtin_amdgcn_s_setprio(kPrioL);  // the orders are the critical path
 #ifdef MGN_STAMPS
     unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0;
+    // the ledger's phases: prices + pre-order sums, units, the Broker, the records
+    unsigned long long Lp1 = 0, Lp2 = 0, Lp3 = 0, lacc[4] = {0, 0, 0, 0};
 #endif
     for (int j = 0;; ++j) {
       const int cur = j & 1, prv = cur ^ 1;
       MGN_T(T0);
+#ifdef MGN_STAMPS
+      Lp1 = Lp2 = Lp3 = T0;
+#endif
       const bool rst = live && j > 0 && sh.reset[prv][el] != 0;
       const bool prev_step = j > 0 && (sh.rFlags[prv][el] & TR_STEP) != 0;
       // WIN: this iteration's tick refills the window (the reset tick or one
@@ -796,6 +801,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           if (j == 0) s0 = port_sums<M, S, ONE>(s.L, s.mep, s.Bm, s.P);
         }
         const double prevEq = (cash + s0.lp) - s0.b;  // Env.h:208
+#ifdef MGN_STAMPS
+        Lp1 = __builtin_amdgcn_s_memtime();
+#endif
         double uc[M], tp[M], tu[M], tc[M], prevVal[M];
         int rk[M];
         const size_t oN = (size_t)k * p.N, oNA = (size_t)k * p.N * A;
@@ -839,6 +847,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         }
         Sums after = s0;
         int any_mc = 0;
+#ifdef MGN_STAMPS
+        Lp2 = __builtin_amdgcn_s_memtime();
+#endif
 #ifdef MGN_TRIO_ABL_L  // diagnostic timing build: no Broker orders
         if (false) {
 #else
@@ -851,6 +862,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
             broker_spec_m2<S, RQ1>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, after, any_mc);
           if (j == 0) MGN_IT(53, TRIO_W);
         }
+#ifdef MGN_STAMPS
+        Lp3 = __builtin_amdgcn_s_memtime();
+#endif
         sa = after;
 #pragma unroll
         for (int m = 0; m < M; ++m) {
@@ -898,6 +912,12 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #ifdef MGN_STAMPS
       acc0 += T1 - T0;
       acc1 += T2 - T1;
+      if (Lp3 != T0) {  // an iteration that stepped
+        lacc[0] += Lp1 - T0;
+        lacc[1] += Lp2 - Lp1;
+        lacc[2] += Lp3 - Lp2;
+        lacc[3] += T1 - Lp3;
+      }
 #endif
       if (trio_exit(j, K, sh.more[j % 3])) break;
     }
@@ -908,6 +928,10 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       for (int i = 0; i < 3; ++i) atomicAdd(&g_duo_stamps[13 + i], s_duo_sub[i]);
       atomicAdd(&g_duo_stamps[18], s_duo_sub[5]);
       atomicAdd(&g_duo_stamps[19], s_duo_sub[6]);
+      atomicAdd(&g_duo_stamps[2], s_duo_sub[3]);
+      atomicAdd(&g_duo_stamps[3], s_duo_sub[4]);
+      atomicAdd(&g_duo_stamps[6], s_duo_sub[7]);
+      for (int i = 0; i < 4; ++i) atomicAdd(&g_duo_stamps[20 + i], lacc[i]);
     }
 #endif
 #ifdef MGN_TRIO_ABL_EPI  // diagnostic timing build: no state write-back

@@ -1,6 +1,6 @@
 #!/bin/bash
 # One evidence pass on the GPU box (TAG names the output directory):
-#   SUITE=1  the GPU test suite (-m gpu) and smoke()
+#   SUITE=1  the GPU test suite (-m gpu; PYK: a -k expression) and smoke()
 #   DRV=1    the driver's bench line (--steps 20 --warmup 5) and the same
 #            command under rocprofv3 --kernel-trace --stats
 #   EXTRA    further bench lines: "name|args;name|args" (each also traced when
@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 O=gpurun_out/${TAG:-pass}
 mkdir -p $O
 if [ -n "$SUITE" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYSEL} \
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYK:+-k "$PYK"} \
     > $O/pytest_gpu.txt 2>&1 || { echo "gpu suite failed"; grep -E "FAILED|Error|error" $O/pytest_gpu.txt | head -20; tail -30 $O/pytest_gpu.txt; exit 1; }
   tail -2 $O/pytest_gpu.txt
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.txt; exit 1; }

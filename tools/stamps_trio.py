@@ -57,6 +57,10 @@ def main():
            "ledger": {"work": round(v[4] / it, 1), "wait": round(v[5] / it, 1),
                       "broker_parts": {k: round(v[13 + i] / it, 1)
                                        for i, k in enumerate(("order_prep", "spec_loop", "post"))}},
+           "ledger_phases": {k: round(v[20 + i] / it, 1) for i, k in
+                             enumerate(("prices_and_pre_sums", "units", "broker", "records"))},
+           "broker_first_pass": {"trees": round(v[2] / it, 1), "cash_chain": round(v[3] / it, 1),
+                                 "checks_and_more_passes": round(v[6] / it, 1)},
            "finish": {"work": round(v[16] / it, 1), "wait": round(v[17] / it, 1)},
            "ledger_passes_per_broker_call": round(v[19] / max(v[18], 1), 3)}
     print(json.dumps(res))

@@ -123,10 +123,10 @@ struct TrioGo {
   const StepArgs& a;
   bool small;
   template <typename Kern>
-  void operator()(Kern kern, bool nst) const {
+  void operator()(Kern kern, bool nst, int npads = 2) const {
     const int epb = (small ? 64 : TRIO_W) / S;
     const int grid = (a.p.N + epb - 1) / epb;
-    const size_t lds = nst ? trio_nst_dyn_lds(S, small ? 64 : TRIO_W, a.p.nstep) : 0;
+    const size_t lds = nst ? trio_nst_dyn_lds(S, small ? 64 : TRIO_W, a.p.nstep, npads) : 0;
     // a refused size is the caller's hipGetLastError (HIP records every
     // call's status); trio_eligible keeps static + dynamic LDS within 160 KiB
     if (lds && hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
@@ -165,8 +165,10 @@ void launch_trio_nst(const StepArgs& a) {
       else goN(k_step_trio<S, false, false, 0, false, 64, true>);
     }
   } else if (disc && a.gkind == MGN_SRC_TRENDOU) {
-    if (a.p.reqm_one) goN(k_step_trio<S, true, true, 0, false, TRIO_W, true, MGN_SRC_TRENDOU>);
-    else goN(k_step_trio<S, false, true, 0, false, TRIO_W, true, MGN_SRC_TRENDOU>);
+    // (the generator role forms the next pop's prefix: a third pad per env)
+    static_assert(trio_npf(true, MGN_SRC_TRENDOU, 1), "");
+    if (a.p.reqm_one) go(k_step_trio<S, true, true, 0, false, TRIO_W, true, MGN_SRC_TRENDOU>, true, 3);
+    else go(k_step_trio<S, false, true, 0, false, TRIO_W, true, MGN_SRC_TRENDOU>, true, 3);
   } else if (disc) {
     if (a.p.reqm_one) goN(k_step_trio<S, true, true, 0, false, TRIO_W, true>);
     else goN(k_step_trio<S, false, true, 0, false, TRIO_W, true>);
@@ -283,24 +285,26 @@ void launch_trio(const StepArgs& a) {
       if (a.p.reqm_one) go(k_step_trio<S, true, false, 0, true>);
       else go(k_step_trio<S, false, false, 0, true>);
     }
-  } else if (disc && om == O_STD) {  // the agent loop's output set
-    if (a.gkind == MGN_SRC_TRENDOU) {
-      if (a.p.reqm_one) go(k_step_trio<S, true, true, O_STD, false, TRIO_W, false, MGN_SRC_TRENDOU>);
-      else go(k_step_trio<S, false, true, O_STD, false, TRIO_W, false, MGN_SRC_TRENDOU>);
-    } else if (a.p.reqm_one) {
-      go(k_step_trio<S, true, true, O_STD>);
-    } else {
-      go(k_step_trio<S, false, true, O_STD>);
-    }
-  } else if (disc && om == O_ALL) {
-    if (a.gkind == MGN_SRC_TRENDOU) {
-      if (a.p.reqm_one) go(k_step_trio<S, true, true, O_ALL, false, TRIO_W, false, MGN_SRC_TRENDOU>);
-      else go(k_step_trio<S, false, true, O_ALL, false, TRIO_W, false, MGN_SRC_TRENDOU>);
-    } else if (a.p.reqm_one) {
-      go(k_step_trio<S, true, true, O_ALL>);
-    } else {
-      go(k_step_trio<S, false, true, O_ALL>);
-    }
+  } else if (disc && (om == O_STD || om == O_ALL)) {  // the agent loop's output sets
+    // one-step launches (the agent loop's K = 1, APAD <= 8) have their own
+    // instantiations (K1: an episode that ends at the launch's step is reset
+    // inside the launch, mgn_trio.h TAIL)
+    auto pick = [&](auto omc, auto k1) {
+      constexpr uint32_t OM = decltype(omc)::value;
+      constexpr bool K1 = decltype(k1)::value && S <= 8;
+      if (a.gkind == MGN_SRC_TRENDOU) {
+        if (a.p.reqm_one) go(k_step_trio<S, true, true, OM, false, TRIO_W, false, MGN_SRC_TRENDOU, false, 1, false, K1>);
+        else go(k_step_trio<S, false, true, OM, false, TRIO_W, false, MGN_SRC_TRENDOU, false, 1, false, K1>);
+      } else if (a.p.reqm_one) {
+        go(k_step_trio<S, true, true, OM, false, TRIO_W, false, -1, false, 1, false, K1>);
+      } else {
+        go(k_step_trio<S, false, true, OM, false, TRIO_W, false, -1, false, 1, false, K1>);
+      }
+    };
+    using STD = std::integral_constant<uint32_t, O_STD>;
+    using ALL = std::integral_constant<uint32_t, O_ALL>;
+    if (a.K == 1) om == O_STD ? pick(STD{}, std::true_type{}) : pick(ALL{}, std::true_type{});
+    else om == O_STD ? pick(STD{}, std::false_type{}) : pick(ALL{}, std::false_type{});
   } else if (disc) {
     if (a.p.reqm_one) go(k_step_trio<S, true, true>);
     else go(k_step_trio<S, false, true>);
@@ -357,7 +361,7 @@ void dispatch_m(int m, const Arg& a) {
     if constexpr (A >= 2 && A <= 16) {                                                       \
       const bool small = win || n_envs * A < 256LL * TRIO_W;                                 \
       return (small ? trio_static_lds<A, 64, true>() : trio_static_lds<A, TRIO_W, true>()) +   \
-             trio_nst_dyn_lds(A, small ? 64 : TRIO_W, nstep);                                \
+             trio_nst_dyn_lds(A, small ? 64 : TRIO_W, nstep, small ? 2 : 3);                \
     }                                                                                        \
     return ~(size_t)0;                                                                       \
   }                                                                                          \

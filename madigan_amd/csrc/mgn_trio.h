@@ -69,11 +69,24 @@ constexpr int kPrioG = 0, kPrioL = 2, kPrioF = 1;
 // prices (the finish role reads them from LDS; GLOG below)
 //
 // NST: rounds of a pop's summands evaluated together (the terms' chains
-// interleave; rounds past the buffer's are computed and dropped).  (Tried and
-// not kept, round 4: the generator role forming the first pop's prefix over
-// the entries already in the ring -- bit-identical, neutral at n = 20 DDR,
-// profiles/r04_ab_nst_prefix.txt)
+// interleave; rounds past the buffer's are computed and dropped)
 constexpr int kNstU = 3;
+
+// NST, one iteration ahead (NPF): a pop sums gamma^k f(r_k; A, B) over the
+// ring's n entries with the shaper state (A, B) the previous pops left, and
+// that state moves only with the popped (oldest) entries -- so the state of
+// the next iteration's first pop, and that pop's summands over every entry
+// already in the ring then, are known an iteration early.  In iteration j the
+// generator role predicts the finish role's buffer after iteration j (it
+// evaluates a step iff the records say so, and pops once when that fills the
+// ring; a done flush is caught below), forms the next pop's summands over
+// the entries the ring holds now and their ordered sum, and publishes them
+// with the state it assumed.  In iteration j + 1 the finish role takes the
+// prefix where its own state matches the prediction bit for bit and adds the
+// remaining one or two entries' summands in entry order -- the same
+// operations in the same order as the full pop; otherwise it pops in full.
+// (Round 4 formed the prefix in the pop's own iteration: neutral,
+// profiles/r04_ab_nst_prefix.txt -- the finish role waited for it.)
 
 // the loop's exit test after iteration j's barrier: iterations 0..K always
 // run (the K steps, one iteration behind for the finish role), so the shared
@@ -82,6 +95,26 @@ constexpr int kNstU = 3;
 __device__ __forceinline__ bool trio_exit(int j, int K, const int32_t& more) {
   if (j < K) return false;
   return !__builtin_amdgcn_readfirstlane(more);
+}
+
+// The finish role's done test of the step L ran in the previous iteration
+// (Env.h:216-218), on the records it reads -- the ledger after the orders,
+// the tick's prices, cash, the price-independent sums and the refused-order
+// flag: the same operands and operations, so the same answer, wherever
+// another role needs it (one-step launches, TAIL_EXACT)
+template <int M, int S, bool ONE>
+__device__ __forceinline__ bool rec_done(const double (&Lr)[M], const double (&P)[M], double cashv, double ml,
+                                         double shv, double b, bool any_mc, const KParams& p) {
+  double tlp[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) tlp[m] = Lr[m] * P[m];
+  Sums q;
+  q.lp = canon<M, S, ONE>(tlp);
+  q.ml = ml;
+  q.sh = shv;
+  q.b = b;
+  const double curEq = (cashv + q.lp) - q.b;
+  return any_mc || margin_call(q, cashv, p.mainM) || (curEq < 0.1 * p.init_cash);
 }
 
 // TR_REFILL (WIN): the iteration's tick was an auto-reset refill tick
@@ -127,6 +160,17 @@ struct TrioShared {
   // generator role for the finish role's window rows
   double lprice[2][NSL];
 };
+// NPF: the finish role's buffer after its pops (F -> G, next iteration):
+// shaper state, oldest index, fill count; the generator's prefix of the next
+// pop (G -> F, next iteration): its sum over the first pcnt entries and the
+// buffer state it assumed (empty where NPF is off: no LDS)
+template <int EPB, bool ON>
+struct NpfShared {
+  double fA[2][EPB], fB[2][EPB], pfx[2][EPB], pA[2][EPB], pB[2][EPB];
+  int32_t fhd[2][EPB], fln[2][EPB], phd[2][EPB], pln[2][EPB], pcnt[2][EPB];
+};
+template <int EPB>
+struct NpfShared<EPB, false> {};
 
 // LDS of k_step_trio<S, ..., TW, NST, ..., M>: its static arrays (an upper
 // bound of the compiler's layout) plus, for NST, the rings in dynamic LDS; the
@@ -134,7 +178,7 @@ struct TrioShared {
 // (kTrioLdsMax, mgn_launch.h)
 template <int S, int TW, bool NST, int M = 1>
 constexpr size_t trio_static_lds() {
-  return sizeof(TrioShared<S, TW, M>) + (size_t)(TW / S) * sizeof(EnvRecs<S * M>) +
+  return sizeof(TrioShared<S, TW, M>) + sizeof(NpfShared<TW / S, NST>) + (size_t)(TW / S) * sizeof(EnvRecs<S * M>) +
          S * M * sizeof(mgn_asset_source) + (MGN_MAX_ASSETS + 1) * sizeof(double) +
          (NST ? MGN_MAX_NSTEP : 1) * sizeof(double) + 256;
 }
@@ -187,10 +231,13 @@ __device__ __forceinline__ void trio_replay_tick(Lane<M>& s, const KParams& p, u
   nx.dend = p.rp_end[s.rcur];
   s.pf_ok = true;
 }
-// per env: the ring and the finish role's pop summands
-inline size_t trio_nst_dyn_lds(int S, int TW, int nstep) {
-  return (size_t)(TW / S) * 2 * nst_pad(nstep, S) * sizeof(double);
+// per env: the ring, the finish role's pop summands and (npads 3, NPF) the
+// generator's prefix summands
+inline size_t trio_nst_dyn_lds(int S, int TW, int nstep, int npads = 2) {
+  return (size_t)(TW / S) * npads * nst_pad(nstep, S) * sizeof(double);
 }
+// NPF: n-step launches whose generator lanes are env-major (one source kind)
+__host__ __device__ constexpr bool trio_npf(bool nst, int gk, int mm) { return nst && gk >= 0 && mm == 1; }
 
 // OMC: the output set when known at compile time (O_ALL, O_STD), else 0.
 // WIN: the handle keeps a window (StackerDiscrete ring, and the launch
@@ -235,7 +282,7 @@ __device__ __forceinline__ void gen_state_copy(Lane<M>& d, const Lane<M>& s) {
 // envs fit one workgroup per CU; slots ls MM + m in the canonical order, the
 // ledger's broker_spec_m2; one-step rewards with a scalar shaper, D = 1)
 template <int S, bool RQ1, bool DISC, uint32_t OMC = 0, bool WIN = false, int TW = TRIO_W, bool NST = false,
-          int GK = -1, bool RP = false, int MM = 1, bool ONE = false>
+          int GK = -1, bool RP = false, int MM = 1, bool ONE = false, bool K1 = false>
 // The leading pointer arguments are the ledger role's state and actions:
 // built with -amdgpu-kernarg-preload-count (madigan_amd/build.py) they arrive
 // in SGPRs with the wave, so the orders' loads issue without waiting for the
@@ -256,11 +303,12 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   MGN_IT(47, 0);
   const int in_kind = DISC ? IN_DISCRETE : in_kind_rt;
   constexpr int M = MM;
-  // (not at two slots per lane with a mixed-kind generator: the candidate's
-  // copy of the generator state spilled at the 168-register budget)
-  constexpr bool TAIL = !RP && !WIN && (MM == 1 || GK >= 0);
+  // TAIL: one-step launches (K1, an instantiation of their own: the code
+  // would cost the longer launches registers), one slot per lane
+  constexpr bool TAIL = K1 && !RP && !WIN && MM == 1;
   constexpr bool GLOG = WIN && !RP;
-  constexpr int NPADS = 2;  // NST: ring, pop summands
+  constexpr bool NPF = trio_npf(NST, GK, MM);
+  constexpr int NPADS = NPF ? 3 : 2;  // NST: ring, pop summands (, NPF: the generator's prefix summands)
   static_assert(M == 1 || (M == 2 && !NST), "two slots per lane: one-step rewards");
   static_assert(!ONE || (S == 2 && M == 1), "a one-asset env on two lanes per role");
   constexpr int APAD = S * M;
@@ -268,6 +316,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   constexpr int TRIO_BLOCK = 3 * TW;
   constexpr int EPB = TRIO_W / S;
   __shared__ TrioShared<S, TW, M> sh;
+  __shared__ NpfShared<TW / S, NPF> npf;
   __shared__ EnvRecs<APAD> recs[EPB];
   __shared__ mgn_asset_source s_src[APAD];
   __shared__ double s_tgt[MGN_MAX_ASSETS + 1];
@@ -283,6 +332,12 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   // Composite's Sine, OU and TrendOU branches no longer run in every
   // generator wave).  Records stay env-major: the lane publishes at el S + ls.
   constexpr bool GSLOT = GK < 0 && !RP && TW / S > 1 && M == 1;
+  // TAIL_EXACT (one-step launches, env-major generator lanes): the generator
+  // and the ledger evaluate the finish role's done test themselves in the
+  // launch's last iteration (rec_done) -- the generator forms the reset tick
+  // only for the envs that end (not as a candidate for every env), and both
+  // write their final state back during that iteration instead of after it
+  constexpr bool TAIL_EXACT = TAIL && !GSLOT;
   const int el = (GSLOT && role == 0) ? l % EPB : l / S;
   const int ls = (GSLOT && role == 0) ? l / EPB : l % S;
   const int lx = (el * S + ls) * M;  // the lane's first (env, asset) slot record index
@@ -518,7 +573,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     Lane<M> s2;
     gen_state_copy<M>(s2, s);
     uint64_t ts2 = 0;
-    bool shadow = false;
+    bool shadow = false, tail_it = false, stored = false;
     int jlast = 0;
     __builtin_amdgcn_s_setprio(kPrioG);
 #ifdef MGN_STAMPS
@@ -635,16 +690,93 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #endif
           k += 1;
         } else if (TAIL && K == 1) {
-          // idle (the launch's ticks done, no reset pending): the candidate of
-          // a reset the finish role may find in this iteration -- Env::reset's
-          // source reset and getData on the final state, kept in s2
-          gen_state_copy<M>(s2, s);
-          ts2 = ts;
-          shadow = true;
-          src_reset<M, false, GK>(s, p, env, ts, QREG ? qr : nullptr);
-          tk = true;
+          // idle (the launch's ticks done, no reset pending): a reset the
+          // finish role finds in this iteration -- Env::reset's source reset
+          // and getData on the final state.  TAIL_EXACT: for the envs whose
+          // step ends (rec_done, the finish role's own test); else a
+          // candidate for every env, kept in s2 and adopted after the loop
+          bool cand = true;
+          if constexpr (TAIL_EXACT) {
+            const int fl = sh.rFlags[prv][el];
+            double Lr[M], Pr[M];
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+              Lr[m] = sh.rL[prv][lx + m];
+              Pr[m] = sh.price[prv][lx + m];
+            }
+            cand = p.auto_reset && (fl & TR_STEP) && !sh.reset[prv][el] &&
+                   rec_done<M, S, ONE>(Lr, Pr, sh.rCash[prv][el], sh.rMl[prv][el], sh.rSh[prv][el],
+                                       sh.rB[prv][el], (fl & TR_ANYMC) != 0, p);
+            tail_it = true;
+          }
+          if (cand) {
+            gen_state_copy<M>(s2, s);
+            ts2 = ts;
+            shadow = true;
+            src_reset<M, false, GK>(s, p, env, ts, QREG ? qr : nullptr);
+            tk = true;
+          }
         }
         if (tk) tick();
+        if constexpr (TAIL_EXACT) {
+          // the final state, written back while the finish role evaluates
+          if (tail_it) {
+            g_store();
+            stored = true;
+          }
+        }
+      }
+      if constexpr (NPF) {
+        // the finish role's next pop, one iteration ahead (NPF above): its
+        // buffer after this iteration -- it appends iff it evaluates a step
+        // here (its own test), and pops the oldest entry once if that fills
+        // the ring -- and, if its next evaluated step fills the ring, that
+        // pop's summands over the entries the ring holds now (the ring and
+        // the state are in LDS from iteration 1 on)
+        int pl = -1;
+        if (j > 0 && live && p.shaper < MGN_SHAPER_SHARPE) {
+          const int n = p.nstep;
+          const double* ring = s_nst + (size_t)el * NPADS * nst_pad(n, S);
+          double* gscr = s_nst + (size_t)el * NPADS * nst_pad(n, S) + 2 * nst_pad(n, S);
+          int he = npf.fhd[prv][el], le = npf.fln[prv][el];
+          int known = le;
+          double Ae = npf.fA[prv][el], Be = npf.fB[prv][el];
+          if ((sh.rFlags[prv][el] & TR_STEP) && !sh.reset[prv][el]) {
+            le += 1;
+            known = le - 1;  // (the appended entry is formed in this iteration)
+            if (le >= n) {   // the pop of the oldest entry: the shaper state moves
+              const double r0 = ring[he];
+              if (p.shaper == MGN_SHAPER_DSR || p.shaper == MGN_SHAPER_DDR) {
+                Ae += p.eta * (r0 - Ae);
+                if (p.shaper == MGN_SHAPER_DSR) {
+                  Be += p.eta * (r0 * r0 - Be);
+                } else {
+                  double m = r0 < 0. ? r0 : 0.;
+                  if (r0 != r0) m = r0;
+                  Be += p.eta * (m * m - Be);
+                }
+              }
+              he = (he + 1 == n) ? 0 : he + 1;
+              le -= 1;
+              known -= 1;
+            }
+          }
+          if (le + 1 == n && known > 0) {
+            nst_summands(ring, gscr, he, known, Ae, Be, pop_pre(p.shaper, Ae, Be));
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (ls == 0) {
+              npf.pfx[cur][el] = nst_sum(gscr, known);
+              npf.pA[cur][el] = Ae;
+              npf.pB[cur][el] = Be;
+              npf.phd[cur][el] = he;
+              npf.pcnt[cur][el] = known;
+            }
+            pl = le;
+          }
+        }
+        if (ls == 0) npf.pln[cur][el] = pl;
       }
 #pragma unroll
       for (int m = 0; m < M; ++m) sh.price[cur][lx + m] = s.P[m];
@@ -697,7 +829,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         ts = ts2;
       }
     }
-    if (live) {
+    if (live && !stored) {  // (TAIL_EXACT: written back in the last iteration)
       g_store();
       if (RP && ls == 0) p.rcur[env] = s.rcur;
     }
@@ -724,6 +856,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     int k = 0;
     int lpend = 0;  // WIN: refill ticks still to come after the reset tick
     int jlast = 0;  // TAIL: the last iteration
+    int lflags = 0;  // TAIL_EXACT: the flags of the last step run
+    bool lstored = false;  // TAIL_EXACT: the ledger written back in the last iteration
     // the ledger write-back at exit
     auto l_store = [&]() {
 #pragma unroll
@@ -887,7 +1021,28 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         // the Broker's post-order margin check (Broker.cpp:156-157) is the
         // finish role's (marginCall output), off this role's chain
         flags = TR_STEP | (any_mc ? TR_ANYMC : 0) | (in_kind != IN_NONE ? TR_MCALL : 0);
+        lflags = flags;
         k += 1;
+      }
+      if constexpr (TAIL_EXACT) {
+        // one-step launches, the last iteration: the finish role's done test
+        // on this env's step (rec_done); an episode that ends leaves the fresh
+        // Broker (Env.h:181-187).  The final ledger is written back here,
+        // while the finish role evaluates the step
+        if (K == 1 && j == 1 && live) {
+          if (p.auto_reset && (lflags & TR_STEP) &&
+              rec_done<M, S, ONE>(s.L, s.P, cash, sa.ml, sa.sh, sa.b, (lflags & TR_ANYMC) != 0, p)) {
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+              s.L[m] = 0.;
+              s.mep[m] = 0.;
+              s.Bm[m] = 0.;
+            }
+            cash = p.init_cash;
+          }
+          l_store();
+          lstored = true;
+        }
       }
       if (WIN && refill) {
         // the refill row's portfolio (the fresh Broker's): F evaluates it
@@ -940,7 +1095,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     if constexpr (TAIL) {
       // a tail reset (the finish role found the episode's end in the last
       // iteration): the fresh Broker (Env.h:181-187)
-      if (live && sh.reset[jlast & 1][el]) {
+      if (live && !lstored && sh.reset[jlast & 1][el]) {
 #pragma unroll
         for (int m = 0; m < M; ++m) {
           s.L[m] = 0.;
@@ -950,7 +1105,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         cash = p.init_cash;
       }
     }
-    if (live) l_store();
+    if (live && !lstored) l_store();
     MGN_IT_DRAIN();
     MGN_IT(45, TRIO_W);
     return;
@@ -1193,13 +1348,35 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           }
           const PopPre c = pop_pre(p.shaper, g.shA, g.shB);
           double acc = 0.0;
-          nst_summands(ring, scr, head, len, g.shA, g.shB, c);
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          // the ordered sum only feeds the popped value the env's first lane
-          // stores: only that lane reads the summands back
-          if (ls == 0) acc = nst_sum(scr, len);
+          bool pre = false;
+          if constexpr (NPF) {
+            // the generator's prefix (NPF): where the buffer is the one it
+            // predicted -- oldest index, fill count and shaper state bit for
+            // bit -- its ordered sum of the first pcnt summands, then the rest
+            // in entry order (the env's first lane)
+            pre = pj == 0 && len == n && npf.pln[prv][el] == nlen && npf.phd[prv][el] == nhead &&
+                  __double_as_longlong(npf.pA[prv][el]) == __double_as_longlong(g.shA) &&
+                  __double_as_longlong(npf.pB[prv][el]) == __double_as_longlong(g.shB);
+          }
+          if constexpr (NPF) {
+            if (pre && ls == 0) {
+              acc = npf.pfx[prv][el];
+              for (int kk = npf.pcnt[prv][el]; kk < len; ++kk) {
+                int idx = head + kk;
+                idx -= (idx >= n) ? n : 0;
+                acc += pop_term(p.shaper, ring[idx], g.shA, g.shB, c, s_disc[kk]);
+              }
+            }
+          }
+          if (!pre) {
+            nst_summands(ring, scr, head, len, g.shA, g.shB, c);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // the ordered sum only feeds the popped value the env's first lane
+            // stores: only that lane reads the summands back
+            if (ls == 0) acc = nst_sum(scr, len);
+          }
           double res = acc;
           if (p.shaper == MGN_SHAPER_DSR || p.shaper == MGN_SHAPER_DDR) {
             res = clip1(acc / len);
@@ -1325,6 +1502,16 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       push_row(Pf, pa, (cashf - bf) / eq, (uint64_t)sh.ts[prv][el], klast, prv);
     }
     if (ls == 0) sh.reset[cur][el] = rst_out;
+    if constexpr (NPF) {
+      // the buffer after this iteration's pops, for the generator's prefix
+      // of the next pop
+      if (ls == 0) {
+        npf.fA[cur][el] = g.shA;
+        npf.fB[cur][el] = g.shB;
+        npf.fhd[cur][el] = nhead;
+        npf.fln[cur][el] = nlen;
+      }
+    }
     // the reset tick runs next iteration -- a tail reset's in this one, by the
     // idle generator role (adopted after the loop)
     if (rst_out && !tail_rst) sh.more[j % 3] = 1;

@@ -32,9 +32,13 @@ def _kernels(usage, unit, pattern):
 CASES = [
     # k_step_trio<S, RQ1, DISC=true, OMC in {O_STD = 4093, O_ALL = 16383}, ...>: the
     # agent loop's instantiations, the C3 headline among them (S = 8, GK = TrendOU)
-    ("mgn_launch_a8.hip", r"k_step_trioILi8ELb[01]ELb1ELj(4093|16383)E", 0, "C3 headline"),
-    ("mgn_launch_a4.hip", r"k_step_trioILi4ELb[01]ELb1ELj(4093|16383)E", 0, "4-asset agent loop"),
-    ("mgn_launch_a2.hip", r"k_step_trioILi2ELb[01]ELb1ELj(4093|16383)E", 0, "2-asset agent loop"),
+    # (the multi-step instantiations: ONE = K1 = false, the name's last two flags)
+    ("mgn_launch_a8.hip", r"k_step_trioILi8ELb[01]ELb1ELj(4093|16383)E.*ELb0ELb0EEEv", 0, "C3 headline"),
+    ("mgn_launch_a4.hip", r"k_step_trioILi4ELb[01]ELb1ELj(4093|16383)E.*ELb0ELb0EEEv", 0, "4-asset agent loop"),
+    ("mgn_launch_a2.hip", r"k_step_trioILi2ELb[01]ELb1ELj(4093|16383)E.*ELb0ELb0EEEv", 0, "2-asset agent loop"),
+    # the one-step instantiations (K1): a few spills in the generator's
+    # last iteration (the reset tick beside the state write-back)
+    ("mgn_launch_a8.hip", r"k_step_trioILi8ELb[01]ELb1ELj(4093|16383)E.*ELb0ELb1EEEv", 8, "C3 one-step launches"),
     # the windowed one-wave-per-role instantiations (C2's OU windows)
     ("mgn_launch_a4.hip", r"k_step_trioILi4ELb[01]ELb1ELj0ELb1ELi64E", 0, "C2"),
     # n-step at APAD 8, built without machine LICM (n = 20 DDR)

@@ -449,6 +449,41 @@ __device__ __forceinline__ double chain_step(double c, double X1, double y, doub
   return go ? ci : c;
 }
 
+// The cash chain of one pass of broker_spec under its guess: lane i holds
+// order i's terms, and the cash before order i is handed from lane to lane
+// over DPP (row_shr:1 -- a segment of S <= 16 lanes lies in one 16-lane row):
+// in step t every lane applies its own order to the cash it holds, and lane
+// t + 1 takes lane t's result -- the serial sequence c_(i+1) =
+// step(c_i, order i), one chain_step per order as the serial form, with no
+// LDS round trip (the first lane's walk over the records in LDS, round 4,
+// cost ~1450 cycles per iteration at C3: each record read waited on, then
+// the published chain read back).  M orders per lane (two-slot layout): the
+// lane's orders in slot order within its step.  c_own[m]: the cash before the
+// lane's order m; cend: after the last order (the segment's last lane's)
+template <int S, int M>
+__device__ __forceinline__ void dpp_chain(double cash0, const OwnChk (&own)[M], const bool (&gown)[M], int ls,
+                                          double (&c_own)[M], double& cend) {
+  double cin = cash0, cout = cash0;
+  double mid[M];
+#pragma unroll
+  for (int t = 0; t < S; ++t) {
+    double c = cin;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      mid[m] = c;
+      c = chain_step(c, own[m].X1, own[m].y, own[m].Z, gown[m]);
+    }
+    cout = c;
+    if (t + 1 < S) {
+      const double sh = dpp_f64<0x111>(cout);  // row_shr:1
+      cin = (ls == t + 1) ? sh : cin;
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < M; ++m) c_own[m] = mid[m];
+  cend = seg_bcast<S, S - 1>(cout);
+}
+
 // The canonical trees of broker_spec in registers: every lane
 // holds its own order's four leaves before (pre) and after (post) the order;
 // the tree of lane ls's check has post leaves for the executed orders j < ls
@@ -550,25 +585,13 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
     if (it == 0) t_tr = __builtin_amdgcn_s_memtime();
 #endif
     // cash before this lane's order, and after the last order, under the
-    // guess: the chain is the env's, not the lane's, so its first lane walks
-    // it (one lane of the env reads the records' cash terms) and publishes
-    // the cash before every order and after the last
-    if (ls == 0) {
-      double c = cash0;
-#pragma unroll
-      for (int i = 0; i < S; ++i) {
-        er.cpre[i] = c;
-        const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
-        const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
-        c = chain_step(c, xz.y, yz.x, yz.y, ((go_bits >> i) & 1) != 0);
-      }
-      er.cpre[S] = c;
+    // guess (dpp_chain)
+    double cown1[1];
+    {
+      const bool g1[1] = {((go_bits >> ls) & 1) != 0};
+      dpp_chain<S, 1>(cash0, oc, g1, ls, cown1, cend);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const double c_own = er.cpre[ls];
-    cend = er.cpre[S];
+    const double c_own = cown1[0];
 #ifdef MGN_STAMPS
     if (it == 0) t_ch = __builtin_amdgcn_s_memtime();
 #endif
@@ -628,8 +651,8 @@ __device__ __forceinline__ void broker_spec(Lane<1>& s, const KParams& p, EnvRec
 // of slot 0 reads the pair pre + pre, slot 1 (post of slot 0 where it
 // executes) + pre, and the pair's P / Q versions go on to dpp_tree4's
 // cross-lane levels, which add the same sibling to both slots' paths.  The
-// cash chain is walked by the env's first lane over all 2 S orders, as in
-// broker_spec; the fix-up of a wrong guess is broker_spec's
+// cash chain is dpp_chain's with the lane's two orders per step; the fix-up
+// of a wrong guess is broker_spec's
 // (the first order whose check disagrees decides, the later ones are guessed
 // again), so the result is the sequential Broker's.
 template <int S, bool RQ1>
@@ -703,27 +726,16 @@ __device__ __forceinline__ void broker_spec_m2(Lane<2>& s, const KParams& p, Env
 #pragma unroll
       for (int q = 0; q < 4; ++q) rootP[q] = nP[q];
     }
-    if (ls == 0) {
-      double c = cash0;
-#pragma unroll
-      for (int i = 0; i < APAD; ++i) {
-        er.cpre[i] = c;
-        const d2 xz = *reinterpret_cast<const d2*>(&er.r[i].aPX);  // {aPX, X1}
-        const d2 yz = *reinterpret_cast<const d2*>(&er.r[i].y);    // {y, Z}
-        c = chain_step(c, xz.y, yz.x, yz.y, ((go_bits >> i) & 1) != 0);
-      }
-      er.cpre[APAD] = c;
+    double cownm[M];
+    {
+      const bool gm[M] = {g0, g1};
+      dpp_chain<S, M>(cash0, oc, gm, ls, cownm, cend);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const d2 cown = *reinterpret_cast<const d2*>(&er.cpre[sh0]);
-    cend = er.cpre[APAD];
     uint32_t badm = 0, gom = 0;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       const double* r = m == 0 ? path0 : path1;
-      const double c_own = m == 0 ? cown.x : cown.y;
+      const double c_own = cownm[m];
       // Portfolio::checkRisk(i, u), Portfolio.cpp:254-279 (as XRounds)
       const double pnl = r[0] - r[1];
       const double balance = c_own + r[2];

@@ -829,16 +829,14 @@ struct alignas(16) OrderRec {
   double Z;        // borrowed repaid / negative-borrow cleared, else +0.0
   uint32_t act, need_mc, need_insuff, pad;
 };
-// cpre: the speculative broker's cash chain (broker_spec, one lane per env):
-// the cash before each order, then after the last.  The stride of an env's
-// records is 4 (mod 8) dwords, so the segments of a wave start in distinct
-// groups of four LDS banks
+// (XRounds' records; the speculative broker keeps its orders in registers.)
+// The stride of an env's records is 4 (mod 8) dwords, so the segments of a
+// wave start in distinct groups of four LDS banks
 template <int APAD>
 struct alignas(16) EnvRecs {
-  static constexpr int kBaseDw = APAD * 28 + (APAD + 2) * 2;
+  static constexpr int kBaseDw = APAD * 28;
   static constexpr int kPadD = (((4 - kBaseDw) % 8 + 8) % 8) / 2;
   OrderRec r[APAD];
-  double cpre[APAD + 2];
   double pad[kPadD > 0 ? kPadD : 4];
 };
 
@@ -954,6 +952,7 @@ struct XRounds {
 // own instead; every order's cash terms X1, y, Z are published either way)
 struct OwnChk {
   double aPX;
+  double X1, y, Z;  // the order's cash terms (the chain's, broker_spec's dpp_chain)
   bool need_mc, need_insuff;
 };
 template <int M, int S, bool WPP = true>
@@ -1012,26 +1011,31 @@ __device__ __forceinline__ void order_prep(const Lane<M>& s, const KParams& p, E
     }
     const double aPX = opp ? fabs(price * excess) : fabs(price * u);
     const double X1v = close ? cur * tprice : -0.0, Zv = (repay || neg) ? bm1 : 0.0;
-    r.X1 = X1v;
-    r.y = use + tcost;
-    r.Z = Zv;
     const bool act = u != 0.;
-    if constexpr (WPP) {  // XRounds reads every order's check operands from LDS
+    if constexpr (WPP) {  // XRounds reads every order's check operands and cash terms from LDS
+      r.X1 = X1v;
+      r.y = use + tcost;
+      r.Z = Zv;
       r.aPX = aPX;
       r.act = act;
       r.need_mc = !opp;
       r.need_insuff = !opp || rev;
       r.pad = 0;
-    } else {  // broker_spec: the lane checks its own order only
+    } else {  // broker_spec: the lane checks its own order and holds its cash terms
       own[m].aPX = aPX;
+      own[m].X1 = X1v;
+      own[m].y = use + tcost;
+      own[m].Z = Zv;
       own[m].need_mc = !opp;
       own[m].need_insuff = !opp || rev;
     }
   }
-  // the segment's records are written by its own lanes: wave-scope ordering
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if constexpr (WPP) {
+    // the segment's records are written by its own lanes: wave-scope ordering
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
 
 }
 

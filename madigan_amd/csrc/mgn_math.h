@@ -165,6 +165,33 @@ constexpr double TWO_M32 = 2.3283064365386962890625e-10;
 // reward would carry its last-bit error at a large relative size.  Every step
 // kernel uses these helpers, so the schedules stay bit-identical.
 constexpr int kNormalClass = (1 << 3) | (1 << 8);  // v_cmp_class: -normal | +normal
+
+// IEEE binary64 x / y split at the reciprocal.  The compiler's division
+// (v_div_scale twice, v_rcp, four Newton fma, mul, fma, v_div_fmas,
+// v_div_fixup) forms a refined reciprocal of y that depends on y alone
+// wherever v_div_scale leaves both operands unscaled -- y and x / y normal,
+// the exponent of x above 53 - 1023 and at most 767 above y's -- and there
+// v_div_fmas is a plain fma and v_div_fixup the identity.  rcp_refined(y) is
+// that reciprocal for |y| in [2^-150, 2^150] (0 outside); div_by_rcp(x, y, r)
+// finishes the quotient with the sequence's last three operations for |x| in
+// [2^-600, 2^600] and falls back to the division elsewhere: the IEEE
+// quotient, bit for bit.  (The three-role kernel's generator forms the
+// reciprocal of each price it publishes, off the ledger's chain.)
+__device__ __forceinline__ double rcp_refined(double y) {
+  const double ay = fabs(y);
+  if (!(ay >= 0x1p-150 && ay <= 0x1p150)) return 0.;
+  const double r = __builtin_amdgcn_rcp(y);
+  const double f1 = __builtin_fma(r, __builtin_fma(-y, r, 1.0), r);
+  return __builtin_fma(f1, __builtin_fma(-y, f1, 1.0), f1);
+}
+__device__ __forceinline__ double div_by_rcp(double x, double y, double r) {
+  const double ax = fabs(x);
+  if (r != 0. && ax >= 0x1p-600 && ax <= 0x1p600) {
+    const double q = x * r;
+    return __builtin_fma(__builtin_fma(-y, q, x), r, q);
+  }
+  return x / y;
+}
 __device__ __forceinline__ double rt_div(double a, double b) {
   if (!__builtin_amdgcn_class(b, kNormalClass)) return a / b;
   double r = __builtin_amdgcn_rcp(b);

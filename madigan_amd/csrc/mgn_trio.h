@@ -137,8 +137,9 @@ struct TrioShared {
   static constexpr int TRIO_W = TW;
   static constexpr int EPB = TRIO_W / S;
   static constexpr int NSL = TRIO_W * M;  // asset slots of the block
-  // prices after the iteration's tick (G -> L, F)
-  double price[2][NSL];
+  // prices after the iteration's tick (G -> L, F) and their refined
+  // reciprocals (G -> L: the unit size's division, rcp_refined)
+  double price[2][NSL], prcp[2][NSL];
   // the orders L ran (L -> F): ledger after the orders, responses, L*P before
   double rL[2][NSL], rTp[2][NSL], rTu[2][NSL], rTc[2][NSL], rPv[2][NSL];
   int32_t rRk[2][NSL];
@@ -779,7 +780,10 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         if (ls == 0) npf.pln[cur][el] = pl;
       }
 #pragma unroll
-      for (int m = 0; m < M; ++m) sh.price[cur][lx + m] = s.P[m];
+      for (int m = 0; m < M; ++m) {
+        sh.price[cur][lx + m] = s.P[m];
+        if (DISC) sh.prcp[cur][lx + m] = rcp_refined(s.P[m]);  // (the ledger's unit size)
+      }
       if constexpr (GLOG) {
         // the window row's log price (StackerDiscrete's log normaliser,
         // preprocessor.py:79-81) off the finish role's chain
@@ -957,7 +961,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #pragma unroll
           for (int m = 0; m < M; ++m) {
             if (s.valid[m]) {
-              const double u = p.unit_size * avM / s.P[m];
+              // (unit_size avM) / P with the generator's reciprocal of P
+              // (iteration 0 reads the handle's prices, not the generator's: no reciprocal)
+              const double u = div_by_rcp(p.unit_size * avM, s.P[m], j > 0 ? sh.prcp[prv][lx + m] : 0.);
               uc[m] = (double)(act_now[m] - half) * u;
               if (act_now[m] == 0) uc[m] = (s.L[m] != 0) ? -s.L[m] : 0.;
             }

@@ -386,7 +386,12 @@ void choose_sched(mgn_env* e) {
     // 8192 x 16 TrendOU) and replay tapes (C5: 405 vs 485 us per 64-step launch),
     // and, where its two-slots-per-lane layout runs the agent loop's discrete
     // steps (trio_m2_ok), windowed generator handles too
-    e->trio = trio_eligible(e) && e->m == 1 &&
+    // one asset with a window: the two-lane layout's one-wave-per-role grid
+    // holds 16384 envs in one round (two workgroups per CU); beyond it the
+    // single-role kernel's one lane per env measured faster (R1 at 65536:
+    // 1098 vs 1507 us per 64-step launch, profiles/r05c_bench_R1.json)
+    const bool one_win_big = e->apad == 1 && e->W > 0 && e->N > 16384;
+    e->trio = trio_eligible(e) && e->m == 1 && !one_win_big &&
               (e->apad <= 8 ||
                (e->apad <= 16 && ((e->W == 0 && e->cfg.nstep == 1) || e->replay ||
                                   mgn::trio_m2_ok(e->N, e->A, e->cfg.nstep, e->D, mgn::IN_DISCRETE))));

@@ -1186,6 +1186,14 @@ __device__ __forceinline__ double root_e(double x, double e) {
 __device__ __forceinline__ double max_m1(double x) { return (x < -1.) ? -1. : x; }          // clip(x, -1, None)
 __device__ __forceinline__ double min_0(double x) { return (x < 0. || x != x) ? x : 0.; }  // minimum(x, 0.)
 
+// sortino_shaperB's summand of entry k of a buffer of more than one entry
+// (nstep_buffer.py:293-312, naive_n's): the clipped, sign-preserving e-th
+// root of the discounted entry; the pop is clip(sum) over the entries in order
+__device__ __forceinline__ double sortinoB_term(double r, double disc_k, double ex) {
+  const double v = max_m1((r - 0.) * disc_k);
+  return (v < 0.) ? -root_e(-v, ex) : v;
+}
+
 // the len(nstep_buffer) == 1 heuristics (:212-216, :244-249, :286-291)
 __device__ __noinline__ double naive1(int shaper, double r, double ex) {
   double diff = r - 0.;

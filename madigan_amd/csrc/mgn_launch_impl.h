@@ -166,9 +166,9 @@ void launch_trio_nst(const StepArgs& a) {
     }
   } else if (disc && a.gkind == MGN_SRC_TRENDOU) {
     // (the generator role forms the next pop's prefix: a third pad per env)
-    static_assert(trio_npf(true, MGN_SRC_TRENDOU, 1), "");
-    if (a.p.reqm_one) go(k_step_trio<S, true, true, 0, false, TRIO_W, true, MGN_SRC_TRENDOU>, true, 3);
-    else go(k_step_trio<S, false, true, 0, false, TRIO_W, true, MGN_SRC_TRENDOU>, true, 3);
+    constexpr int np = trio_npf(true, MGN_SRC_TRENDOU, 1) ? 3 : 2;
+    if (a.p.reqm_one) go(k_step_trio<S, true, true, 0, false, TRIO_W, true, MGN_SRC_TRENDOU>, true, np);
+    else go(k_step_trio<S, false, true, 0, false, TRIO_W, true, MGN_SRC_TRENDOU>, true, np);
   } else if (disc) {
     if (a.p.reqm_one) goN(k_step_trio<S, true, true, 0, false, TRIO_W, true>);
     else goN(k_step_trio<S, false, true, 0, false, TRIO_W, true>);

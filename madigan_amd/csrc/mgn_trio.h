@@ -238,7 +238,12 @@ inline size_t trio_nst_dyn_lds(int S, int TW, int nstep, int npads = 2) {
   return (size_t)(TW / S) * npads * nst_pad(nstep, S) * sizeof(double);
 }
 // NPF: n-step launches whose generator lanes are env-major (one source kind)
-__host__ __device__ constexpr bool trio_npf(bool nst, int gk, int mm) { return nst && gk >= 0 && mm == 1; }
+__host__ __device__ constexpr bool trio_npf(bool nst, int gk, int mm) {
+#if defined(MGN_DIAG) && defined(MGN_NO_NPF)  // diagnostic A/B builds: the finish role pops in full
+  return false;
+#endif
+  return nst && gk >= 0 && mm == 1;
+}
 
 // OMC: the output set when known at compile time (O_ALL, O_STD), else 0.
 // WIN: the handle keeps a window (StackerDiscrete ring, and the launch
@@ -515,7 +520,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #ifdef MGN_NST_ABL_TERM  // diagnostic timing build (outputs wrong): no summand arithmetic
         const double t = rr[u];
 #else
-        const double t = pop_term(p.shaper, rr[u], A, B, c, dd[u]);
+        const double t = (p.shaper == MGN_SHAPER_SORTINO_B) ? sortinoB_term(rr[u], dd[u], p.sexp)
+                                                            : pop_term(p.shaper, rr[u], A, B, c, dd[u]);
 #endif
         if (j + u < R) scr[kk] = (kk < len) ? t : 0.0;
       }
@@ -735,7 +741,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         // pop's summands over the entries the ring holds now (the ring and
         // the state are in LDS from iteration 1 on)
         int pl = -1;
-        if (j > 0 && live && p.shaper < MGN_SHAPER_SHARPE) {
+        if (j > 0 && live && (p.shaper < MGN_SHAPER_SHARPE || p.shaper == MGN_SHAPER_SORTINO_B)) {
           const int n = p.nstep;
           const double* ring = s_nst + (size_t)el * NPADS * nst_pad(n, S);
           double* gscr = s_nst + (size_t)el * NPADS * nst_pad(n, S) + 2 * nst_pad(n, S);
@@ -1338,11 +1344,13 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          if (p.shaper >= MGN_SHAPER_SHARPE) {
+          if (p.shaper == MGN_SHAPER_SHARPE || p.shaper == MGN_SHAPER_SORTINO_A ||
+              (p.shaper == MGN_SHAPER_SORTINO_B && len == 1)) {
             // the naive shapers (sharpe_shaper, sortino_shaperA / B,
             // nstep_buffer.py:207-312) over the ring by the env's first lane,
             // nstep_column's evaluation: the single-entry heuristic or the
-            // discounted sums in entry order
+            // discounted sums in entry order (sortino_shaperB's one sum, over
+            // more than one entry, takes the summand path below)
             if (ls == 0) {
               const double res = (len == 1) ? naive1(p.shaper, ring[head], p.sexp)
                                             : naive_n(p.shaper, ring, n, 1, 0, head, len, s_disc, p.sexp);
@@ -1370,7 +1378,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
               for (int kk = npf.pcnt[prv][el]; kk < len; ++kk) {
                 int idx = head + kk;
                 idx -= (idx >= n) ? n : 0;
-                acc += pop_term(p.shaper, ring[idx], g.shA, g.shB, c, s_disc[kk]);
+                acc += (p.shaper == MGN_SHAPER_SORTINO_B) ? sortinoB_term(ring[idx], s_disc[kk], p.sexp)
+                                                          : pop_term(p.shaper, ring[idx], g.shA, g.shB, c, s_disc[kk]);
               }
             }
           }
@@ -1384,6 +1393,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
             if (ls == 0) acc = nst_sum(scr, len);
           }
           double res = acc;
+          if (p.shaper == MGN_SHAPER_SORTINO_B) res = clip1(acc);  // (naive_n, len > 1)
           if (p.shaper == MGN_SHAPER_DSR || p.shaper == MGN_SHAPER_DDR) {
             res = clip1(acc / len);
             const double r0 = ring[head];

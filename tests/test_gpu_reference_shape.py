@@ -62,6 +62,7 @@ def _launch_vs_oracle(g, orc, acts, tag, shaped_rtol):
     (8192, "DDR", {}, 1e-10),
     (8192, "sortino_shaperB", dict(sortino_exp=1.1), 1e-10),
     (65536, "DDR", {}, 1e-10),
+    (2048, "sortino_shaperB", dict(sortino_exp=1.5), 1e-10),
 ])
 def test_reference_shape_vs_oracle(gpu, N, shaper, extra, rtol):
     from madigan_amd import _lib as L
@@ -69,7 +70,9 @@ def test_reference_shape_vs_oracle(gpu, N, shaper, extra, rtol):
     kw = dict(REF_KW, reward_shaper=shaper, **extra, seed=0x6D6164 + 21)
     kw.update(required_margin=0.05, unit_size=0.9)
     g, orc = make_pair(ou_sources(1), N, **kw)
-    assert g.lib.mgn_get_schedule(g.h) == L.SCHED_TRIO
+    # (beyond 16384 one-asset window envs the automatic schedule takes the
+    # single-role kernel, measured faster there)
+    assert g.lib.mgn_get_schedule(g.h) == (L.SCHED_TRIO if N <= 16384 else L.SCHED_SINGLE)
     K = 64 if N <= 8192 else 24
     acts = g.generate_actions(2 * K, seed=0x6D6164 + 22)
     ends = _launch_vs_oracle(g, orc, acts[:K], f"{shaper} N={N} launch 0", rtol)

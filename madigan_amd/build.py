@@ -127,18 +127,23 @@ RESOURCE_USAGE = os.path.join(OBJ, "resource_usage.json")
 
 
 def _flags_key() -> str:
+    """The build's configuration and inputs: flags per unit, the target and a
+    digest of every source and header (content, not mtime: an edit made while
+    a build was compiling must not look built)."""
+    import hashlib
     units = {os.path.basename(s): UNIT_FLAGS.get(os.path.basename(s), []) for s in sources()}
-    return repr((FLAGS, sorted(units.items()), ARCH))
+    h = hashlib.sha256()
+    for d in sorted(deps()):
+        with open(d, "rb") as f:
+            h.update(d.encode() + b"\0" + f.read())
+    return repr((FLAGS, sorted(units.items()), ARCH, h.hexdigest()))
 
 
 def needs_build() -> bool:
     if not os.path.exists(OUT) or not os.path.exists(FLAGS_STAMP) or not os.path.exists(RESOURCE_USAGE):
         return True
     with open(FLAGS_STAMP) as f:
-        if f.read() != _flags_key():
-            return True
-    t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(d) > t for d in deps())
+        return f.read() != _flags_key()
 
 
 def parse_resource_usage(text: str) -> dict:
@@ -163,6 +168,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
         _optional_pycall(False, verbose)
         return OUT
     os.makedirs(OBJ, exist_ok=True)
+    key = _flags_key()  # the inputs as they are when the compiles start
     cc = hipcc()
     jobs = jobs or min(8, os.cpu_count() or 4)
 
@@ -188,7 +194,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
     with open(RESOURCE_USAGE, "w") as f:
         json.dump({unit: usage for _, unit, usage in res}, f, indent=0, sort_keys=True)
     with open(FLAGS_STAMP, "w") as f:
-        f.write(_flags_key())
+        f.write(key)
     cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs, "-ldl"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

@@ -63,7 +63,7 @@ def test_step_kernels_do_not_spill(usage, unit, pattern, max_spill, what):
 def test_flag_change_rebuilds(monkeypatch):
     assert os.path.exists(B.FLAGS_STAMP)
     if B.needs_build():
-        pytest.skip("the library is out of date (sources newer than the build)")
+        pytest.skip("the library is out of date (its inputs changed since the build)")
     monkeypatch.setattr(B, "FLAGS", B.FLAGS + ["-DMGN_UNUSED_FLAG"])
     assert B.needs_build(), "a flag change alone must rebuild"
     monkeypatch.setattr(B, "UNIT_FLAGS", {})

@@ -29,17 +29,22 @@ ARCH = os.environ.get("MADIGAN_OFFLOAD_ARCH", "gfx950")
 # segment (k_step_trio passes its ledger-role pointers first)
 FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-fno-fast-math", "-Wall", "-mllvm", "-amdgpu-kernarg-preload-count=6"]
-# per-unit flags: the three-role kernel's two-slots-per-lane instantiations
-# (mgn_launch_a16m2.hip) are built without machine-level loop-invariant code
-# motion -- hoisting the math kernels' 64-bit polynomial constants out of the
-# step loop left them live across it at the 168-register budget and spilled
-# them to scratch (48 -> 4 spilled registers in the generic generator build)
-# The same holds for the n-step instantiations at APAD 8 (their own unit,
-# mgn_launch_a8nst.hip): n = 20 DDR 3.80 -> 3.69 us/step, while the one-step
-# instantiations of mgn_launch_a8.hip measured 1.5-2.7 % slower without it
-# (profiles/r04_ab_licm.txt)
-UNIT_FLAGS = {"mgn_launch_a16m2.hip": ["-mllvm", "-disable-machine-licm"],
-              "mgn_launch_a8nst.hip": ["-mllvm", "-disable-machine-licm"]}
+# per-unit flags: the step-kernel units are built without machine-level
+# loop-invariant code motion -- it hoisted the math kernels' 64-bit polynomial
+# constants out of the step loop, left them live across it at the register
+# budget and spilled them to scratch: 87-195 VGPRs in the 256-lane n-step
+# kernels, 24-264 in the single-role kernels, 72-91 in the two-role n-step
+# kernels, 48 -> 4 in the two-slot layout; without it every one of them
+# keeps its registers (tests/test_build.py; the single-role kernel's 4 and 8
+# slots per lane, 32 and 64 assets, still spill 14-75).  The C3 headline's unit
+# (mgn_launch_a8t.hip, the agent loop's instantiations at A = 8) keeps it: its
+# one-step instantiations measured 1.5-2.7 % slower without it
+# (profiles/r04_ab_licm.txt).  The n-step instantiations live in units of
+# their own (mgn_launch_a{1t,2,4,8,16}nst.hip).
+_NO_LICM = ["-mllvm", "-disable-machine-licm"]
+UNIT_FLAGS = {f"mgn_launch_{u}.hip": _NO_LICM
+              for u in ("a1", "a1t", "a1tnst", "a2", "a2nst", "a4", "a4nst", "a8", "a8nst", "a16", "a16m2", "a16nst",
+                        "a32", "a64")}
 
 
 def hipcc() -> str:

@@ -58,11 +58,20 @@ inline bool trio_m2_ok(long long n_envs, int A, int nstep, int D, int in_kind) {
          in_kind == IN_DISCRETE;
 }
 void launch_trio_m2_a16(const StepArgs& a);
-// the n-step three-role launches at APAD = 8, in their own unit (mgn_launch_a8nst.hip)
+// the agent loop's three-role launches at APAD = 8 (the C3 headline), in their
+// own unit (mgn_launch_a8t.hip)
+void launch_trio_agent_a8(const StepArgs& a);
+// the n-step three-role launches, in units of their own
+// (mgn_launch_a{2,4,8,16}nst.hip: built without machine LICM)
+void launch_trio_nst_a2(const StepArgs& a);
+void launch_trio_nst_a4(const StepArgs& a);
 void launch_trio_nst_a8(const StepArgs& a);
+void launch_trio_nst_a16(const StepArgs& a);
 // the three-role kernel for one-asset envs (ONE: S = 2 lanes, the second a
-// pad), in its own unit (mgn_launch_a1t.hip): discrete steps (the agent loop)
+// pad), in its own unit (mgn_launch_a1t.hip; the n-step handles in
+// mgn_launch_a1tnst.hip): discrete steps (the agent loop)
 void launch_trio_one(const StepArgs& a);
+void launch_trio_one_nst(const StepArgs& a);
 
 // smallest assets-per-lane with at most 16 lanes per env (DPP-only reductions)
 constexpr int min_m(int apad) { return apad > 16 ? apad / 16 : 1; }

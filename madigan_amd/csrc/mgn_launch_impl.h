@@ -139,8 +139,11 @@ struct TrioGo {
 
 // three-role pipelined step kernel (mgn_trio.h): S = APAD lanes per env per role
 // NST: the finish role's NStepBuffer rings in dynamic LDS (D = 1), with a
-// window for discrete steps (trio_launchable).  APAD 8 instantiates it in its
-// own unit (mgn_launch_a8nst.hip, UNIT_FLAGS)
+// window for discrete steps (trio_launchable).  Instantiated only by the
+// n-step units (mgn_launch_a{2,4,8,16}nst.hip, mgn_launch_a1tnst.hip), which
+// are built without machine-level LICM (madigan_amd/build.py UNIT_FLAGS: with
+// it, the loop-invariant constants hoisted out of the step loop spilled
+// 87-195 VGPRs of the 256-lane n-step kernels)
 template <int S>
 void launch_trio_nst(const StepArgs& a) {
   const bool small = (long long)a.p.N * S < 256LL * TRIO_W;
@@ -182,11 +185,12 @@ void launch_trio_nst(const StepArgs& a) {
 // sums are lane 0's one leaf), discrete steps (trio_launchable): window or
 // not, n = 1 or n-step (generator sources, any source kind); window handles
 // at one wave per role (the finish role's rows and pops need > 168 registers)
-// (a template: instantiated only by mgn_launch_a1t.hip)
-template <int S = 2>
+// (a template: instantiated only by mgn_launch_a1t.hip, NS = false, and by
+// mgn_launch_a1tnst.hip, NS = true: the n-step handles)
+template <int S = 2, bool NS_ = false>
 void launch_trio_one_impl(const StepArgs& a) {
   static_assert(S == 2, "one asset on two lanes per role");
-  const bool win = a.p.W > 0, nst = a.p.nstep > 1;
+  const bool win = a.p.W > 0;
   const bool small = win || (long long)a.p.N * S < 256LL * TRIO_W;
   const TrioGo<S> go{a, small};
   auto pick = [&](auto rq1, auto winc, auto nstc) {
@@ -200,13 +204,44 @@ void launch_trio_one_impl(const StepArgs& a) {
   };
   using T = std::true_type;
   using F = std::false_type;
+  using N = std::integral_constant<bool, NS_>;
   if (a.p.reqm_one) {
-    if (win) nst ? pick(T{}, T{}, T{}) : pick(T{}, T{}, F{});
-    else nst ? pick(T{}, F{}, T{}) : pick(T{}, F{}, F{});
+    win ? pick(T{}, T{}, N{}) : pick(T{}, F{}, N{});
   } else {
-    if (win) nst ? pick(F{}, T{}, T{}) : pick(F{}, T{}, F{});
-    else nst ? pick(F{}, F{}, T{}) : pick(F{}, F{}, F{});
+    win ? pick(F{}, T{}, N{}) : pick(F{}, F{}, N{});
   }
+}
+
+// the agent loop's output sets (O_STD / O_ALL) at the 256-lane layout,
+// discrete actions, generator sources, one-step rewards: compile-time output
+// masks.  One-step launches (the agent loop's K = 1, APAD <= 8) have their own
+// instantiations (K1: an episode that ends at the launch's step is reset
+// inside the launch, mgn_trio.h TAIL).  APAD 8 (the C3 headline) instantiates
+// it in its own unit (mgn_launch_a8t.hip, built with machine LICM)
+template <int S>
+void launch_trio_agent(const StepArgs& a) {
+  const int grid = (a.p.N + TRIO_W / S - 1) / (TRIO_W / S);
+  auto go = [&](auto kern) {
+    launch_timed(a.ev0, a.ev1, kern, dim3(grid), dim3(TRIO_BLOCK), 0, a.stream, a.p.L, a.p.mep, a.p.Bm, a.p.P,
+                 a.p.cash, a.act, a.p, a.out, a.in_kind, a.units, a.aidx, a.K);
+  };
+  const uint32_t om = traj_mask(a.out);
+  auto pick = [&](auto omc, auto k1) {
+    constexpr uint32_t OM = decltype(omc)::value;
+    constexpr bool K1 = decltype(k1)::value && S <= 8;
+    if (a.gkind == MGN_SRC_TRENDOU) {
+      if (a.p.reqm_one) go(k_step_trio<S, true, true, OM, false, TRIO_W, false, MGN_SRC_TRENDOU, false, 1, false, K1>);
+      else go(k_step_trio<S, false, true, OM, false, TRIO_W, false, MGN_SRC_TRENDOU, false, 1, false, K1>);
+    } else if (a.p.reqm_one) {
+      go(k_step_trio<S, true, true, OM, false, TRIO_W, false, -1, false, 1, false, K1>);
+    } else {
+      go(k_step_trio<S, false, true, OM, false, TRIO_W, false, -1, false, 1, false, K1>);
+    }
+  };
+  using STD = std::integral_constant<uint32_t, O_STD>;
+  using ALL = std::integral_constant<uint32_t, O_ALL>;
+  if (a.K == 1) om == O_STD ? pick(STD{}, std::true_type{}) : pick(ALL{}, std::true_type{});
+  else om == O_STD ? pick(STD{}, std::false_type{}) : pick(ALL{}, std::false_type{});
 }
 
 template <int S>
@@ -254,8 +289,12 @@ void launch_trio(const StepArgs& a) {
     return;
   }
   if (a.p.nstep > 1) {
-    if constexpr (S == 8) launch_trio_nst_a8(a);  // mgn_launch_a8nst.hip
-    else launch_trio_nst<S>(a);
+    // the n-step instantiations live in units of their own
+    // (mgn_launch_a{2,4,8,16}nst.hip, built without machine LICM)
+    if constexpr (S == 2) launch_trio_nst_a2(a);
+    else if constexpr (S == 4) launch_trio_nst_a4(a);
+    else if constexpr (S == 8) launch_trio_nst_a8(a);
+    else if constexpr (S == 16) launch_trio_nst_a16(a);
     return;
   }
   if (small) {  // runtime output mask, window or not
@@ -286,25 +325,8 @@ void launch_trio(const StepArgs& a) {
       else go(k_step_trio<S, false, false, 0, true>);
     }
   } else if (disc && (om == O_STD || om == O_ALL)) {  // the agent loop's output sets
-    // one-step launches (the agent loop's K = 1, APAD <= 8) have their own
-    // instantiations (K1: an episode that ends at the launch's step is reset
-    // inside the launch, mgn_trio.h TAIL)
-    auto pick = [&](auto omc, auto k1) {
-      constexpr uint32_t OM = decltype(omc)::value;
-      constexpr bool K1 = decltype(k1)::value && S <= 8;
-      if (a.gkind == MGN_SRC_TRENDOU) {
-        if (a.p.reqm_one) go(k_step_trio<S, true, true, OM, false, TRIO_W, false, MGN_SRC_TRENDOU, false, 1, false, K1>);
-        else go(k_step_trio<S, false, true, OM, false, TRIO_W, false, MGN_SRC_TRENDOU, false, 1, false, K1>);
-      } else if (a.p.reqm_one) {
-        go(k_step_trio<S, true, true, OM, false, TRIO_W, false, -1, false, 1, false, K1>);
-      } else {
-        go(k_step_trio<S, false, true, OM, false, TRIO_W, false, -1, false, 1, false, K1>);
-      }
-    };
-    using STD = std::integral_constant<uint32_t, O_STD>;
-    using ALL = std::integral_constant<uint32_t, O_ALL>;
-    if (a.K == 1) om == O_STD ? pick(STD{}, std::true_type{}) : pick(ALL{}, std::true_type{});
-    else om == O_STD ? pick(STD{}, std::false_type{}) : pick(ALL{}, std::false_type{});
+    if constexpr (S == 8) launch_trio_agent_a8(a);  // mgn_launch_a8t.hip
+    else launch_trio_agent<S>(a);
   } else if (disc) {
     if (a.p.reqm_one) go(k_step_trio<S, true, true>);
     else go(k_step_trio<S, false, true>);

@@ -186,11 +186,18 @@ __device__ __forceinline__ double rcp_refined(double y) {
 }
 __device__ __forceinline__ double div_by_rcp(double x, double y, double r) {
   const double ax = fabs(x);
-  if (r != 0. && ax >= 0x1p-600 && ax <= 0x1p600) {
-    const double q = x * r;
-    return __builtin_fma(__builtin_fma(-y, q, x), r, q);
+  const bool fast = r != 0. && ax >= 0x1p-600 && ax <= 0x1p600;
+  double q = x * r;
+  q = __builtin_fma(__builtin_fma(-y, q, x), r, q);
+  if (!fast) {
+    // (the empty volatile asm keeps the division in its branch: speculated,
+    // as the compiler otherwise does with a lone fdiv, every lane would run
+    // it beside the finish above)
+    double xs = x;
+    asm volatile("" : "+v"(xs));
+    q = xs / y;
   }
-  return x / y;
+  return q;
 }
 __device__ __forceinline__ double rt_div(double a, double b) {
   if (!__builtin_amdgcn_class(b, kNormalClass)) return a / b;

@@ -1,11 +1,12 @@
 """CPU checks of the product build (madigan_amd/build.py): the library is
-rebuilt when only its flags change, and the step kernels the automatic
-schedule runs at the benchmarked shapes keep their registers -- no spill to
-scratch -- as the compiler reports them (-Rpass-analysis=kernel-resource-usage,
-recorded by every build in madigan_amd/_obj/resource_usage.json).  Two units
-are built without machine LICM (build.UNIT_FLAGS), which kept their math
-constants from being hoisted out of the step loop and spilled; a compiler
-update that re-spills them fails here rather than only measuring slower."""
+rebuilt when only its flags change, and the step kernels keep their registers
+-- no spill to scratch -- as the compiler reports them
+(-Rpass-analysis=kernel-resource-usage, recorded by every build in
+madigan_amd/_obj/resource_usage.json).  The step units other than A = 8 are
+built without machine LICM (build.UNIT_FLAGS), which kept their math constants
+from being hoisted out of the step loop and spilled (87-264 VGPRs in the n-step,
+two-role n-step and single-role kernels); a compiler update that re-spills them
+fails here rather than only measuring slower."""
 import json
 import os
 import re
@@ -29,24 +30,22 @@ def _kernels(usage, unit, pattern):
 
 
 # (unit, mangled-name pattern, the most VGPRs the kernels may spill, why)
+_NO_LICM_UNITS = sorted(B.UNIT_FLAGS)
 CASES = [
     # k_step_trio<S, RQ1, DISC=true, OMC in {O_STD = 4093, O_ALL = 16383}, ...>: the
     # agent loop's instantiations, the C3 headline among them (S = 8, GK = TrendOU)
     # (the multi-step instantiations: ONE = K1 = false, the name's last two flags)
-    ("mgn_launch_a8.hip", r"k_step_trioILi8ELb[01]ELb1ELj(4093|16383)E.*ELb0ELb0EEEv", 0, "C3 headline"),
-    ("mgn_launch_a4.hip", r"k_step_trioILi4ELb[01]ELb1ELj(4093|16383)E.*ELb0ELb0EEEv", 0, "4-asset agent loop"),
-    ("mgn_launch_a2.hip", r"k_step_trioILi2ELb[01]ELb1ELj(4093|16383)E.*ELb0ELb0EEEv", 0, "2-asset agent loop"),
+    ("mgn_launch_a8t.hip", r"k_step_trioILi8ELb[01]ELb1ELj(4093|16383)E.*ELb0ELb0EEEv", 0, "C3 headline"),
     # the one-step instantiations (K1): a few spills in the generator's
     # last iteration (the reset tick beside the state write-back)
-    ("mgn_launch_a8.hip", r"k_step_trioILi8ELb[01]ELb1ELj(4093|16383)E.*ELb0ELb1EEEv", 8, "C3 one-step launches"),
-    # the windowed one-wave-per-role instantiations (C2's OU windows)
-    ("mgn_launch_a4.hip", r"k_step_trioILi4ELb[01]ELb1ELj0ELb1ELi64E", 0, "C2"),
-    # n-step at APAD 8, built without machine LICM (n = 20 DDR)
-    ("mgn_launch_a8nst.hip", r"k_step_trio", 0, "n-step, -disable-machine-licm"),
-    # two slots per lane (C5, 16 assets), built without machine LICM: 48 -> 4
-    # spilled VGPRs in round 4; more is a regression
-    ("mgn_launch_a16m2.hip", r"k_step_trio", 4, "two slots per lane, -disable-machine-licm"),
-]
+    ("mgn_launch_a8t.hip", r"k_step_trioILi8ELb[01]ELb1ELj(4093|16383)E.*ELb0ELb1EEEv", 8, "C3 one-step launches"),
+    # the two-slot layout's window instantiations (C5's): 48 -> 2 in round 4
+    ("mgn_launch_a16m2.hip", r"k_step_trio", 2, "two slots per lane"),
+    # the single-role kernel's 4 and 8 slots per lane (32 / 64 assets)
+    ("mgn_launch_a32.hip", r"k_stepILi4E", 32, "single-role, 4 slots per lane"),
+    ("mgn_launch_a64.hip", r"k_stepILi[48]E", 80, "single-role, 4 / 8 slots per lane"),
+] + [(u, r"k_step(_trio|_duo|ILi[12]E)", 0, "built without machine LICM")
+     for u in _NO_LICM_UNITS if u not in ("mgn_launch_a16m2.hip", "mgn_launch_a64.hip")]
 
 
 @pytest.mark.parametrize("unit,pattern,max_spill,what", CASES)

@@ -2,7 +2,7 @@
 
     python tools/build_variant.py NAME [-DMGN_STAMPS ...]
 
-Recompiles mgn_api.hip and mgn_launch_a8.hip (the A = 8 step kernels) with the
+Recompiles mgn_api.hip and mgn_launch_a8t.hip (the C3 headline kernels) with the
 extra flags, links them with the product objects of the other APAD units into
 tools/_var/NAME/libmadigan_hip.so; select it with MADIGAN_LIB_PATH.  Development
 tool only: the product library is madigan_amd/libmadigan_hip.so.
@@ -26,8 +26,8 @@ def main():
     os.makedirs(out_dir, exist_ok=True)
     cc = B.hipcc()
     # the translation units rebuilt with the extra flags (MGN_VARIANT_UNITS,
-    # comma-separated APADs: default the A = 8 kernels)
-    units = os.environ.get("MGN_VARIANT_UNITS", "8").split(",")
+    # comma-separated unit suffixes: default 8t, the C3 headline's unit)
+    units = os.environ.get("MGN_VARIANT_UNITS", "8t").split(",")
     redo = {"mgn_api.hip"} | {f"mgn_launch_a{u}.hip" for u in units}
 
     def one(src):

@@ -31,7 +31,13 @@ def main():
     assert int(env.lib.mgn_get_schedule(env.h)) == L.SCHED_TRIO
     # the two-slot kernels (9..16 assets at >= 4096 envs) keep their stamps in
     # their own unit (mgn_launch_a16m2.hip)
-    fn = env.lib.mgn_diag_stamps_m2 if env.A > 8 and N * 16 >= 65536 else env.lib.mgn_diag_stamps
+    # (and the n-step kernels at APAD 8 in mgn_launch_a8nst.hip)
+    if env.A > 8 and N * 16 >= 65536:
+        fn = env.lib.mgn_diag_stamps_m2
+    elif nst > 1 and env.A == 8:
+        fn = env.lib.mgn_diag_stamps_nst
+    else:
+        fn = env.lib.mgn_diag_stamps
     fn.argtypes = [C.POINTER(C.c_ulonglong)]
     acts = env.generate_actions(fuse, seed=5)
     out = env.alloc_traj(fuse, fields=["reward", "shaped", "done", "obs_price", "obs_port", "timestamp",

@@ -439,49 +439,51 @@ __device__ __forceinline__ void duo_store(const DuoRec<S>& sh, const Lane<1>& s,
   }
 }
 
-// One order of the Broker's cash chain (Broker.cpp:128-135): cash becomes
-// ((cash + X1) - y) - Z when the order executes.  (Tried and not kept, round
-// 4: the skipped orders' terms masked to the additions' identities, 2-5 %
-// slower, profiles/r04_ab_chain_mask.txt; a one-subtraction chain when no
-// order of the wave closes or settles, mixed, profiles/r04_ab_plain_chain.txt)
-__device__ __forceinline__ double chain_step(double c, double X1, double y, double Z, bool go) {
-  const double ci = ((c + X1) - y) - Z;
-  return go ? ci : c;
-}
-
-// The cash chain of one pass of broker_spec under its guess: lane i holds
-// order i's terms, and the cash before order i is handed from lane to lane
-// over DPP (row_shr:1 -- a segment of S <= 16 lanes lies in one 16-lane row):
-// in step t every lane applies its own order to the cash it holds, and lane
-// t + 1 takes lane t's result -- the serial sequence c_(i+1) =
-// step(c_i, order i), one chain_step per order as the serial form, with no
-// LDS round trip (the first lane's walk over the records in LDS, round 4,
-// cost ~1450 cycles per iteration at C3: each record read waited on, then
-// the published chain read back).  M orders per lane (two-slot layout): the
-// lane's orders in slot order within its step.  c_own[m]: the cash before the
-// lane's order m; cend: after the last order (the segment's last lane's)
+// The cash chain of one pass of broker_spec under its guess (Broker.cpp:
+// 128-135: cash becomes ((cash + X1) - y) - Z when an order executes), systolic over
+// DPP (row_shr:1 -- a segment of S <= 16 lanes lies in one 16-lane row): lane
+// i holds order i's terms, masked once per pass to the additions' identities
+// where the guess skips the order ((c + -0.0) - 0.0 - 0.0 == c, bit for bit,
+// -0.0 and NaN included); in every step each lane applies its order to the
+// cash it holds and hands the result to lane i + 1, while the segment's first
+// lane keeps cash0.  After step t the lanes 0..t + 1 hold their final values
+// (lane i: the serial c_i = step(c_(i-1), order i-1), one chain_step per
+// order as the serial form), so S - 1 steps leave every lane its cash before
+// its own order, with no LDS round trip (the first lane's walk over the
+// records in LDS, round 4, cost ~1450 cycles per iteration at C3) and no
+// per-step select of the executing orders (masking the terms was 2-5 %
+// slower on round 4's one-lane walk, profiles/r04_ab_chain_mask.txt, where it
+// replaced one select per order).  M orders per lane (two-slot
+// layout): the lane's orders in slot order within its step.  c_own[m]: the
+// cash before the lane's order m; cend: after the last order (the segment's
+// last lane's)
 template <int S, int M>
 __device__ __forceinline__ void dpp_chain(double cash0, const OwnChk (&own)[M], const bool (&gown)[M], int ls,
                                           double (&c_own)[M], double& cend) {
-  double cin = cash0, cout = cash0;
-  double mid[M];
+  double X1[M], y[M], Z[M];
 #pragma unroll
-  for (int t = 0; t < S; ++t) {
-    double c = cin;
+  for (int m = 0; m < M; ++m) {
+    X1[m] = gown[m] ? own[m].X1 : -0.0;
+    y[m] = gown[m] ? own[m].y : 0.0;
+    Z[m] = gown[m] ? own[m].Z : 0.0;
+  }
+  auto apply = [&](double c, double (&mid)[M]) {
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       mid[m] = c;
-      c = chain_step(c, own[m].X1, own[m].y, own[m].Z, gown[m]);
+      c = ((c + X1[m]) - y[m]) - Z[m];
     }
-    cout = c;
-    if (t + 1 < S) {
-      const double sh = dpp_f64<0x111>(cout);  // row_shr:1
-      cin = (ls == t + 1) ? sh : cin;
-    }
+    return c;
+  };
+  double v = cash0, mid[M];
+#pragma unroll
+  for (int t = 0; t + 1 < S; ++t) {
+    const double sh = dpp_f64<0x111>(apply(v, mid));  // row_shr:1
+    v = (ls == 0) ? cash0 : sh;
   }
+  cend = seg_bcast<S, S - 1>(apply(v, mid));
 #pragma unroll
   for (int m = 0; m < M; ++m) c_own[m] = mid[m];
-  cend = seg_bcast<S, S - 1>(cout);
 }
 
 // The canonical trees of broker_spec in registers: every lane

@@ -37,13 +37,14 @@ FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=
 # kernels, 48 -> 4 in the two-slot layout; without it every one of them
 # keeps its registers (tests/test_build.py; the single-role kernel's 4 and 8
 # slots per lane, 32 and 64 assets, still spill 14-75).  The C3 headline's unit
-# (mgn_launch_a8t.hip, the agent loop's instantiations at A = 8) keeps it: its
-# one-step instantiations measured 1.5-2.7 % slower without it
-# (profiles/r04_ab_licm.txt).  The n-step instantiations live in units of
+# (mgn_launch_a8t.hip, the agent loop's multi-step instantiations at A = 8)
+# keeps it: its 20-step launch measured 1-2 % slower without it
+# (profiles/r05e_licm20; the one-step launches, mgn_launch_a8k1.hip, 5 %
+# faster without it, r05e_licm1).  The n-step instantiations live in units of
 # their own (mgn_launch_a{1t,2,4,8,16}nst.hip).
 _NO_LICM = ["-mllvm", "-disable-machine-licm"]
 UNIT_FLAGS = {f"mgn_launch_{u}.hip": _NO_LICM
-              for u in ("a1", "a1t", "a1tnst", "a2", "a2nst", "a4", "a4nst", "a8", "a8nst", "a16", "a16m2", "a16nst",
+              for u in ("a1", "a1t", "a1tnst", "a2", "a2nst", "a4", "a4nst", "a8", "a8k1", "a8nst", "a16", "a16m2", "a16nst",
                         "a32", "a64")}
 
 

@@ -58,9 +58,10 @@ inline bool trio_m2_ok(long long n_envs, int A, int nstep, int D, int in_kind) {
          in_kind == IN_DISCRETE;
 }
 void launch_trio_m2_a16(const StepArgs& a);
-// the agent loop's three-role launches at APAD = 8 (the C3 headline), in their
-// own unit (mgn_launch_a8t.hip)
+// the agent loop's three-role launches at APAD = 8 (the C3 headline), in units
+// of their own: multi-step (mgn_launch_a8t.hip), one-step (mgn_launch_a8k1.hip)
 void launch_trio_agent_a8(const StepArgs& a);
+void launch_trio_agent_k1_a8(const StepArgs& a);
 // the n-step three-role launches, in units of their own
 // (mgn_launch_a{2,4,8,16}nst.hip: built without machine LICM)
 void launch_trio_nst_a2(const StepArgs& a);

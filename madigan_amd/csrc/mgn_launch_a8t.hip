@@ -1,9 +1,9 @@
-// the three-role kernel's agent-loop instantiations at APAD = 8 -- the C3
-// headline and its one-step launches (launch_trio_agent, mgn_launch_impl.h):
-// their own unit, the one built with machine LICM (madigan_amd/build.py)
+// the three-role kernel's multi-step agent-loop instantiations at APAD = 8 --
+// the C3 headline (launch_trio_agent_k, mgn_launch_impl.h): their own unit,
+// the one built with machine LICM (madigan_amd/build.py)
 #include "mgn_launch_impl.h"
 namespace mgn {
-void launch_trio_agent_a8(const StepArgs& a) { launch_trio_agent<8>(a); }
+void launch_trio_agent_a8(const StepArgs& a) { launch_trio_agent_k<8, false>(a); }
 }  // namespace mgn
 // diagnostic builds: this unit's copies of the stamp buffers (the headline's)
 #if defined(MGN_STAMPS) || defined(MGN_WALLX)

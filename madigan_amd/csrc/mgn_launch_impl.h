@@ -217,18 +217,20 @@ void launch_trio_one_impl(const StepArgs& a) {
 // masks.  One-step launches (the agent loop's K = 1, APAD <= 8) have their own
 // instantiations (K1: an episode that ends at the launch's step is reset
 // inside the launch, mgn_trio.h TAIL).  APAD 8 (the C3 headline) instantiates
-// it in its own unit (mgn_launch_a8t.hip, built with machine LICM)
-template <int S>
-void launch_trio_agent(const StepArgs& a) {
+// them in units of their own: the multi-step launches in mgn_launch_a8t.hip
+// (built with machine LICM), the one-step launches in mgn_launch_a8k1.hip
+// (without: with it they spilled 6 VGPRs and measured 7.3 against 6.9 us,
+// profiles/r05e_licm1)
+template <int S, bool K1_>
+void launch_trio_agent_k(const StepArgs& a) {
   const int grid = (a.p.N + TRIO_W / S - 1) / (TRIO_W / S);
   auto go = [&](auto kern) {
     launch_timed(a.ev0, a.ev1, kern, dim3(grid), dim3(TRIO_BLOCK), 0, a.stream, a.p.L, a.p.mep, a.p.Bm, a.p.P,
                  a.p.cash, a.act, a.p, a.out, a.in_kind, a.units, a.aidx, a.K);
   };
-  const uint32_t om = traj_mask(a.out);
-  auto pick = [&](auto omc, auto k1) {
+  auto pick = [&](auto omc) {
     constexpr uint32_t OM = decltype(omc)::value;
-    constexpr bool K1 = decltype(k1)::value && S <= 8;
+    constexpr bool K1 = K1_ && S <= 8;
     if (a.gkind == MGN_SRC_TRENDOU) {
       if (a.p.reqm_one) go(k_step_trio<S, true, true, OM, false, TRIO_W, false, MGN_SRC_TRENDOU, false, 1, false, K1>);
       else go(k_step_trio<S, false, true, OM, false, TRIO_W, false, MGN_SRC_TRENDOU, false, 1, false, K1>);
@@ -238,10 +240,18 @@ void launch_trio_agent(const StepArgs& a) {
       go(k_step_trio<S, false, true, OM, false, TRIO_W, false, -1, false, 1, false, K1>);
     }
   };
-  using STD = std::integral_constant<uint32_t, O_STD>;
-  using ALL = std::integral_constant<uint32_t, O_ALL>;
-  if (a.K == 1) om == O_STD ? pick(STD{}, std::true_type{}) : pick(ALL{}, std::true_type{});
-  else om == O_STD ? pick(STD{}, std::false_type{}) : pick(ALL{}, std::false_type{});
+  if (traj_mask(a.out) == O_STD) pick(std::integral_constant<uint32_t, O_STD>{});
+  else pick(std::integral_constant<uint32_t, O_ALL>{});
+}
+template <int S>
+void launch_trio_agent(const StepArgs& a) {
+  if constexpr (S == 8) {
+    if (a.K == 1) launch_trio_agent_k1_a8(a);  // mgn_launch_a8k1.hip
+    else launch_trio_agent_a8(a);              // mgn_launch_a8t.hip
+  } else {
+    if (a.K == 1) launch_trio_agent_k<S, true>(a);
+    else launch_trio_agent_k<S, false>(a);
+  }
 }
 
 template <int S>
@@ -325,8 +335,7 @@ void launch_trio(const StepArgs& a) {
       else go(k_step_trio<S, false, false, 0, true>);
     }
   } else if (disc && (om == O_STD || om == O_ALL)) {  // the agent loop's output sets
-    if constexpr (S == 8) launch_trio_agent_a8(a);  // mgn_launch_a8t.hip
-    else launch_trio_agent<S>(a);
+    launch_trio_agent<S>(a);
   } else if (disc) {
     if (a.p.reqm_one) go(k_step_trio<S, true, true>);
     else go(k_step_trio<S, false, true>);

@@ -104,7 +104,7 @@ __device__ __forceinline__ bool trio_exit(int j, int K, const int32_t& more) {
 // another role needs it (one-step launches, TAIL_EXACT)
 template <int M, int S, bool ONE>
 __device__ __forceinline__ bool rec_done(const double (&Lr)[M], const double (&P)[M], double cashv, double ml,
-                                         double shv, double b, bool any_mc, const KParams& p) {
+                                         double shv, double b, bool any_mc, const KParams& p, double& curEq) {
   double tlp[M];
 #pragma unroll
   for (int m = 0; m < M; ++m) tlp[m] = Lr[m] * P[m];
@@ -113,7 +113,7 @@ __device__ __forceinline__ bool rec_done(const double (&Lr)[M], const double (&P
   q.ml = ml;
   q.sh = shv;
   q.b = b;
-  const double curEq = (cashv + q.lp) - q.b;
+  curEq = (cashv + q.lp) - q.b;
   return any_mc || margin_call(q, cashv, p.mainM) || (curEq < 0.1 * p.init_cash);
 }
 
@@ -711,9 +711,10 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
               Lr[m] = sh.rL[prv][lx + m];
               Pr[m] = sh.price[prv][lx + m];
             }
+            double eq;
             cand = p.auto_reset && (fl & TR_STEP) && !sh.reset[prv][el] &&
                    rec_done<M, S, ONE>(Lr, Pr, sh.rCash[prv][el], sh.rMl[prv][el], sh.rSh[prv][el],
-                                       sh.rB[prv][el], (fl & TR_ANYMC) != 0, p);
+                                       sh.rB[prv][el], (fl & TR_ANYMC) != 0, p, eq);
             tail_it = true;
           }
           if (cand) {
@@ -858,6 +859,19 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     p.unit_size = in_vgpr(p.unit_size);
     const uint32_t act_step = (uint32_t)p.N * (uint32_t)A;
     const bool need_ar = (p.reward_mode != MGN_REWARD_ENV_LOG) || (om & O_AREW);  // as the finish role's
+    // the Broker responses' outputs (per asset (k, env, asset), as the finish role's)
+    struct {
+      MGN_G double *tprice, *tunits, *tcost;
+      MGN_G uint8_t* risk;
+      MGN_G double *obs_price, *obs_port;  // TAIL_EXACT
+    } ovl = {(om & O_TP) ? vptr(out.tprice) : nullptr, (om & O_TU) ? vptr(out.tunits) : nullptr,
+             (om & O_TC) ? vptr(out.tcost) : nullptr, (om & O_RISK) ? vptr(out.risk) : nullptr,
+             (TAIL_EXACT && (om & O_OPR)) ? vptr(out.obs_price) : nullptr,
+             (TAIL_EXACT && (om & O_OPT)) ? vptr(out.obs_port) : nullptr};
+    const uint32_t sNA = (uint32_t)p.N * (uint32_t)A, sNF = (uint32_t)p.N * (uint32_t)p.F,
+                   sNA1 = (uint32_t)p.N * (uint32_t)(A + 1);
+    const size_t bA = (size_t)env * A + s.asset[0], bP = (size_t)env * p.F + s.asset[0],
+                 bO = (size_t)env * (A + 1);
     // sums of the ledger (canonical trees): ml, sh, b change only with the
     // orders, lp with the prices; `fresh` = recompute all four (start, reset)
     Sums sa = port_sums<M, S, ONE>(s.L, s.mep, s.Bm, s.P);
@@ -1015,11 +1029,23 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #pragma unroll
         for (int m = 0; m < M; ++m) {
           sh.rL[cur][lx + m] = s.L[m];
-          sh.rTp[cur][lx + m] = tp[m];
-          sh.rTu[cur][lx + m] = tu[m];
-          sh.rTc[cur][lx + m] = tc[m];
-          if (M == 1 && need_ar) sh.rPv[cur][lx + m] = prevVal[m];  // the agent reward's L * P before the orders
-          sh.rRk[cur][lx + m] = rk[m];
+          if (need_ar) {  // the agent reward's operands: the orders' responses, L * P before them
+            sh.rTp[cur][lx + m] = tp[m];
+            sh.rTu[cur][lx + m] = tu[m];
+            sh.rTc[cur][lx + m] = tc[m];
+            if (M == 1) sh.rPv[cur][lx + m] = prevVal[m];
+          }
+          // the step's Broker responses (EnvInfo: transaction price / units /
+          // cost, risk) are stored here rather than by the finish role: a
+          // speculative step that F voids runs again under the same k, and
+          // its stores overwrite these
+          if (s.valid[m]) {
+            const size_t i = kidx(k, sNA, bA) + m;
+            if (om & O_TP) ost(ovl.tprice + i, tp[m]);
+            if (om & O_TU) ost(ovl.tunits + i, tu[m]);
+            if (om & O_TC) ost(ovl.tcost + i, tc[m]);
+            if (om & O_RISK) ost(ovl.risk + i, (uint8_t)rk[m]);
+          }
         }
         if (ls == 0) {
           sh.rCash[cur][el] = cash;
@@ -1040,17 +1066,33 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         // one-step launches, the last iteration: the finish role's done test
         // on this env's step (rec_done); an episode that ends leaves the fresh
         // Broker (Env.h:181-187).  The final ledger is written back here,
-        // while the finish role evaluates the step
+        // while the finish role evaluates the step.  The step's State (prices
+        // and ledgerNormedFull, preprocessor-independent) is stored here too,
+        // from the finish role's operands with its operations (the step of
+        // iteration 0 is never voided: no reset is pending in iteration 1), so
+        // the finish role's chain keeps only the reward, done and shaping
         if (K == 1 && j == 1 && live) {
-          if (p.auto_reset && (lflags & TR_STEP) &&
-              rec_done<M, S, ONE>(s.L, s.P, cash, sa.ml, sa.sh, sa.b, (lflags & TR_ANYMC) != 0, p)) {
+          if (lflags & TR_STEP) {
+            double curEq;
+            const bool dn = rec_done<M, S, ONE>(s.L, s.P, cash, sa.ml, sa.sh, sa.b, (lflags & TR_ANYMC) != 0, p, curEq);
+            const int ks = k - 1;  // the step's index
 #pragma unroll
             for (int m = 0; m < M; ++m) {
-              s.L[m] = 0.;
-              s.mep[m] = 0.;
-              s.Bm[m] = 0.;
+              if (s.valid[m]) {
+                if (om & O_OPR) ost(ovl.obs_price + (kidx(ks, sNF, bP) + m), s.P[m]);
+                if (om & O_OPT) ost(ovl.obs_port + (kidx(ks, sNA1, bO) + 1 + s.asset[m]), (s.L[m] * s.P[m]) / curEq);
+              }
             }
-            cash = p.init_cash;
+            if (ls == 0 && (om & O_OPT)) ost(ovl.obs_port + kidx(ks, sNA1, bO), (cash - sa.b) / curEq);
+            if (p.auto_reset && dn) {
+#pragma unroll
+              for (int m = 0; m < M; ++m) {
+                s.L[m] = 0.;
+                s.mep[m] = 0.;
+                s.Bm[m] = 0.;
+              }
+              cash = p.init_cash;
+            }
           }
           l_store();
           lstored = true;
@@ -1159,6 +1201,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     g.cos_qn = sqrt(tgt_g[0] * tgt_g[0] + canon<M, S, ONE>(qq));
   }
   const bool need_ar = (p.reward_mode != MGN_REWARD_ENV_LOG) || (om & O_AREW);
+  // one-step launches (TAIL_EXACT): the ledger role stores the step's State
+  const bool lobs = TAIL_EXACT && K == 1;
   // output element strides per step (32-bit: checked on the host) and the
   // lane's bases: per asset (k, env, asset), State.price (k, env, feature),
   // State.portfolio (k, env, 0), per env (k, env)
@@ -1286,7 +1330,16 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       const bool done = (flags & TR_ANYMC) || margin_call(q, cashv, p.mainM) || (curEq < 0.1 * p.init_cash);
       // ledgerNormedFull, agent reward, PPC, shaper (as k_step_duo's finish)
       double ar[M], portA[M];
-      const double port0 = (cashv - q.b) / curEq;
+      // lobs (one-step launches): State is stored by the ledger role; the
+      // portfolio fractions only where the PPC cosine needs them (the divisions
+      // kept in their branch: the compiler would run them beside it)
+      const bool need_pa = !lobs || p.shaper == MGN_SHAPER_PPC;
+      double port0 = 0.;
+      if (need_pa) {
+        double x = cashv - q.b;
+        asm volatile("" : "+v"(x));
+        port0 = x / curEq;
+      }
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         const double Lc = f.L[m], P = f.P[m];
@@ -1298,7 +1351,12 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           v = (v < .35) ? .35 : v;
           ar[m] = log_ratio(v);
         }
-        portA[m] = (Lc * P) / curEq;
+        portA[m] = 0.;
+        if (need_pa) {
+          double x = Lc * P;
+          asm volatile("" : "+v"(x));
+          portA[m] = x / curEq;
+        }
       }
       double cos_term = 0.;
       if (p.shaper == MGN_SHAPER_PPC) {
@@ -1439,12 +1497,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         if (f.valid[m]) {
           const size_t i = kidx(k, sNA, bA) + m;
           const int x = lx + m;
-          if (om & O_TP) ost(ov.tprice + i, sh.rTp[prv][x]);
-          if (om & O_TU) ost(ov.tunits + i, sh.rTu[prv][x]);
-          if (om & O_TC) ost(ov.tcost + i, sh.rTc[prv][x]);
-          if (om & O_RISK) ost(ov.risk + i, (uint8_t)sh.rRk[prv][x]);
-          if (!RP && (om & O_OPR)) ost(ov.obs_price + (kidx(k, sNF, bP) + m), f.P[m]);
-          if (om & O_OPT) ost(ov.obs_port + (kidx(k, sNA1, bO) + 1 + f.asset[m]), portA[m]);
+          if (!RP && !lobs && (om & O_OPR)) ost(ov.obs_price + (kidx(k, sNF, bP) + m), f.P[m]);
+          if (!lobs && (om & O_OPT)) ost(ov.obs_port + (kidx(k, sNA1, bO) + 1 + f.asset[m]), portA[m]);
           if (D != 1) {
             if (om & O_AREW) ost(ov.agent_reward + i, ar[m]);
             if (om & O_SHP) ost(ov.shaped + i, shaped_v);
@@ -1456,7 +1510,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #ifndef MGN_ABL_NOSTORE_ENV
       if (ls == 0) {
         const size_t ie = kidx(k, sN, (size_t)env);
-        if (om & O_OPT) ost(ov.obs_port + kidx(k, sNA1, bO), port0);
+        if (!lobs && (om & O_OPT)) ost(ov.obs_port + kidx(k, sNA1, bO), port0);
         if (om & O_DONE) ost(ov.done + ie, (uint8_t)(done ? 1 : 0));
         if (om & O_MC) {
           // TR_MCALL: orders ran (in_kind != NONE); the check on the sums after them

@@ -36,9 +36,8 @@ CASES = [
     # agent loop's instantiations, the C3 headline among them (S = 8, GK = TrendOU)
     # (the multi-step instantiations: ONE = K1 = false, the name's last two flags)
     ("mgn_launch_a8t.hip", r"k_step_trioILi8ELb[01]ELb1ELj(4093|16383)E.*ELb0ELb0EEEv", 0, "C3 headline"),
-    # the one-step instantiations (K1): a few spills in the generator's
-    # last iteration (the reset tick beside the state write-back)
-    ("mgn_launch_a8t.hip", r"k_step_trioILi8ELb[01]ELb1ELj(4093|16383)E.*ELb0ELb1EEEv", 8, "C3 one-step launches"),
+    # the one-step instantiations (K1), their own unit
+    ("mgn_launch_a8k1.hip", r"k_step_trioILi8ELb[01]ELb1ELj(4093|16383)E.*ELb0ELb1EEEv", 0, "C3 one-step launches"),
     # the two-slot layout's window instantiations (C5's): 48 -> 2 in round 4
     ("mgn_launch_a16m2.hip", r"k_step_trio", 2, "two slots per lane"),
     # the single-role kernel's 4 and 8 slots per lane (32 / 64 assets)

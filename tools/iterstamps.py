@@ -1,5 +1,6 @@
 """Per-iteration timeline of the three-role kernel (diagnostic build -DMGN_ITERSTAMP).
 
+    MGN_VARIANT_UNITS=8t,8k1 python tools/build_variant.py iter -DMGN_ITERSTAMP
     MADIGAN_LIB_PATH=tools/_var/iter/libmadigan_hip.so python tools/iterstamps.py [FUSE] [LAUNCHES]
 
 Runs the driver's C3 shape (a 5-step warm launch, then FUSE-step launches),
@@ -30,7 +31,8 @@ def main():
               "tcost", "risk", "margin_call"]
     out = env.alloc_traj(fuse, fields=fields)
     acts = env.generate_actions(5 + fuse * launches, seed=0x6D6164)
-    fn = env.lib.mgn_diag_iter
+    # (one-step launches run in mgn_launch_a8k1.hip, with its own stamp buffer)
+    fn = env.lib.mgn_diag_iter_k1 if fuse == 1 else env.lib.mgn_diag_iter
     fn.argtypes = [C.POINTER(C.c_ulonglong)]
     buf = (C.c_ulonglong * (256 * 64))()
     w5 = env.alloc_traj(5, fields=fields)

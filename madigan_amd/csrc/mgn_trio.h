@@ -918,6 +918,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #ifdef MGN_STAMPS
       Lp1 = Lp2 = Lp3 = T0;
 #endif
+      // one-step launches: in the last iteration the finish role's chain is
+      // the critical path, this role's work (done test, State, write-back) not
+      if (TAIL_EXACT && K == 1 && j == 1) __builtin_amdgcn_s_setprio(kPrioG);
       const bool rst = live && j > 0 && sh.reset[prv][el] != 0;
       const bool prev_step = j > 0 && (sh.rFlags[prv][el] & TR_STEP) != 0;
       // WIN: this iteration's tick refills the window (the reset tick or one
@@ -961,13 +964,14 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         Sums s0;
         if (after_reset && j > 0) {
           s0 = port_sums<M, S, ONE>(s.L, s.mep, s.Bm, s.P);  // after a reset tick
+        } else if (j == 0) {
+          s0 = sa;  // the prologue's sums of the handle's state and prices
         } else {
           double tlp[M];
 #pragma unroll
           for (int m = 0; m < M; ++m) tlp[m] = s.L[m] * s.P[m];
           s0 = sa;
           s0.lp = canon<M, S, ONE>(tlp);
-          if (j == 0) s0 = port_sums<M, S, ONE>(s.L, s.mep, s.Bm, s.P);
         }
         const double prevEq = (cash + s0.lp) - s0.b;  // Env.h:208
 #ifdef MGN_STAMPS
@@ -1297,6 +1301,26 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       }
     }
   };
+  // the finish role's state write-back (the n-step ring's in the epilogue)
+  bool fstored = false;
+  const auto f_store = [&]() {
+    if (ls == 0) {
+      if (WIN) {
+        p.rhead[env] = rhead;
+        p.rlen[env] = rlen;
+      }
+      p.ep[(size_t)env * 2] = ep_ret;
+      p.ep[(size_t)env * 2 + 1] = ep_len;
+      if (D == 1) {
+        p.sA[env] = g.shA;
+        p.sB[env] = g.shB;
+      }
+    }
+    if (D != 1 && s.valid[0]) {
+      p.sA[(size_t)env * A + s.asset[0]] = g.shA;
+      p.sB[(size_t)env * A + s.asset[0]] = g.shB;
+    }
+  };
   drain_vmem();
   __builtin_amdgcn_s_setprio(kPrioF);
 #ifdef MGN_STAMPS
@@ -1582,6 +1606,14 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       for (int m = 0; m < M; ++m) pa[m] = (Lf[m] * Pf[m]) / eq;
       push_row(Pf, pa, (cashf - bf) / eq, (uint64_t)sh.ts[prv][el], klast, prv);
     }
+    if constexpr (TAIL_EXACT) {
+      // one-step launches: the last iteration -- the state write-back issued
+      // before its barrier (it no longer changes)
+      if (K == 1 && j == 1 && live) {
+        f_store();
+        fstored = true;
+      }
+    }
     if (ls == 0) sh.reset[cur][el] = rst_out;
     if constexpr (NPF) {
       // the buffer after this iteration's pops, for the generator's prefix
@@ -1624,22 +1656,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       p.nhead[env] = nhead;
     }
   }
-  if (ls == 0) {
-    if (WIN) {
-      p.rhead[env] = rhead;
-      p.rlen[env] = rlen;
-    }
-    p.ep[(size_t)env * 2] = ep_ret;
-    p.ep[(size_t)env * 2 + 1] = ep_len;
-    if (D == 1) {
-      p.sA[env] = g.shA;
-      p.sB[env] = g.shB;
-    }
-  }
-  if (D != 1 && s.valid[0]) {
-    p.sA[(size_t)env * A + s.asset[0]] = g.shA;
-    p.sB[(size_t)env * A + s.asset[0]] = g.shB;
-  }
+  if (!fstored) f_store();
   MGN_IT_DRAIN();
   MGN_IT(46, 2 * TRIO_W);
 }

@@ -921,8 +921,20 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       // one-step launches: in the last iteration the finish role's chain is
       // the critical path, this role's work (done test, State, write-back) not
       if (TAIL_EXACT && K == 1 && j == 1) __builtin_amdgcn_s_setprio(kPrioG);
-      const bool rst = live && j > 0 && sh.reset[prv][el] != 0;
-      const bool prev_step = j > 0 && (sh.rFlags[prv][el] & TR_STEP) != 0;
+      // the previous iteration's records -- reset, flags, the tick's prices
+      // and their reciprocals -- read together ahead of the tests on them (a
+      // compiler-only memory barrier keeps them from being sunk into the
+      // branches; iteration 0 reads records no role wrote, and uses none)
+      const int rs_rec = sh.reset[prv][el], fl_rec = sh.rFlags[prv][el];
+      double p_rec[M], r_rec[M];
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        p_rec[m] = sh.price[prv][lx + m];
+        r_rec[m] = DISC ? sh.prcp[prv][lx + m] : 0.;
+      }
+      asm volatile("" ::: "memory");
+      const bool rst = live && j > 0 && rs_rec != 0;
+      const bool prev_step = j > 0 && (fl_rec & TR_STEP) != 0;
       // WIN: this iteration's tick refills the window (the reset tick or one
       // of the W - 1 after it): no step
       const bool refill = WIN && live && (rst || lpend > 0);
@@ -931,7 +943,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       // the handle's current prices)
 #pragma unroll
       for (int m = 0; m < M; ++m)
-        if (j > 0 && live && s.valid[m]) s.P[m] = sh.price[prv][lx + m];
+        if (j > 0 && live && s.valid[m]) s.P[m] = p_rec[m];
       if (rst) {
         // the episode ended at the step F evaluated: the speculative step of
         // iteration j-1 is void; a fresh Broker (Env.h:181-187) waits for the
@@ -998,7 +1010,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
             if (s.valid[m]) {
               // (unit_size avM) / P with the generator's reciprocal of P
               // (iteration 0 reads the handle's prices, not the generator's: no reciprocal)
-              const double u = div_by_rcp(p.unit_size * avM, s.P[m], j > 0 ? sh.prcp[prv][lx + m] : 0.);
+              const double u = div_by_rcp(p.unit_size * avM, s.P[m], j > 0 ? r_rec[m] : 0.);
               uc[m] = (double)(act_now[m] - half) * u;
               if (act_now[m] == 0) uc[m] = (s.L[m] != 0) ? -s.L[m] : 0.;
             }
@@ -1333,20 +1345,35 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     bool tail_rst = false;  // TAIL: the launch's last step ended its episode
     // the step L ran in iteration j-1, unless F voided it at iteration j-1
     const int flags = j > 0 ? sh.rFlags[prv][el] : 0;
+    // the step's records are read with its flags, ahead of the tests on them
+    // (one LDS round trip on this role's chain instead of three; iteration 0
+    // reads records no role wrote, and uses none)
+    const int rsv = j > 0 ? sh.reset[prv][el] : 0;
+    const int krec = sh.rK[prv][el];
+    double Lrec[M], Prec[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      Lrec[m] = sh.rL[prv][lx + m];
+      Prec[m] = sh.price[prv][lx + m];
+    }
+    const double cashrec = sh.rCash[prv][el], prevrec = sh.rPrevEq[prv][el];
+    // (a compiler-only memory barrier: the reads stay ahead of the tests --
+    // the compiler would sink them into the branch -- and nothing waits here)
+    asm volatile("" ::: "memory");
 #ifdef MGN_TRIO_ABL_F  // diagnostic timing build: no step finish, no outputs
     if (false) {
 #else
-    if (live && (flags & TR_STEP) && !sh.reset[prv][el]) {
+    if (live && (flags & TR_STEP) && !rsv) {
 #endif
-      const int k = sh.rK[prv][el];
+      const int k = krec;
       Lane<M> f = s;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        f.L[m] = sh.rL[prv][lx + m];
-        f.P[m] = sh.price[prv][lx + m];
+        f.L[m] = Lrec[m];
+        f.P[m] = Prec[m];
       }
-      const double cashv = sh.rCash[prv][el];
-      const double prevEq = sh.rPrevEq[prv][el];
+      const double cashv = cashrec;
+      const double prevEq = prevrec;
       // post-tick sums, equity, reward, done (Env.h:211-223)
       Sums q;
       {

@@ -431,10 +431,22 @@ def main():
             k += n
         return seq
 
-    def run(seq):
+    # every step-kernel launch in issue order, (label, steps per launch,
+    # launches): tools/reconcile.py matches a kernel trace of this command to
+    # the line's figures launch by launch
+    launch_log = []
+
+    def logl(label, K, n):
+        if launch_log and launch_log[-1][0] == label and launch_log[-1][1] == K:
+            launch_log[-1][2] += n
+        else:
+            launch_log.append([label, K, n])
+
+    def run(seq, label):
         rc = 0
-        for fn, k, _ in seq:
+        for fn, k, n in seq:
             rc |= fn(k)
+            logl(label, n, 1)
         return rc
 
     warm, timed = plan(0, args.warmup), plan(args.warmup, total)
@@ -443,14 +455,14 @@ def main():
     # stream (mgn_set_timing; pooled events, created during the warmup)
     tmode = 2 if args.timing == "launch" else 1
     L.check(lib.mgn_set_timing(h, tmode), h)
-    L.check(run(warm), h)
+    L.check(run(warm, "warmup"), h)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     L.check(lib.mgn_set_timing(h, tmode), h)
     t0 = time.perf_counter()
-    rc = run(timed)
+    rc = run(timed, "timed")
     # the closing wait is on the handle's stream, the only one the steps use
     # (a device-wide synchronize costs ~3 us more on an idle device)
     rc |= sync()
@@ -497,9 +509,10 @@ def main():
     sw_actions = env.generate_actions(T_ACT, seed=0x6D6165) if rank == 0 and args.k_sweep else None
     sw_at = [0]
 
-    def sw_launches(fn, K, n):
+    def sw_launches(fn, K, n, label):
         """n K-step launches of `fn` (bound to sw_actions), fresh rows each."""
         rc = 0
+        logl(label, K, n)
         for _ in range(n):
             if sw_at[0] + K > T_ACT:
                 sw_at[0] = 0
@@ -507,11 +520,11 @@ def main():
             sw_at[0] += K
         return rc
 
-    def kernel_launch_us(fn, K, n):
+    def kernel_launch_us(fn, K, n, label):
         """The step kernel's own duration (HIP events recorded by the launch)
         averaged over n launches."""
         L.check(lib.mgn_set_timing(h, 2), h)
-        L.check(sw_launches(fn, K, n), h)
+        L.check(sw_launches(fn, K, n, label), h)
         torch.cuda.synchronize()
         tk = (C.c_double * 4)()
         L.check(lib.mgn_get_timing(h, tk), h)
@@ -530,7 +543,7 @@ def main():
         nonlocal age
         while age < target:
             n = min(256, target - age)
-            L.check(sw_launches(sw_fn(n), n, 1), h)
+            L.check(sw_launches(sw_fn(n), n, 1, "advance"), h)
             age += n
         torch.cuda.synchronize()
 
@@ -542,7 +555,7 @@ def main():
         nonlocal age
         advance_to(target)
         Kh = int(round(steps_per_launch))
-        us = kernel_launch_us(sw_fn(Kh), Kh, n)
+        us = kernel_launch_us(sw_fn(Kh), Kh, n, f"age_{target}")
         a0 = age
         age += Kh * n
         ep = int(env.episode_stats[:, 3].sum().item())
@@ -568,13 +581,13 @@ def main():
         for K in ((1, 16, 64, 256) if args.sweep else (1, 16, 256)):
             reps = max(4, 512 // K)
             fn = sw_fn(K)
-            L.check(sw_launches(fn, K, 1), h)  # warm
+            L.check(sw_launches(fn, K, 1, f"sweep_{K}_warm"), h)  # warm
             torch.cuda.synchronize()
             a0 = age + K
-            launch_us = kernel_launch_us(fn, K, reps)
+            launch_us = kernel_launch_us(fn, K, reps, f"sweep_{K}")
             s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s_ev.record(stream)
-            L.check(sw_launches(fn, K, reps), h)
+            L.check(sw_launches(fn, K, reps, f"sweep_{K}_back_to_back"), h)
             e_ev.record(stream)
             torch.cuda.synchronize()
             age += K * (1 + 2 * reps)
@@ -664,6 +677,7 @@ def main():
                 "the headline's launch on the same handle after the timed region, at the handle's step "
                 "index age_steps (fresh actions): kernel time from the launch's own HIP events; the "
                 "steady-state figure is the one after >= 2000 untimed steps (episodes ended)")
+        res["launch_log"] = launch_log
         if sweep:
             res["launch_lengths"] = sweep
             res["launch_lengths_note"] = (

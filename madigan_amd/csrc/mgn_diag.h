@@ -58,7 +58,10 @@ __device__ unsigned long long g_duo_wall[2048 * 32];
 // lane 0 after its epilogue stores (with their completion wait); [47] G lane 0
 // once the kernel arguments arrived, [48] G lane 0 once its iteration-0 tick
 // is published to LDS, [49] L lane 0 once its iteration-0 records are
-// published, [50] F lane 0 once its iteration-1 outputs are issued
+// published, [50] F lane 0 once its iteration-1 outputs are issued; [51] L
+// state loaded, [52] / [53] L's orders start / done (iteration 0), [54] G
+// state loaded, [55] / [56] / [57] F's iteration-1 sums / reward / shaping
+// done, [58] L's prevEq formed (iteration 0)
 __device__ unsigned long long g_iter[256 * 64];
 #define MGN_IT(slot, lane0)                                             \
   if (threadIdx.x == (lane0) && blockIdx.x < 256 && (slot) < 64)        \

@@ -986,6 +986,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           s0.lp = canon<M, S, ONE>(tlp);
         }
         const double prevEq = (cash + s0.lp) - s0.b;  // Env.h:208
+        if (j == 0) MGN_IT(58, TRIO_W);
 #ifdef MGN_STAMPS
         Lp1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1382,6 +1383,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         for (int m = 0; m < M; ++m) tlp[m] = f.L[m] * f.P[m];
         q.lp = canon<M, S, ONE>(tlp);
       }
+      if (j == 1) MGN_IT(55, 2 * TRIO_W);
       q.ml = sh.rMl[prv][el];
       q.sh = sh.rSh[prv][el];
       q.b = sh.rB[prv][el];
@@ -1389,6 +1391,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       const double ratio = curEq / prevEq;
       const double clampv = (in_kind == IN_SINGLE) ? 0.01 : 0.3;
       const double reward = log_ratio((ratio < clampv) ? clampv : ratio);
+      if (j == 1) MGN_IT(56, 2 * TRIO_W);
       const bool done = (flags & TR_ANYMC) || margin_call(q, cashv, p.mainM) || (curEq < 0.1 * p.init_cash);
       // ledgerNormedFull, agent reward, PPC, shaper (as k_step_duo's finish)
       double ar[M], portA[M];
@@ -1552,6 +1555,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       } else {
         shaped_v = f.valid[0] ? shape(p.shaper, ar[0], g.shA, g.shB, p.eta, cos_term, p.sexp) : 0.;  // M = 1
       }
+      if (j == 1) MGN_IT(57, 2 * TRIO_W);
       // outputs of step k (the speculative runs never reach F)
 #ifndef MGN_ABL_NOSTORE_ASSET
 #pragma unroll

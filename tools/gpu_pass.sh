@@ -24,8 +24,10 @@ line() {  # name, args...
   python tools/bench_brief.py $O/$n.json
   if [ -n "$TRACE" ]; then
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_$n -o kt -- python3 bench.py "$@" \
-      > $O/kt_$n.log 2>&1 || { echo "$n trace failed"; tail -20 $O/kt_$n.log; exit 1; }
+      > $O/kt_$n.json 2> $O/kt_$n.log || { echo "$n trace failed"; tail -20 $O/kt_$n.log; exit 1; }
     python tools/kt_brief.py $O/kt_$n
+    python tools/bench_brief.py $O/kt_$n.json
+    if grep -q launch_log $O/kt_$n.json; then python tools/reconcile.py $O/kt_$n.json $O/kt_$n --out $O/reconcile_$n.json; fi
   fi
 }
 if [ -n "$DRV" ]; then

@@ -69,9 +69,11 @@ def main():
            # iteration-1 barrier, each role's epilogue
            "timeline_from_entry": {n: med(rel[:, :, i]) for n, i in (
                ("kernargs", 47), ("prologue_barrier", 1), ("g_state_loaded", 54),
-               ("l_state_loaded", 51), ("l_orders_start_it0", 52), ("l_orders_done_it0", 53),
+               ("l_state_loaded", 51), ("l_prev_eq_it0", 58), ("l_orders_start_it0", 52),
+               ("l_orders_done_it0", 53),
                ("g_tick_done_it0", 48),
-               ("l_records_done_it0", 49), ("barrier_it0", 2), ("f_outputs_issued_it1", 50),
+               ("l_records_done_it0", 49), ("barrier_it0", 2), ("f_sums_it1", 55), ("f_reward_it1", 56),
+               ("f_shaped_it1", 57), ("f_outputs_issued_it1", 50),
                ("barrier_it1", 3), ("g_epilogue", 44), ("l_epilogue", 45), ("f_epilogue", 46))},
            "block_entry_spread_cycles": med(st[:, :, 0].max(1) - st[:, :, 0].min(1))}
     print(json.dumps(res, indent=1))

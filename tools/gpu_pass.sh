@@ -27,7 +27,10 @@ line() {  # name, args...
       > $O/kt_$n.json 2> $O/kt_$n.log || { echo "$n trace failed"; tail -20 $O/kt_$n.log; exit 1; }
     python tools/kt_brief.py $O/kt_$n
     python tools/bench_brief.py $O/kt_$n.json
-    if grep -q launch_log $O/kt_$n.json; then python tools/reconcile.py $O/kt_$n.json $O/kt_$n --out $O/reconcile_$n.json; fi
+    # the un-profiled line against the trace (profiled launch events read longer)
+    if grep -q launch_log $O/kt_$n.json; then
+      python tools/reconcile.py $O/$n.json $O/kt_$n --trace-line $O/kt_$n.json --out $O/reconcile_$n.json
+    fi
   fi
 }
 if [ -n "$DRV" ]; then

@@ -1,15 +1,20 @@
 """Reconcile a bench.py line with a rocprofv3 kernel trace of the same command.
 
-    rocprofv3 --kernel-trace --stats --output-format csv -d DIR -o kt -- python3 bench.py ARGS > line.json
-    python tools/reconcile.py line.json DIR [--out profiles/rNN_reconcile.json]
+    python bench.py ARGS > line.json                      # the un-profiled line
+    rocprofv3 --kernel-trace --stats --output-format csv -d DIR -o kt -- python3 bench.py ARGS > kt.json
+    python tools/reconcile.py line.json DIR [--trace-line kt.json] [--out profiles/rNN_reconcile.json]
 
 The line's `launch_log` lists every step-kernel launch in issue order (label,
 steps per launch, launches); the trace's step-kernel dispatches, sorted by
-start time, are assigned to those entries in that order.  For each figure the
-line reports from the launches' own HIP events -- the timed region's launch
+start time, are assigned to those entries in that order (the traced run's
+log, --trace-line, must hold the same entries).  For each figure the line
+reports from the launches' own HIP events -- the timed region's launch
 (roofline.avg_launch_us), the episode-age launches (episode_age, the steady
 state among them), the launch-length sweep (launch_lengths) -- the trace's
-mean and median over the same dispatches and their ratio to the line's figure.
+mean and median over the same dispatches and their ratio to the line's
+figure.  (Under the profiler the launch events themselves read longer -- about
+4 us per launch on this box -- so the line to compare is the un-profiled one;
+the traced run's own figures are reported beside it as `profiled_line_us`.)
 """
 import csv
 import glob
@@ -30,8 +35,13 @@ def dispatches(d):
 
 def main():
     line = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+    tline = line
+    if "--trace-line" in sys.argv:
+        tline = json.loads(open(sys.argv[sys.argv.index("--trace-line") + 1]).read().strip().splitlines()[-1])
+        if [e[:2] for e in tline["launch_log"]] != [e[:2] for e in line["launch_log"]]:
+            sys.exit("the traced run's launch log differs from the line's")
     disp = dispatches(sys.argv[2])
-    log = line["launch_log"]
+    log = tline["launch_log"]
     need = sum(n for _, _, n in log)
     if len(disp) != need:
         sys.exit(f"trace holds {len(disp)} step dispatches, the launch log {need}")
@@ -42,18 +52,21 @@ def main():
         i += n
     res = {"line": sys.argv[1], "trace": sys.argv[2], "figures": {}}
 
-    def fig(name, label, line_us):
+    def fig(name, label, get):
         us = groups[label]["us"]
         mean, med = statistics.fmean(us), statistics.median(us)
+        line_us = get(line)
         res["figures"][name] = {"launches": len(us), "steps_per_launch": groups[label]["steps_per_launch"],
                                 "line_us": line_us, "trace_mean_us": mean, "trace_median_us": med,
-                                "trace_over_line": mean / line_us}
+                                "trace_over_line": mean / line_us, "profiled_line_us": get(tline)}
 
-    fig("timed_region_launch", "timed", line["roofline"]["avg_launch_us"])
-    for age, a in line.get("episode_age", {}).items():
-        fig(f"episode_age_{age}", f"age_{age}", a["kernel_us_per_launch"])
-    for K, s in line.get("launch_lengths", {}).items():
-        fig(f"launch_length_{K}", f"sweep_{K}", s["kernel_us_per_launch"])
+    fig("timed_region_launch", "timed", lambda d: d["roofline"]["avg_launch_us"])
+    for age in line.get("episode_age", {}):
+        key = age if age in tline.get("episode_age", {}) else None
+        if key:
+            fig(f"episode_age_{age}", f"age_{age}", lambda d, a=age: d["episode_age"][a]["kernel_us_per_launch"])
+    for K in line.get("launch_lengths", {}):
+        fig(f"launch_length_{K}", f"sweep_{K}", lambda d, k=K: d["launch_lengths"][k]["kernel_us_per_launch"])
     res["within_3pct"] = all(abs(f["trace_over_line"] - 1) <= 0.03 for f in res["figures"].values())
     res["kernels"] = sorted({k for _, k in disp})
     out = json.dumps(res, indent=1)

@@ -1142,35 +1142,6 @@ __device__ __forceinline__ double ddr_one_pre(double r, double A, double B, cons
   const double num = pos ? h : (B * h - (A * (r * r)) / 2);
   return rt_div(num, pos ? q.dpos : q.dneg);
 }
-// ddr_one_pre with the reciprocals of both denominators formed ahead, as
-// rt_div forms them (one-step launches: the finish role forms them while it
-// waits for the step) -- the same operations on the same operands
-struct DdrPreR {
-  DdrPre q;
-  double rpos, rneg;
-};
-__device__ __forceinline__ double rt_rcp(double b) {
-  double r = __builtin_amdgcn_rcp(b);
-  r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
-  return __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
-}
-__device__ __forceinline__ DdrPreR ddr_pre_r(double A, double B) {
-  const DdrPre q = ddr_pre(A, B);
-  return DdrPreR{q, rt_rcp(q.dpos), rt_rcp(q.dneg)};
-}
-__device__ __forceinline__ double ddr_one_r(double r, double A, double B, const DdrPreR& c) {
-  const double h = r - c.q.hA;
-  const bool pos = r > 0.;
-  const double num = pos ? h : (B * h - (A * (r * r)) / 2);
-  const double den = pos ? c.q.dpos : c.q.dneg;
-  double out = num * (pos ? c.rpos : c.rneg);
-  if (!__builtin_amdgcn_class(den, kNormalClass)) {  // (rt_div's IEEE case, kept in its branch)
-    double a = num;
-    asm volatile("" : "+v"(a));
-    out = a / den;
-  }
-  return out;
-}
 __device__ __forceinline__ double clip1(double v) { return v < -1. ? -1. : (v > 1. ? 1. : v); }
 // dsr_one with its reward-independent denominator evaluated once per pop (the
 // same operations on the same operands)

@@ -161,9 +161,8 @@ constexpr double TWO_M32 = 2.3283064365386962890625e-10;
 // the IEEE sequence's 11), sqrt x from v_rsq_f64 with one Goldschmidt
 // refinement (<= 1 ulp; 8 VALU instead of 17).  Operands outside the normal
 // class (zero, denormal, inf, NaN, negative square-root arguments) take the
-// IEEE operation.  The reward ratio curEq / prevEq stays IEEE (div_by_rcp
-// below): a small log reward would carry its last-bit error at a large
-// relative size.  Every step
+// IEEE operation.  The reward ratio curEq / prevEq stays IEEE: a small log
+// reward would carry its last-bit error at a large relative size.  Every step
 // kernel uses these helpers, so the schedules stay bit-identical.
 constexpr int kNormalClass = (1 << 3) | (1 << 8);  // v_cmp_class: -normal | +normal
 
@@ -175,11 +174,9 @@ constexpr int kNormalClass = (1 << 3) | (1 << 8);  // v_cmp_class: -normal | +no
 // v_div_fmas is a plain fma and v_div_fixup the identity.  rcp_refined(y) is
 // that reciprocal for |y| in [2^-150, 2^150] (0 outside); div_by_rcp(x, y, r)
 // finishes the quotient with the sequence's last three operations for |x| in
-// [2^-600, 2^600] (x = +-0: x r, the signed zero) and falls back to the
-// division elsewhere: the IEEE quotient, bit for bit.  (The three-role
-// kernel's generator forms the reciprocal of each price it publishes, off the
-// ledger's chain; its finish role the reciprocal of each equity it forms, for
-// the portfolio fractions and the next step's reward ratio.)
+// [2^-600, 2^600] and falls back to the division elsewhere: the IEEE
+// quotient, bit for bit.  (The three-role kernel's generator forms the
+// reciprocal of each price it publishes, off the ledger's chain.)
 __device__ __forceinline__ double rcp_refined(double y) {
   const double ay = fabs(y);
   if (!(ay >= 0x1p-150 && ay <= 0x1p150)) return 0.;
@@ -189,10 +186,9 @@ __device__ __forceinline__ double rcp_refined(double y) {
 }
 __device__ __forceinline__ double div_by_rcp(double x, double y, double r) {
   const double ax = fabs(x);
-  // (x = +-0: the quotient is x r, the IEEE signed zero)
-  const bool fast = r != 0. && (ax == 0. || (ax >= 0x1p-600 && ax <= 0x1p600));
+  const bool fast = r != 0. && ax >= 0x1p-600 && ax <= 0x1p600;
   double q = x * r;
-  if (ax != 0.) q = __builtin_fma(__builtin_fma(-y, q, x), r, q);
+  q = __builtin_fma(__builtin_fma(-y, q, x), r, q);
   if (!fast) {
     // (the empty volatile asm keeps the division in its branch: speculated,
     // as the compiler otherwise does with a lone fdiv, every lane would run

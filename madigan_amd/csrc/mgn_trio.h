@@ -1231,31 +1231,6 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   const bool need_ar = (p.reward_mode != MGN_REWARD_ENV_LOG) || (om & O_AREW);
   // one-step launches (TAIL_EXACT): the ledger role stores the step's State
   const bool lobs = TAIL_EXACT && K == 1;
-  // the equity of the last step evaluated and its refined reciprocal: the next
-  // step's reward ratio curEq / prevEq divides by it (prevEq is the ledger's
-  // equity before the orders, bit for bit the finish role's curEq of the step
-  // before, and rcp_refined / div_by_rcp give the IEEE quotient).  One-step
-  // launches form it in the prologue from the handle's state, as the ledger
-  // forms prevEq (port_sums), and the DDR shaper's reward-independent terms
-  // with their reciprocals, while the finish role waits for the step
-  double eq_last = 0., rcp_last = 0.;
-  DdrPreR dpr{};
-  if constexpr (TAIL_EXACT) {
-    if (live && K == 1) {
-      double Lp[M], mp[M], Bp[M], Pp[M];
-#pragma unroll
-      for (int m = 0; m < M; ++m) {
-        Lp[m] = s.valid[m] ? kL[li + m] : 0.;
-        mp[m] = s.valid[m] ? kmep[li + m] : 0.;
-        Bp[m] = s.valid[m] ? kBm[li + m] : 0.;
-        Pp[m] = s.valid[m] ? kP[li + m] : 0.;
-      }
-      const Sums s0 = port_sums<M, S, ONE>(Lp, mp, Bp, Pp);
-      eq_last = (kcash[envc] + s0.lp) - s0.b;
-      rcp_last = rcp_refined(eq_last);
-      if (p.shaper == MGN_SHAPER_DDR && D == 1) dpr = ddr_pre_r(g.shA, g.shB);
-    }
-  }
   // output element strides per step (32-bit: checked on the host) and the
   // lane's bases: per asset (k, env, asset), State.price (k, env, feature),
   // State.portfolio (k, env, 0), per env (k, env)
@@ -1413,10 +1388,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       q.sh = sh.rSh[prv][el];
       q.b = sh.rB[prv][el];
       const double curEq = (cashv + q.lp) - q.b;
-      const double ratio =
-          div_by_rcp(curEq, prevEq, __double_as_longlong(prevEq) == __double_as_longlong(eq_last) ? rcp_last : 0.);
-      eq_last = curEq;
-      rcp_last = rcp_refined(curEq);
+      const double ratio = curEq / prevEq;
       const double clampv = (in_kind == IN_SINGLE) ? 0.01 : 0.3;
       const double reward = log_ratio((ratio < clampv) ? clampv : ratio);
       if (j == 1) MGN_IT(56, 2 * TRIO_W);
@@ -1428,7 +1400,11 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       // kept in their branch: the compiler would run them beside it)
       const bool need_pa = !lobs || p.shaper == MGN_SHAPER_PPC;
       double port0 = 0.;
-      if (need_pa) port0 = div_by_rcp(cashv - q.b, curEq, rcp_last);
+      if (need_pa) {
+        double x = cashv - q.b;
+        asm volatile("" : "+v"(x));
+        port0 = x / curEq;
+      }
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         const double Lc = f.L[m], P = f.P[m];
@@ -1440,7 +1416,12 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           v = (v < .35) ? .35 : v;
           ar[m] = log_ratio(v);
         }
-        portA[m] = need_pa ? div_by_rcp(Lc * P, curEq, rcp_last) : 0.;
+        portA[m] = 0.;
+        if (need_pa) {
+          double x = Lc * P;
+          asm volatile("" : "+v"(x));
+          portA[m] = x / curEq;
+        }
       }
       double cos_term = 0.;
       if (p.shaper == MGN_SHAPER_PPC) {
@@ -1563,10 +1544,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S, ONE>(ar) : reward;
         if (p.shaper == MGN_SHAPER_DDR) {  // shape() for DDR (nstep_buffer.py:128-162)
           const double r = rin_s;
-          if (lobs)  // (the terms formed in the prologue)
-            shaped_s = clip1((0.0 + 1.0 * ddr_one_r(r, g.shA, g.shB, dpr)) / 1);
-          else
-            shaped_s = clip1((0.0 + 1.0 * ddr_one_pre(r, g.shA, g.shB, ddr_pre(g.shA, g.shB))) / 1);
+          shaped_s = clip1((0.0 + 1.0 * ddr_one_pre(r, g.shA, g.shB, ddr_pre(g.shA, g.shB))) / 1);
           double m = r < 0. ? r : 0.;
           if (r != r) m = r;
           g.shA += p.eta * (r - g.shA);

@@ -344,13 +344,6 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   // only for the envs that end (not as a candidate for every env), and both
   // write their final state back during that iteration instead of after it
   constexpr bool TAIL_EXACT = TAIL && !GSLOT;
-  // GOBS (multi-step launches, a kind-specialized generator role without a
-  // window or a tape): the State of the step the finish role evaluates --
-  // prices, ledgerNormedFull, timestamp -- is stored by the generator role,
-  // whose work the step's time hides (it issues at the lowest priority into
-  // the other roles' stalls), from the same records with the finish role's
-  // operations; the finish role keeps the reward, done and shaping chain
-  constexpr bool GOBS = GK >= 0 && !GSLOT && !RP && !WIN && M == 1 && !TAIL;
   const int el = (GSLOT && role == 0) ? l % EPB : l / S;
   const int ls = (GSLOT && role == 0) ? l / EPB : l % S;
   const int lx = (el * S + ls) * M;  // the lane's first (env, asset) slot record index
@@ -646,23 +639,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         p.dskip[env] = s.dskip;
       }
     };
-    // GOBS: the State outputs' pointers and bases (as the finish role's)
-    const uint32_t om_g = OMC ? OMC : traj_mask(out);
-    MGN_G double* const gop = GOBS && (om_g & O_OPR) ? vptr(out.obs_price) : nullptr;
-    MGN_G double* const gopt = GOBS && (om_g & O_OPT) ? vptr(out.obs_port) : nullptr;
-    MGN_G uint64_t* const gots = GOBS && (om_g & O_TS) ? vptr(out.timestamp) : nullptr;
     for (int j = 0;; ++j) {
       const int cur = j & 1, prv = cur ^ 1;
       MGN_T(T0);
-      // GOBS: the State the previous iteration published (the step the
-      // finish role evaluates in this one)
-      double Pprev[GOBS ? M : 1];
-      uint64_t tsprev = 0;
-      if constexpr (GOBS) {
-#pragma unroll
-        for (int m = 0; m < M; ++m) Pprev[m] = s.P[m];
-        tsprev = ts;
-      }
       if (threadIdx.x == 0) sh.more[(j + 1) % 3] = 0;
       if (live) {
         if constexpr (TAIL) {
@@ -832,34 +811,6 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         }
       }
       if (ls == 0) sh.ts[cur][el] = ts;
-      if constexpr (GOBS) {
-        // the finish role's test of the step it evaluates in this iteration
-        // (the ledger's step of the previous one, unless a reset voids it)
-        if (live && j > 0 && (sh.rFlags[prv][el] & TR_STEP) && !sh.reset[prv][el]) {
-          const int kk = sh.rK[prv][el];
-          double Lr[M], tlp[M];
-#pragma unroll
-          for (int m = 0; m < M; ++m) {
-            Lr[m] = sh.rL[prv][lx + m];
-            tlp[m] = Lr[m] * Pprev[m];
-          }
-          const double cashv = sh.rCash[prv][el], bv = sh.rB[prv][el];
-          const double curEq = (cashv + canon<M, S, ONE>(tlp)) - bv;  // Env.h:211, the finish role's
-          const uint32_t sNF = (uint32_t)p.N * (uint32_t)p.F, sNA1 = (uint32_t)p.N * (uint32_t)(A + 1);
-          const size_t bP = (size_t)env * p.F + s.asset[0], bO = (size_t)env * (A + 1);
-#pragma unroll
-          for (int m = 0; m < M; ++m) {
-            if (s.valid[m]) {
-              if (gop) ost(gop + (kidx(kk, sNF, bP) + m), Pprev[m]);
-              if (gopt) ost(gopt + (kidx(kk, sNA1, bO) + 1 + s.asset[m]), (Lr[m] * Pprev[m]) / curEq);
-            }
-          }
-          if (ls == 0) {
-            if (gopt) ost(gopt + kidx(kk, sNA1, bO), (cashv - bv) / curEq);
-            if (gots) ost(gots + kidx(kk, (uint32_t)p.N, (size_t)env), tsprev);
-          }
-        }
-      }
       if constexpr (RP) {
         if (ls == 0) {
           sh.row[cur][el] = rp.row;
@@ -1278,9 +1229,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     g.cos_qn = sqrt(tgt_g[0] * tgt_g[0] + canon<M, S, ONE>(qq));
   }
   const bool need_ar = (p.reward_mode != MGN_REWARD_ENV_LOG) || (om & O_AREW);
-  // one-step launches (TAIL_EXACT): the ledger role stores the step's State;
-  // multi-step launches with GOBS: the generator role
-  const bool lobs = (TAIL_EXACT && K == 1) || GOBS;
+  // one-step launches (TAIL_EXACT): the ledger role stores the step's State
+  const bool lobs = TAIL_EXACT && K == 1;
   // output element strides per step (32-bit: checked on the host) and the
   // lane's bases: per asset (k, env, asset), State.price (k, env, feature),
   // State.portfolio (k, env, 0), per env (k, env)
@@ -1637,7 +1587,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         if (om & O_DEND) ost(ov.data_end + ie, (uint8_t)(RP ? sh.dend[prv][el] : 0u));
         if (om & O_REW) ost(ov.reward + ie, reward);
         if (om & O_NSH) ost(ov.n_shaped + ie, (uint8_t)pops);
-        if (!GOBS && (om & O_TS)) ost(ov.timestamp + ie, (uint64_t)sh.ts[prv][el]);
+        if (om & O_TS) ost(ov.timestamp + ie, (uint64_t)sh.ts[prv][el]);
         if (D == 1) {
           if (om & O_AREW) ost(ov.agent_reward + ie, rin_s);
           if (!NST && (om & O_SHP)) ost(ov.shaped + ie, shaped_s);

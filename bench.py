@@ -372,7 +372,13 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1: nccl (RCCL; the statistics all-gather is the C ABI's "
                          "mgn_stats_allgather) or gloo (several ranks may share one GPU)")
+    ap.add_argument("--sched-spin", action="store_true",
+                    help="diagnostic: hipSetDeviceFlags(hipDeviceScheduleSpin) before the device is used "
+                         "(the host waits by spinning)")
     args = ap.parse_args()
+    if args.sched_spin:
+        import ctypes
+        ctypes.CDLL("libamdhip64.so").hipSetDeviceFlags(1)  # hipDeviceScheduleSpin
 
     import torch
     import torch.distributed as dist

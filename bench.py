@@ -376,12 +376,13 @@ def main():
                     help="diagnostic: hipSetDeviceFlags(hipDeviceScheduleSpin) before the device is used "
                          "(the host waits by spinning)")
     args = ap.parse_args()
-    if args.sched_spin:
-        import ctypes
-        ctypes.CDLL("libamdhip64.so").hipSetDeviceFlags(1)  # hipDeviceScheduleSpin
 
     import torch
     import torch.distributed as dist
+    if args.sched_spin:
+        # (the runtime torch loaded -- by its soname -- before the device is used)
+        import ctypes
+        ctypes.CDLL("libamdhip64.so.7").hipSetDeviceFlags(1)  # hipDeviceScheduleSpin
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

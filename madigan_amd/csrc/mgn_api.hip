@@ -781,18 +781,11 @@ int mgn_window(mgn_env* e, double* price_dev, double* port_dev, uint64_t* ts_dev
   return check_hip(e, hipGetLastError(), "mgn_window");
 }
 
-// timing events: no system-scope fence when they are recorded (the cache
-// write-back and invalidation it costs would be timed with the kernel, and
-// slow the host's launch; they only measure time -- every wait on the work
-// they bracket is a stream or device synchronize)
-static bool timing_event(hipEvent_t* ev) {
-  return hipEventCreateWithFlags(ev, hipEventDisableSystemFence) == hipSuccess;
-}
 static void time_mark(mgn_env* e, std::vector<hipEvent_t>& v, size_t& n, hipStream_t st) {
   if (!e->timing) return;
   if (n == v.size()) {
     hipEvent_t ev;
-    if (!timing_event(&ev)) return;
+    if (hipEventCreate(&ev) != hipSuccess) return;
     v.push_back(ev);
   }
   (void)hipEventRecord(v[n++], st);
@@ -802,7 +795,7 @@ static void time_mark(mgn_env* e, std::vector<hipEvent_t>& v, size_t& n, hipStre
 static bool time_pair(mgn_env* e, hipEvent_t& a, hipEvent_t& b) {
   while (e->t_step.size() < e->t_step_n + 2) {
     hipEvent_t ev;
-    if (!timing_event(&ev)) return false;
+    if (hipEventCreate(&ev) != hipSuccess) return false;
     e->t_step.push_back(ev);
   }
   a = e->t_step[e->t_step_n];

@@ -1142,6 +1142,43 @@ __device__ __forceinline__ double ddr_one_pre(double r, double A, double B, cons
   const double num = pos ? h : (B * h - (A * (r * r)) / 2);
   return rt_div(num, pos ? q.dpos : q.dneg);
 }
+// ddr_one_pre / dsr_one_den with the reciprocals of their denominators formed
+// once per pop rather than per summand, as rt_div forms them (the IEEE
+// division where a denominator is not a normal number): the same operations
+// on the same operands
+__device__ __forceinline__ double rt_rcp(double b) {
+  double r = __builtin_amdgcn_rcp(b);
+  r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
+  return __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
+}
+__device__ __forceinline__ double div_pre(double a, double b, double rb) {
+  double q = a * rb;
+  if (!__builtin_amdgcn_class(b, kNormalClass)) {  // (rt_div's IEEE case, kept in its branch)
+    double x = a;
+    asm volatile("" : "+v"(x));
+    q = x / b;
+  }
+  return q;
+}
+struct DdrPreR {
+  DdrPre q;
+  double rpos, rneg;
+};
+__device__ __forceinline__ DdrPreR ddr_pre_r(double A, double B) {
+  const DdrPre q = ddr_pre(A, B);
+  return DdrPreR{q, rt_rcp(q.dpos), rt_rcp(q.dneg)};
+}
+__device__ __forceinline__ double ddr_one_r(double r, double A, double B, const DdrPreR& c) {
+  const double h = r - c.q.hA;
+  const bool pos = r > 0.;
+  const double num = pos ? h : (B * h - (A * (r * r)) / 2);
+  return div_pre(num, pos ? c.q.dpos : c.q.dneg, pos ? c.rpos : c.rneg);
+}
+__device__ __forceinline__ double dsr_one_r(double r, double A, double B, double den, double rden) {
+  const double dA = r - A;
+  const double dB = r * r - B;
+  return div_pre(B * dA - (A * dB) / 2, den, rden);
+}
 __device__ __forceinline__ double clip1(double v) { return v < -1. ? -1. : (v > 1. ? 1. : v); }
 // dsr_one with its reward-independent denominator evaluated once per pop (the
 // same operations on the same operands)

@@ -529,10 +529,14 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   };
   const auto nst_summands = [&](const double* ring, double* scr, int head, int len, double A, double B,
                                 const PopPre& c) {
-    if (p.shaper == MGN_SHAPER_DDR)
-      nst_rounds(ring, scr, head, len, [&](double r, double d) { return d * ddr_one_pre(r, A, B, c.q); });
-    else if (p.shaper == MGN_SHAPER_DSR)
-      nst_rounds(ring, scr, head, len, [&](double r, double d) { return d * dsr_one_den(r, A, B, c.dden); });
+    // (DDR / DSR: the denominators' reciprocals formed once per pop)
+    if (p.shaper == MGN_SHAPER_DDR) {
+      const DdrPreR cr{c.q, rt_rcp(c.q.dpos), rt_rcp(c.q.dneg)};
+      nst_rounds(ring, scr, head, len, [&](double r, double d) { return d * ddr_one_r(r, A, B, cr); });
+    } else if (p.shaper == MGN_SHAPER_DSR) {
+      const double rden = rt_rcp(c.dden);
+      nst_rounds(ring, scr, head, len, [&](double r, double d) { return d * dsr_one_r(r, A, B, c.dden, rden); });
+    }
     else if (p.shaper == MGN_SHAPER_SORTINO_B)
       nst_rounds(ring, scr, head, len, [&](double r, double d) { return sortinoB_term(r, d, p.sexp); });
     else  // PPC / none: the stored value

@@ -77,6 +77,14 @@ def main():
                 "wait_any_frac": m["SQ_WAIT_ANY"] / m["SQ_WAVE_CYCLES"]
                 if "SQ_WAIT_ANY" in m and "SQ_WAVE_CYCLES" in m else None,
             })
+        if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
+            # gfx950: FETCH_SIZE reports half the bytes of a wide streaming read
+            # (MI355X_MICROARCH.md, HBM): doubled; WRITE_SIZE exact; kilobytes
+            out["hbm_bytes_per_launch"] = (2 * m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024
+            out["fetch_kb_raw"] = m["FETCH_SIZE"]
+            out["write_kb"] = m["WRITE_SIZE"]
+        if "SQ_INSTS_VALU" in m:
+            out["valu_wave_insts_per_launch"] = m["SQ_INSTS_VALU"]
         if dur:
             out["dispatch_us"] = 1e6 * sum(dur) / len(dur)
             if "GRBM_GUI_ACTIVE" in m:
@@ -95,6 +103,18 @@ def main():
         print(n, json.dumps(brief))
     if "--json" in sys.argv:
         json.dump(res, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
+    if "--update" in sys.argv:
+        # the bench's lookups (bench.load_pmc_traffic / valu_issue): per workload
+        # key (the library name of the pass), per launch
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        for fname, field in (("pmc_traffic.json", "hbm_bytes_per_launch"),
+                             ("pmc_valu.json", "valu_wave_insts_per_launch")):
+            path = os.path.join(root, "profiles", fname)
+            d = json.load(open(path)) if os.path.exists(path) else {}
+            for n, r in res.items():
+                if r.get(field) and re.match(r"(C\d|R1)_", n):
+                    d[n] = r[field]
+            json.dump(d, open(path, "w"), indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":

@@ -389,7 +389,8 @@ void choose_sched(mgn_env* e) {
     // one asset with a window: the two-lane layout's one-wave-per-role grid
     // holds 16384 envs in one round (two workgroups per CU); beyond it the
     // single-role kernel's one lane per env measured faster (R1 at 65536:
-    // 1098 vs 1507 us per 64-step launch, profiles/r05c_bench_R1.json)
+    // 1098 vs 1507 us per 64-step launch, profiles/r05c_bench_R1_64k{_single,}.json;
+    // at 8192 envs the three-role kernel 337 vs 809, r05c_bench_R1_8k{,_single}.json)
     const bool one_win_big = e->apad == 1 && e->W > 0 && e->N > 16384;
     e->trio = trio_eligible(e) && e->m == 1 && !one_win_big &&
               (e->apad <= 8 ||

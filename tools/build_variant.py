@@ -35,8 +35,10 @@ def main():
         if base not in redo:
             return os.path.join(B.OBJ, base.replace(".hip", ".o"))
         obj = os.path.join(out_dir, base.replace(".hip", ".o"))
-        subprocess.run([cc, *B.FLAGS, *B.UNIT_FLAGS.get(base, []), "-DMGN_DIAG", *extra, "-c", "-o", obj, src],
-                       check=True)
+        # (MGN_VARIANT_NO_UNIT_FLAGS=1: without the unit's own flags, e.g. with
+        # machine LICM in a unit the product builds without it)
+        uf = [] if os.environ.get("MGN_VARIANT_NO_UNIT_FLAGS") else B.UNIT_FLAGS.get(base, [])
+        subprocess.run([cc, *B.FLAGS, *uf, "-DMGN_DIAG", *extra, "-c", "-o", obj, src], check=True)
         return obj
 
     with ThreadPoolExecutor(4) as ex:

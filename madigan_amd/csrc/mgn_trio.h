@@ -599,7 +599,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     int jlast = 0;
     __builtin_amdgcn_s_setprio(kPrioG);
 #ifdef MGN_STAMPS
-    unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0;
+    unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0, Tg = 0, accg = 0;
     int jn = 0;
 #endif
     int gpend = 0;  // WIN: refill ticks still to come after the reset tick
@@ -749,6 +749,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           }
         }
       }
+#ifdef MGN_STAMPS
+      Tg = __builtin_amdgcn_s_memtime();
+#endif
       if constexpr (NPF) {
         // the finish role's next pop, one iteration ahead (NPF above): its
         // buffer after this iteration -- it appends iff it evaluates a step
@@ -801,6 +804,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         }
         if (ls == 0) npf.pln[cur][el] = pl;
       }
+#ifdef MGN_STAMPS
+      accg += __builtin_amdgcn_s_memtime() - Tg;  // the generator's NPF block
+#endif
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         sh.price[cur][lx + m] = s.P[m];
@@ -840,6 +846,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     if (threadIdx.x == 0) {
       atomicAdd(&g_duo_stamps[0], acc0);
       atomicAdd(&g_duo_stamps[1], acc1);
+      atomicAdd(&g_duo_stamps[7], accg);
       atomicAdd(&g_duo_stamps[8], (unsigned long long)(jn + 1));
       atomicAdd(&g_duo_stamps[10], 1ull);
     }
@@ -1341,11 +1348,14 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   drain_vmem();
   __builtin_amdgcn_s_setprio(kPrioF);
 #ifdef MGN_STAMPS
-  unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0;
+  unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0, Tf1 = 0, Tf2 = 0, facc[3] = {0, 0, 0};
 #endif
   for (int j = 0;; ++j) {
     const int cur = j & 1, prv = cur ^ 1;
     MGN_T(T0);
+#ifdef MGN_STAMPS
+    Tf1 = Tf2 = 0;
+#endif
     int rst_out = 0;
     bool tail_rst = false;  // TAIL: the launch's last step ended its episode
     // the step L ran in iteration j-1, unless F voided it at iteration j-1
@@ -1443,6 +1453,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       }
       double shaped_s = 0., rin_s = 0., shaped_v = 0.;
       int pops = 1;
+#ifdef MGN_STAMPS
+      Tf1 = __builtin_amdgcn_s_memtime();
+#endif
       if (NST) {
         // NStepBuffer.add + pop_nstep_sarsd (nstep_buffer.py:315-356, driven as
         // replay_buffer.py:68-80) for the env's scalar column: append, pop once
@@ -1560,6 +1573,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         shaped_v = f.valid[0] ? shape(p.shaper, ar[0], g.shA, g.shB, p.eta, cos_term, p.sexp) : 0.;  // M = 1
       }
       if (j == 1) MGN_IT(57, 2 * TRIO_W);
+#ifdef MGN_STAMPS
+      Tf2 = __builtin_amdgcn_s_memtime();
+#endif
       // outputs of step k (the speculative runs never reach F)
 #ifndef MGN_ABL_NOSTORE_ASSET
 #pragma unroll
@@ -1670,6 +1686,11 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #ifdef MGN_STAMPS
     acc0 += T1 - T0;
     acc1 += T2 - T1;
+    if (Tf2) {  // the iterations that evaluated a step: before / in / after the reward's shaping
+      facc[0] += Tf1 - T0;
+      facc[1] += Tf2 - Tf1;
+      facc[2] += T1 - Tf2;
+    }
 #endif
     if (trio_exit(j, K, sh.more[j % 3])) break;
   }
@@ -1677,6 +1698,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   if (l == 0) {
     atomicAdd(&g_duo_stamps[16], acc0);
     atomicAdd(&g_duo_stamps[17], acc1);
+    atomicAdd(&g_duo_stamps[9], facc[0]);
+    atomicAdd(&g_duo_stamps[11], facc[1]);
+    atomicAdd(&g_duo_stamps[12], facc[2]);
   }
 #endif
 #ifdef MGN_TRIO_ABL_EPI

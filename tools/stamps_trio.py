@@ -67,7 +67,12 @@ def main():
                              enumerate(("prices_and_pre_sums", "units", "broker", "records"))},
            "broker_first_pass": {"trees": round(v[2] / it, 1), "cash_chain": round(v[3] / it, 1),
                                  "checks_and_more_passes": round(v[6] / it, 1)},
-           "finish": {"work": round(v[16] / it, 1), "wait": round(v[17] / it, 1)},
+           "finish": {"work": round(v[16] / it, 1), "wait": round(v[17] / it, 1),
+                      # per iteration that evaluated a step (averaged over all
+                      # iterations): records to reward / shaping / outputs
+                      "phases": {k: round(v[i] / it, 1) for k, i in
+                                 (("to_reward", 9), ("shaping", 11), ("outputs", 12))}},
+           "gen_npf_block": round(v[7] / it, 1),
            "ledger_passes_per_broker_call": round(v[19] / max(v[18], 1), 3)}
     print(json.dumps(res))
 

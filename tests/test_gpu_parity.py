@@ -324,6 +324,38 @@ def test_nstep_generator_prefix_vs_oracle(gpu, A, N, n, shaper):
     close(g.shaper_b.cpu().numpy(), orc.scalar("shaperB"), "B")
 
 
+@pytest.mark.parametrize("extra", [(), ("n_shaped",)])
+def test_nstep_agent_output_sets_bit_identical(gpu, extra):
+    """The n-step agent loop's output sets (O_STD, and O_STD with the popped
+    counts) have instantiations of their own with the output mask at compile
+    time (mgn_launch_impl.h launch_trio_nst): the 8192 x 8 TrendOU n = 20 DDR
+    shape stepped through them equals, bit for bit, the same handle stepped
+    with every output (the runtime-mask kernel the oracle tests pin), over two
+    launches with auto-resets, and the final state matches the oracle."""
+    K = 24
+    kw = dict(required_margin=0.02, maintenance_margin=0.25, transaction_cost_rel=0.02,
+              unit_size=0.9, auto_reset=1, init_cash=1e5, reward_shaper="DDR",
+              adaptation_rate=0.01, nstep_return=20, discount=0.97)
+    src = trendou_sources(8, [0.2, 2, 6, 0.05, 0.2, 5.0, 0.15, 0.3, 0.2, 0.99])
+    std = ("reward", "shaped", "done", "obs_price", "obs_port", "timestamp", "tprice", "tunits", "tcost",
+           "risk", "margin_call") + extra
+    g, orc = make_pair(src, 8192, **kw)
+    h, _ = make_pair(src, 8192, **kw)
+    acts = g.generate_actions(2 * K, seed=23)
+    ends = 0
+    for half in range(2):
+        a = acts[half * K:(half + 1) * K]
+        o = g.alloc_traj(K, fields=std)
+        g.rollout(a, o)
+        full = {k: v.cpu().numpy() for k, v in h.rollout(a).items()}
+        orc.rollout(a.cpu().numpy())
+        for k, v in o.items():
+            assert_bits(v.cpu().numpy(), full[k], f"{k} {extra} {half}")
+        ends += int(full["done"].sum())
+    assert ends > 0
+    state_check(g, orc, f"nstep output sets {extra}")
+
+
 def test_nstep64_two_assets_auto_schedule(gpu):
     """2 assets, n = 64, at a batch that takes the 256-lane layout: the
     three-role kernel's static arrays plus 128 envs' rings (128 KiB) exceed a

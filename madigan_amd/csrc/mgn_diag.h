@@ -11,8 +11,7 @@
      defined(MGN_ABL_NOSTORE_ASSET) || defined(MGN_ABL_NOSTORE_ENV) || defined(MGN_ABL_DRAW) ||          \
      defined(MGN_TRIO_ABL_PRO) || defined(MGN_TRIO_ABL_G) || defined(MGN_TRIO_ABL_L) ||                  \
      defined(MGN_TRIO_ABL_F) || defined(MGN_TRIO_ABL_EPI) || defined(MGN_NST_ABL_TERM) ||                \
-     defined(MGN_NST_ABL_SUM) || defined(MGN_NST_ABL_ROW) || defined(MGN_NO_GK) ||          \
-     defined(MGN_NO_NPF))
+     defined(MGN_NST_ABL_SUM) || defined(MGN_NST_ABL_ROW) || defined(MGN_NO_GK))
 #error "stamp / ablation switches belong to diagnostic builds (-DMGN_DIAG, tools/build_variant.py)"
 #endif
 

@@ -123,10 +123,10 @@ struct TrioGo {
   const StepArgs& a;
   bool small;
   template <typename Kern>
-  void operator()(Kern kern, bool nst, int npads = 2) const {
+  void operator()(Kern kern, bool nst) const {
     const int epb = (small ? 64 : TRIO_W) / S;
     const int grid = (a.p.N + epb - 1) / epb;
-    const size_t lds = nst ? trio_nst_dyn_lds(S, small ? 64 : TRIO_W, a.p.nstep, npads) : 0;
+    const size_t lds = nst ? trio_nst_dyn_lds(S, small ? 64 : TRIO_W, a.p.nstep) : 0;
     // a refused size is the caller's hipGetLastError (HIP records every
     // call's status); trio_eligible keeps static + dynamic LDS within 160 KiB
     if (lds && hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
@@ -168,15 +168,13 @@ void launch_trio_nst(const StepArgs& a) {
       else goN(k_step_trio<S, false, false, 0, false, 64, true>);
     }
   } else if (disc && a.gkind == MGN_SRC_TRENDOU) {
-    // (the generator role forms the next pop's prefix: a third pad per env);
     // the agent loop's output sets at compile time (O_STD, with the popped
-    // counts O_STDN): n = 20 DDR 3.74 -> 3.64 us/step against the runtime
-    // mask (profiles/r05s_nst_ab.txt)
-    constexpr int np = trio_npf(true, MGN_SRC_TRENDOU, 1) ? 3 : 2;
+    // counts O_STDN): with the finish role popping in full, n = 20 DDR 3.37
+    // against 3.67 us/step (profiles/r05s_nst_ab.txt)
     auto pick = [&](auto omc) {
       constexpr uint32_t OM = decltype(omc)::value;
-      if (a.p.reqm_one) go(k_step_trio<S, true, true, OM, false, TRIO_W, true, MGN_SRC_TRENDOU>, true, np);
-      else go(k_step_trio<S, false, true, OM, false, TRIO_W, true, MGN_SRC_TRENDOU>, true, np);
+      if (a.p.reqm_one) goN(k_step_trio<S, true, true, OM, false, TRIO_W, true, MGN_SRC_TRENDOU>);
+      else goN(k_step_trio<S, false, true, OM, false, TRIO_W, true, MGN_SRC_TRENDOU>);
     };
     const uint32_t om = traj_mask(a.out);
     if (om == O_STD) pick(std::integral_constant<uint32_t, O_STD>{});
@@ -402,7 +400,7 @@ void dispatch_m(int m, const Arg& a) {
     if constexpr (A >= 2 && A <= 16) {                                                       \
       const bool small = win || n_envs * A < 256LL * TRIO_W;                                 \
       return (small ? trio_static_lds<A, 64, true>() : trio_static_lds<A, TRIO_W, true>()) +   \
-             trio_nst_dyn_lds(A, small ? 64 : TRIO_W, nstep, small ? 2 : 3);                \
+             trio_nst_dyn_lds(A, small ? 64 : TRIO_W, nstep);                               \
     }                                                                                        \
     return ~(size_t)0;                                                                       \
   }                                                                                          \

@@ -72,21 +72,13 @@ constexpr int kPrioG = 0, kPrioL = 2, kPrioF = 1;
 // interleave; rounds past the buffer's are computed and dropped)
 constexpr int kNstU = 3;
 
-// NST, one iteration ahead (NPF): a pop sums gamma^k f(r_k; A, B) over the
-// ring's n entries with the shaper state (A, B) the previous pops left, and
-// that state moves only with the popped (oldest) entries -- so the state of
-// the next iteration's first pop, and that pop's summands over every entry
-// already in the ring then, are known an iteration early.  In iteration j the
-// generator role predicts the finish role's buffer after iteration j (it
-// evaluates a step iff the records say so, and pops once when that fills the
-// ring; a done flush is caught below), forms the next pop's summands over
-// the entries the ring holds now and their ordered sum, and publishes them
-// with the state it assumed.  In iteration j + 1 the finish role takes the
-// prefix where its own state matches the prediction bit for bit and adds the
-// remaining one or two entries' summands in entry order -- the same
-// operations in the same order as the full pop; otherwise it pops in full.
-// (Round 4 formed the prefix in the pop's own iteration: neutral,
-// profiles/r04_ab_nst_prefix.txt -- the finish role waited for it.)
+// NST: the finish role pops in full, after its reward chain.  (Forming a
+// pop's prefix -- its summands over the entries already in the ring, and
+// their ordered sum -- ahead of the pop in another role measured neutral in
+// the pop's own iteration, round 4, profiles/r04_ab_nst_prefix.txt, and
+// slower one or two iterations ahead, round 5: n = 20 DDR 3.37 against 3.67
+// us/step with the prefix one iteration ahead by the generator role,
+// profiles/r05s_nst_ab.txt.)
 
 // the loop's exit test after iteration j's barrier: iterations 0..K always
 // run (the K steps, one iteration behind for the finish role), so the shared
@@ -161,17 +153,6 @@ struct TrioShared {
   // generator role for the finish role's window rows
   double lprice[2][NSL];
 };
-// NPF: the finish role's buffer after its pops (F -> G, next iteration):
-// shaper state, oldest index, fill count; the generator's prefix of the next
-// pop (G -> F, next iteration): its sum over the first pcnt entries and the
-// buffer state it assumed (empty where NPF is off: no LDS)
-template <int EPB, bool ON>
-struct NpfShared {
-  double fA[2][EPB], fB[2][EPB], pfx[2][EPB], pA[2][EPB], pB[2][EPB];
-  int32_t fhd[2][EPB], fln[2][EPB], phd[2][EPB], pln[2][EPB], pcnt[2][EPB];
-};
-template <int EPB>
-struct NpfShared<EPB, false> {};
 
 // LDS of k_step_trio<S, ..., TW, NST, ..., M>: its static arrays (an upper
 // bound of the compiler's layout) plus, for NST, the rings in dynamic LDS; the
@@ -179,7 +160,7 @@ struct NpfShared<EPB, false> {};
 // (kTrioLdsMax, mgn_launch.h)
 template <int S, int TW, bool NST, int M = 1>
 constexpr size_t trio_static_lds() {
-  return sizeof(TrioShared<S, TW, M>) + sizeof(NpfShared<TW / S, NST>) + (size_t)(TW / S) * sizeof(EnvRecs<S * M>) +
+  return sizeof(TrioShared<S, TW, M>) + (size_t)(TW / S) * sizeof(EnvRecs<S * M>) +
          S * M * sizeof(mgn_asset_source) + (MGN_MAX_ASSETS + 1) * sizeof(double) +
          (NST ? MGN_MAX_NSTEP : 1) * sizeof(double) + 256;
 }
@@ -232,17 +213,9 @@ __device__ __forceinline__ void trio_replay_tick(Lane<M>& s, const KParams& p, u
   nx.dend = p.rp_end[s.rcur];
   s.pf_ok = true;
 }
-// per env: the ring, the finish role's pop summands and (npads 3, NPF) the
-// generator's prefix summands
-inline size_t trio_nst_dyn_lds(int S, int TW, int nstep, int npads = 2) {
-  return (size_t)(TW / S) * npads * nst_pad(nstep, S) * sizeof(double);
-}
-// NPF: n-step launches whose generator lanes are env-major (one source kind)
-__host__ __device__ constexpr bool trio_npf(bool nst, int gk, int mm) {
-#if defined(MGN_DIAG) && defined(MGN_NO_NPF)  // diagnostic A/B builds: the finish role pops in full
-  return false;
-#endif
-  return nst && gk >= 0 && mm == 1;
+// per env: the ring and the finish role's pop summands
+inline size_t trio_nst_dyn_lds(int S, int TW, int nstep) {
+  return (size_t)(TW / S) * 2 * nst_pad(nstep, S) * sizeof(double);
 }
 
 // OMC: the output set when known at compile time (O_ALL, O_STD), else 0.
@@ -313,8 +286,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   // would cost the longer launches registers), one slot per lane
   constexpr bool TAIL = K1 && !RP && !WIN && MM == 1;
   constexpr bool GLOG = WIN && !RP;
-  constexpr bool NPF = trio_npf(NST, GK, MM);
-  constexpr int NPADS = NPF ? 3 : 2;  // NST: ring, pop summands (, NPF: the generator's prefix summands)
+  constexpr int NPADS = 2;  // NST: ring, pop summands
   static_assert(M == 1 || (M == 2 && !NST), "two slots per lane: one-step rewards");
   static_assert(!ONE || (S == 2 && M == 1), "a one-asset env on two lanes per role");
   constexpr int APAD = S * M;
@@ -322,7 +294,6 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   constexpr int TRIO_BLOCK = 3 * TW;
   constexpr int EPB = TRIO_W / S;
   __shared__ TrioShared<S, TW, M> sh;
-  __shared__ NpfShared<TW / S, NPF> npf;
   __shared__ EnvRecs<APAD> recs[EPB];
   __shared__ mgn_asset_source s_src[APAD];
   __shared__ double s_tgt[MGN_MAX_ASSETS + 1];
@@ -599,7 +570,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     int jlast = 0;
     __builtin_amdgcn_s_setprio(kPrioG);
 #ifdef MGN_STAMPS
-    unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0, Tg = 0, accg = 0;
+    unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0;
     int jn = 0;
 #endif
     int gpend = 0;  // WIN: refill ticks still to come after the reset tick
@@ -749,64 +720,6 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           }
         }
       }
-#ifdef MGN_STAMPS
-      Tg = __builtin_amdgcn_s_memtime();
-#endif
-      if constexpr (NPF) {
-        // the finish role's next pop, one iteration ahead (NPF above): its
-        // buffer after this iteration -- it appends iff it evaluates a step
-        // here (its own test), and pops the oldest entry once if that fills
-        // the ring -- and, if its next evaluated step fills the ring, that
-        // pop's summands over the entries the ring holds now (the ring and
-        // the state are in LDS from iteration 1 on)
-        int pl = -1;
-        if (j > 0 && live && (p.shaper < MGN_SHAPER_SHARPE || p.shaper == MGN_SHAPER_SORTINO_B)) {
-          const int n = p.nstep;
-          const double* ring = s_nst + (size_t)el * NPADS * nst_pad(n, S);
-          double* gscr = s_nst + (size_t)el * NPADS * nst_pad(n, S) + 2 * nst_pad(n, S);
-          int he = npf.fhd[prv][el], le = npf.fln[prv][el];
-          int known = le;
-          double Ae = npf.fA[prv][el], Be = npf.fB[prv][el];
-          if ((sh.rFlags[prv][el] & TR_STEP) && !sh.reset[prv][el]) {
-            le += 1;
-            known = le - 1;  // (the appended entry is formed in this iteration)
-            if (le >= n) {   // the pop of the oldest entry: the shaper state moves
-              const double r0 = ring[he];
-              if (p.shaper == MGN_SHAPER_DSR || p.shaper == MGN_SHAPER_DDR) {
-                Ae += p.eta * (r0 - Ae);
-                if (p.shaper == MGN_SHAPER_DSR) {
-                  Be += p.eta * (r0 * r0 - Be);
-                } else {
-                  double m = r0 < 0. ? r0 : 0.;
-                  if (r0 != r0) m = r0;
-                  Be += p.eta * (m * m - Be);
-                }
-              }
-              he = (he + 1 == n) ? 0 : he + 1;
-              le -= 1;
-              known -= 1;
-            }
-          }
-          if (le + 1 == n && known > 0) {
-            nst_summands(ring, gscr, he, known, Ae, Be, pop_pre(p.shaper, Ae, Be));
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (ls == 0) {
-              npf.pfx[cur][el] = nst_sum(gscr, known);
-              npf.pA[cur][el] = Ae;
-              npf.pB[cur][el] = Be;
-              npf.phd[cur][el] = he;
-              npf.pcnt[cur][el] = known;
-            }
-            pl = le;
-          }
-        }
-        if (ls == 0) npf.pln[cur][el] = pl;
-      }
-#ifdef MGN_STAMPS
-      accg += __builtin_amdgcn_s_memtime() - Tg;  // the generator's NPF block
-#endif
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         sh.price[cur][lx + m] = s.P[m];
@@ -846,7 +759,6 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     if (threadIdx.x == 0) {
       atomicAdd(&g_duo_stamps[0], acc0);
       atomicAdd(&g_duo_stamps[1], acc1);
-      atomicAdd(&g_duo_stamps[7], accg);
       atomicAdd(&g_duo_stamps[8], (unsigned long long)(jn + 1));
       atomicAdd(&g_duo_stamps[10], 1ull);
     }
@@ -1502,36 +1414,13 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           }
           const PopPre c = pop_pre(p.shaper, g.shA, g.shB);
           double acc = 0.0;
-          bool pre = false;
-          if constexpr (NPF) {
-            // the generator's prefix (NPF): where the buffer is the one it
-            // predicted -- oldest index, fill count and shaper state bit for
-            // bit -- its ordered sum of the first pcnt summands, then the rest
-            // in entry order (the env's first lane)
-            pre = pj == 0 && len == n && npf.pln[prv][el] == nlen && npf.phd[prv][el] == nhead &&
-                  __double_as_longlong(npf.pA[prv][el]) == __double_as_longlong(g.shA) &&
-                  __double_as_longlong(npf.pB[prv][el]) == __double_as_longlong(g.shB);
-          }
-          if constexpr (NPF) {
-            if (pre && ls == 0) {
-              acc = npf.pfx[prv][el];
-              for (int kk = npf.pcnt[prv][el]; kk < len; ++kk) {
-                int idx = head + kk;
-                idx -= (idx >= n) ? n : 0;
-                acc += (p.shaper == MGN_SHAPER_SORTINO_B) ? sortinoB_term(ring[idx], s_disc[kk], p.sexp)
-                                                          : pop_term(p.shaper, ring[idx], g.shA, g.shB, c, s_disc[kk]);
-              }
-            }
-          }
-          if (!pre) {
-            nst_summands(ring, scr, head, len, g.shA, g.shB, c);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // the ordered sum only feeds the popped value the env's first lane
-            // stores: only that lane reads the summands back
-            if (ls == 0) acc = nst_sum(scr, len);
-          }
+          nst_summands(ring, scr, head, len, g.shA, g.shB, c);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          // the ordered sum only feeds the popped value the env's first lane
+          // stores: only that lane reads the summands back
+          if (ls == 0) acc = nst_sum(scr, len);
           double res = acc;
           if (p.shaper == MGN_SHAPER_SORTINO_B) res = clip1(acc);  // (naive_n, len > 1)
           if (p.shaper == MGN_SHAPER_DSR || p.shaper == MGN_SHAPER_DDR) {
@@ -1666,16 +1555,6 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       }
     }
     if (ls == 0) sh.reset[cur][el] = rst_out;
-    if constexpr (NPF) {
-      // the buffer after this iteration's pops, for the generator's prefix
-      // of the next pop
-      if (ls == 0) {
-        npf.fA[cur][el] = g.shA;
-        npf.fB[cur][el] = g.shB;
-        npf.fhd[cur][el] = nhead;
-        npf.fln[cur][el] = nlen;
-      }
-    }
     // the reset tick runs next iteration -- a tail reset's in this one, by the
     // idle generator role (adopted after the loop)
     if (rst_out && !tail_rst) sh.more[j % 3] = 1;

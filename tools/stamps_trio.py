@@ -72,7 +72,6 @@ def main():
                       # iterations): records to reward / shaping / outputs
                       "phases": {k: round(v[i] / it, 1) for k, i in
                                  (("to_reward", 9), ("shaping", 11), ("outputs", 12))}},
-           "gen_npf_block": round(v[7] / it, 1),
            "ledger_passes_per_broker_call": round(v[19] / max(v[18], 1), 3)}
     print(json.dumps(res))
 

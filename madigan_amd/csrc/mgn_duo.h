@@ -132,6 +132,8 @@ constexpr uint32_t O_ALL = 16383u;
 constexpr uint32_t O_STD = O_REW | O_SHP | O_DONE | O_OPR | O_OPT | O_TS | O_TP | O_TU | O_TC | O_RISK | O_MC;
 // an n-step agent loop's: O_STD and the popped-value counts
 constexpr uint32_t O_STDN = O_STD | O_NSH;
+// a windowed n-step agent loop's (bench.py windowed()): O_STDN and data_end
+constexpr uint32_t O_WSTD = O_STD | O_DEND | O_NSH;
 // element index k * stride + base as one 32 x 32 + 64 multiply-add (the
 // host checks that every stride fits 32 bits)
 __device__ __forceinline__ size_t kidx(int k, uint32_t stride, size_t base) {

@@ -24,12 +24,19 @@ REF_KW = dict(required_margin=1.0, maintenance_margin=0.25, transaction_cost_rel
               discount=0.99, reward_mode="agent_sum")
 
 
-def _launch_vs_oracle(g, orc, acts, tag, shaped_rtol):
+# the bench's output set for the windowed workloads (bench.py windowed(): the
+# agent loop's State / EnvInfo, data_end and the popped counts), which the
+# one-asset OU n-step window handles instantiate with the set at compile time
+BENCH_FIELDS = ["reward", "shaped", "done", "obs_price", "obs_port", "timestamp", "tprice", "tunits", "tcost",
+                "risk", "margin_call", "data_end", "n_shaped"]
+
+
+def _launch_vs_oracle(g, orc, acts, tag, shaped_rtol, fields=None):
     import ctypes as C
     import torch
     from madigan_amd import _lib as L
     K, N, W, A, F = acts.shape[0], g.N, g.W, g.A, g.F
-    traj = g.alloc_traj(K)
+    traj = g.alloc_traj(K, fields=fields)
     wp = torch.empty((K, N, W, F), dtype=torch.float64, device=g.device)
     wo = torch.empty((K, N, W, A + 1), dtype=torch.float64, device=g.device)
     wt = torch.empty((K, N, W), dtype=torch.int64, device=g.device)
@@ -47,7 +54,8 @@ def _launch_vs_oracle(g, orc, acts, tag, shaped_rtol):
         for f in ("risk", "done", "margin_call", "n_shaped"):
             assert np.array_equal(host[f][k], r[f][0]), f"{tag} {f} step {k}"
         close(host["reward"][k], r["reward"][0], f"{tag} reward step {k}")
-        close(host["agent_reward"][k], r["agent_reward"][0], f"{tag} agent reward step {k}")
+        if "agent_reward" in host:
+            close(host["agent_reward"][k], r["agent_reward"][0], f"{tag} agent reward step {k}")
         np.testing.assert_allclose(host["shaped"][k], r["shaped"][0], rtol=shaped_rtol, atol=1e-14,
                                    err_msg=f"{tag} n-step row step {k}")
         rpr, rpo, rts = orc.window()
@@ -91,3 +99,19 @@ def test_reference_shape_vs_oracle(gpu, N, shaper, extra, rtol):
     acts2 = g.generate_actions(8, seed=0x6D6164 + 23)
     _launch_vs_oracle(g, orc, acts2, f"{shaper} N={N} after units", rtol)
     state_check(g, orc, f"{shaper} N={N} end")
+
+
+@pytest.mark.parametrize("shaper,extra", [("DDR", {}), ("sortino_shaperB", dict(sortino_exp=1.1))])
+def test_reference_shape_bench_outputs_vs_oracle(gpu, shaper, extra):
+    """The bench's output set (BENCH_FIELDS) at 8192 envs: the instantiation
+    with that set and the OU generator at compile time
+    (mgn_launch_impl.h launch_trio_one_impl) against the oracle, every
+    output, n-step row and window of two 64-step launches with auto-resets."""
+    kw = dict(REF_KW, reward_shaper=shaper, **extra, seed=0x6D6164 + 31)
+    kw.update(required_margin=0.05, unit_size=0.9)
+    g, orc = make_pair(ou_sources(1), 8192, **kw)
+    K = 64
+    acts = g.generate_actions(2 * K, seed=0x6D6164 + 32)
+    ends = _launch_vs_oracle(g, orc, acts[:K], f"{shaper} bench set launch 0", 1e-10, BENCH_FIELDS)
+    ends += _launch_vs_oracle(g, orc, acts[K:], f"{shaper} bench set launch 1", 1e-10, BENCH_FIELDS)
+    assert ends > 8192 // 20, f"{ends} episode ends"

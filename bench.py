@@ -614,7 +614,8 @@ def main():
         np.save(args.dump_stats, gathered.cpu().numpy())
     if rank == 0:
         K = int(round(steps_per_launch))
-        workload = f"C3_trendou_{N}x{A}_fuse{K}"
+        # (n-step handles have PMC entries of their own: the pops' rows)
+        workload = f"C3_trendou_{N}x{A}" + (f"_n{args.nstep}" if args.nstep > 1 else "") + f"_fuse{K}"
         traffic, traffic_key = load_pmc_traffic(workload)
         probe = bandwidth_probe(dev) if args.probe else None
         roof = {"bound": "hbm", "achieved": achieved_gbs, "peak": PEAK_HBM_GBS,

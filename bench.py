@@ -372,6 +372,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1: nccl (RCCL; the statistics all-gather is the C ABI's "
                          "mgn_stats_allgather) or gloo (several ranks may share one GPU)")
+    ap.add_argument("--wait", default="stream", choices=["stream", "spin"],
+                    help="the timed region's closing wait on the handle's stream: "
+                         "hipStreamSynchronize or polling hipStreamQuery (mgn_synchronize_spin)")
     ap.add_argument("--sched-spin", action="store_true",
                     help="diagnostic: hipSetDeviceFlags(hipDeviceScheduleSpin) before the device is used "
                          "(the host waits by spinning)")
@@ -457,7 +460,8 @@ def main():
         return rc
 
     warm, timed = plan(0, args.warmup), plan(args.warmup, total)
-    sync = env.stream_synchronizer()  # the handle's stream (every launch is on it)
+    # the handle's stream (every launch is on it); --wait spin polls it
+    sync = env.stream_synchronizer(spin=args.wait == "spin")
     # kernel durations: HIP events around each step launch on the handle's
     # stream (mgn_set_timing; pooled events, created during the warmup)
     tmode = 2 if args.timing == "launch" else 1

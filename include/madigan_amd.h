@@ -431,6 +431,10 @@ int mgn_bandwidth_probe(void *dst_dev, const void *src_dev, size_t bytes, int32_
                         double *gbps_out);
 /* synchronise the handle's stream */
 int mgn_synchronize(mgn_env *env);
+/* synchronise the handle's stream by polling it (hipStreamQuery until the
+ * stream is idle: the calling thread busy-waits; for short waits, e.g. an
+ * agent loop's per-step wait) */
+int mgn_synchronize_spin(mgn_env *env);
 const char *mgn_last_error(const mgn_env *env);
 const char *mgn_global_error(void);
 

@@ -145,6 +145,7 @@ SYMBOLS = {
     "mgn_bandwidth_probe": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int32, C.c_void_p,
                                       C.POINTER(C.c_double)]),
     "mgn_synchronize": (C.c_int, [C.c_void_p]),
+    "mgn_synchronize_spin": (C.c_int, [C.c_void_p]),
     "mgn_last_error": (C.c_char_p, [C.c_void_p]),
     "mgn_global_error": (C.c_char_p, []),
 }

@@ -1303,6 +1303,14 @@ int mgn_synchronize(mgn_env* e) {
   return check_hip(e, hipStreamSynchronize(e->stream), "hipStreamSynchronize");
 }
 
+int mgn_synchronize_spin(mgn_env* e) {
+  if (!e) return MGN_ERR_ARG;
+  hipError_t st;
+  while ((st = hipStreamQuery(e->stream)) == hipErrorNotReady) {
+  }
+  return check_hip(e, st, "hipStreamQuery");
+}
+
 const char* mgn_last_error(const mgn_env* e) { return e ? e->err.c_str() : g_error.c_str(); }
 const char* mgn_global_error(void) { return g_error.c_str(); }
 

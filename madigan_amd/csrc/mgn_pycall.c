@@ -8,6 +8,7 @@
  * way the reference's pybind11 Env.step binding calls Env::step.
  *
  *   rollout(env, actions, k, traj) -> int   (= mgn_rollout(env, actions, k, traj))
+ *   synchronize_spin(env) -> int            (= mgn_synchronize_spin(env): polling)
  *   synchronize(env) -> int                 (= mgn_synchronize(env): the handle's
  *                                            stream, not the whole device)
  *
@@ -52,10 +53,24 @@ static PyObject *synchronize(PyObject *self, PyObject *arg) {
   Py_END_ALLOW_THREADS return PyLong_FromLong(rc);
 }
 
+static PyObject *synchronize_spin(PyObject *self, PyObject *arg) {
+  (void)self;
+  mgn_env *env = (mgn_env *)PyLong_AsVoidPtr(arg);
+  if (PyErr_Occurred()) return NULL;
+  if (env == NULL) {
+    PyErr_SetString(PyExc_ValueError, "synchronize_spin: null handle");
+    return NULL;
+  }
+  int rc;
+  Py_BEGIN_ALLOW_THREADS rc = mgn_synchronize_spin(env);
+  Py_END_ALLOW_THREADS return PyLong_FromLong(rc);
+}
+
 static PyMethodDef methods[] = {
     {"rollout", (PyCFunction)(void (*)(void))rollout, METH_FASTCALL,
      "mgn_rollout(env, actions, k, traj) -> int (MGN_OK = 0)"},
     {"synchronize", (PyCFunction)synchronize, METH_O, "mgn_synchronize(env) -> int (MGN_OK = 0)"},
+    {"synchronize_spin", (PyCFunction)synchronize_spin, METH_O, "mgn_synchronize_spin(env) -> int (MGN_OK = 0)"},
     {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_mgn_pycall", NULL, -1, methods};

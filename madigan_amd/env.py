@@ -545,15 +545,18 @@ class BatchedEnv:
         launch._keep = (t, actions)
         return launch
 
-    def stream_synchronizer(self):
+    def stream_synchronizer(self, spin: bool = False):
         """A zero-argument callable that waits for the handle's stream
         (mgn_synchronize) -- every launch of the handle is on it -- rather than
-        the whole device (torch.cuda.synchronize); returns the status code."""
+        the whole device (torch.cuda.synchronize); returns the status code.
+        spin: poll the stream instead (mgn_synchronize_spin: the thread
+        busy-waits), for short waits such as an agent loop's per step."""
+        name = "synchronize_spin" if spin else "synchronize"
         pc = L.pycall()
-        if pc is not None and hasattr(pc, "synchronize"):
-            f, hv = pc.synchronize, self.h.value
+        if pc is not None and hasattr(pc, name):
+            f, hv = getattr(pc, name), self.h.value
             return lambda: f(hv)
-        fn, h = self.lib.mgn_synchronize, self.h
+        fn, h = getattr(self.lib, "mgn_" + name), self.h
         return lambda: fn(h)
 
     # ---- Env::setDataSource / checkpoint --------------------------------------------

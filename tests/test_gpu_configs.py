@@ -276,7 +276,8 @@ def test_stats_allgather_rccl_single_rank(gpu):
 def test_rollout_launcher_matches_rollout(gpu, binding, monkeypatch):
     """BatchedEnv.rollout_launcher (bench.py's timed loop) through the CPython
     binding and through ctypes: the same launches as rollout() into the same
-    output buffers, bit-exact against the oracle (C3 shape, 1- and 20-step)."""
+    output buffers, bit-exact against the oracle (C3 shape, 1- and 20-step);
+    the stream waits (polling and plain) through the same binding."""
     from madigan_amd import _lib as L
     if binding == "ctypes":
         monkeypatch.setattr(L, "pycall", lambda: None)
@@ -293,6 +294,10 @@ def test_rollout_launcher_matches_rollout(gpu, binding, monkeypatch):
         out = g.alloc_traj(K, fields=list(STD_FIELDS))
         launch = g.rollout_launcher(out, K)
         assert launch(acts[k0:k0 + K].data_ptr()) == 0
+        # the handle's stream waits (the one-step launch's by polling it,
+        # mgn_synchronize_spin; then the plain one on an idle stream)
+        assert g.stream_synchronizer(spin=(K == 1))() == 0
+        assert g.stream_synchronizer(spin=(K != 1))() == 0
         ref = orc.rollout(a[k0:k0 + K], threads=THREADS)
         o = _host(out)
         for f in ("obs_price", "obs_port", "tprice", "tunits", "tcost"):

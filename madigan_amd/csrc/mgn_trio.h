@@ -1471,7 +1471,6 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       for (int m = 0; m < M; ++m) {
         if (f.valid[m]) {
           const size_t i = kidx(k, sNA, bA) + m;
-          const int x = lx + m;
           if (!RP && !lobs && (om & O_OPR)) ost(ov.obs_price + (kidx(k, sNF, bP) + m), f.P[m]);
           if (!lobs && (om & O_OPT)) ost(ov.obs_port + (kidx(k, sNA1, bO) + 1 + f.asset[m]), portA[m]);
           if (D != 1) {

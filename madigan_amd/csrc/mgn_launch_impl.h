@@ -207,8 +207,8 @@ void launch_trio_one_impl(const StepArgs& a) {
       if constexpr (NS) {
         // the reference's own experiment shape (one OU asset, a window,
         // n-step returns) with the bench's output set (O_WSTD) and the OU
-        // generator at compile time: R1 8192 DDR step launch 230 -> 225 us
-        // (profiles/r05s_nst_ab.txt)
+        // generator at compile time: R1 8192 DDR 9.40e8 -> 9.57e8 env-steps/s
+        // on one box (profiles/r05s_nst_ab.txt)
         if (a.gkind == MGN_SRC_OU && traj_mask(a.out) == O_WSTD) {
           go(k_step_trio<S, R, true, O_WSTD, W, 64, NS, MGN_SRC_OU, false, 1, true>, NS);
           return;

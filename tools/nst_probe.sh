@@ -24,7 +24,7 @@ for r in $(seq 1 ${ROUNDS:-2}); do
     if [ -n "$lib" ]; then L="MADIGAN_LIB_PATH=$lib"; else L=""; fi
     env $L timeout -k 10 300 python bench.py $ARGS --no-cpu-baseline --no-probe --no-k-sweep > $O/${n}_$r.json 2> $O/${n}_$r.err \
       || { echo "$n $r failed"; tail -20 $O/${n}_$r.err; exit 1; }
-    python -c "import json;d=json.loads(open('$O/${n}_$r.json').read().strip().splitlines()[-1]);r=d['roofline'];print('$n $r', 'us/step %.4f'%d.get('kernel_us_per_step', 0), 'launch_us %.2f'%r.get('avg_launch_us', 0), 'value %.4g'%d['value'])"
+    python -c "import json;d=json.loads(open('$O/${n}_$r.json').read().strip().splitlines()[-1]);r=d['roofline'];print('$n $r', 'us/step %.4f'%d.get('kernel_us_per_step', 0), 'launch_us %.2f'%r.get('avg_launch_us', 0), 'step_launch_us %.2f'%d.get('step_launch_avg_us', 0), 'value %.4g'%d['value'])"
   done
 done
 echo "$O done"

@@ -324,23 +324,28 @@ def test_nstep_generator_prefix_vs_oracle(gpu, A, N, n, shaper):
     close(g.shaper_b.cpu().numpy(), orc.scalar("shaperB"), "B")
 
 
-@pytest.mark.parametrize("extra", [(), ("n_shaped",)])
-def test_nstep_agent_output_sets_bit_identical(gpu, extra):
+@pytest.mark.parametrize("A,N,extra", [(8, 8192, ()), (8, 8192, ("n_shaped",)), (4, 16384, ("n_shaped",)),
+                                        (16, 4096, ())])
+def test_nstep_agent_output_sets_bit_identical(gpu, A, N, extra):
     """The n-step agent loop's output sets (O_STD, and O_STD with the popped
     counts) have instantiations of their own with the output mask at compile
-    time (mgn_launch_impl.h launch_trio_nst): the 8192 x 8 TrendOU n = 20 DDR
-    shape stepped through them equals, bit for bit, the same handle stepped
+    time (mgn_launch_impl.h launch_trio_nst, every 256-lane layout): the
+    8192 x 8 TrendOU n = 20 DDR shape (and 4 / 16 assets on the three-role
+    kernel) stepped through them equals, bit for bit, the same handle stepped
     with every output (the runtime-mask kernel the oracle tests pin), over two
     launches with auto-resets, and the final state matches the oracle."""
+    from madigan_amd import _lib as L
     K = 24
     kw = dict(required_margin=0.02, maintenance_margin=0.25, transaction_cost_rel=0.02,
               unit_size=0.9, auto_reset=1, init_cash=1e5, reward_shaper="DDR",
               adaptation_rate=0.01, nstep_return=20, discount=0.97)
-    src = trendou_sources(8, [0.2, 2, 6, 0.05, 0.2, 5.0, 0.15, 0.3, 0.2, 0.99])
+    src = trendou_sources(A, [0.2, 2, 6, 0.05, 0.2, 5.0, 0.15, 0.3, 0.2, 0.99])
     std = ("reward", "shaped", "done", "obs_price", "obs_port", "timestamp", "tprice", "tunits", "tcost",
            "risk", "margin_call") + extra
-    g, orc = make_pair(src, 8192, **kw)
-    h, _ = make_pair(src, 8192, **kw)
+    g, orc = make_pair(src, N, **kw)
+    h, _ = make_pair(src, N, **kw)
+    for e in (g, h):  # (16 assets with n-step: the automatic schedule takes the two-role kernel)
+        L.check(e.lib.mgn_set_schedule(e.h, L.SCHED_TRIO), e.h)
     acts = g.generate_actions(2 * K, seed=23)
     ends = 0
     for half in range(2):

@@ -334,9 +334,69 @@ def kernel_name(env, A: int) -> str:
     return f"mgn::k_step<{m}, {apad // m}, {rq1}, {nst}>"
 
 
+def free_port() -> int:
+    """A free TCP port on 127.0.0.1 for the ranks' rendezvous."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv, backend: str) -> int:
+    """`bench.py --gpus N` without a launcher: start N child ranks of this
+    script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR 127.0.0.1 /
+    MASTER_PORT in their environment, one process per GPU), and wait.  This
+    process never touches the GPU (no HIP call: it only counts devices, which
+    does not initialise the runtime on this image) and never execs; rank 0
+    prints the JSON line on the inherited stdout.  When a rank fails, the
+    others are ended (by their own PIDs: the survivors would wait in a
+    collective) and the worst exit status is returned."""
+    if backend == "nccl":
+        import torch  # device count only (no runtime initialisation)
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py --gpus {n}: {have} GPU(s) visible; one rank per GPU needs {n} "
+                  "(--dist-backend gloo lets ranks share a GPU)", file=sys.stderr)
+            return 2
+    port = free_port()
+    base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = []
+    every_rank = "--rank-probe" in argv  # (the test hook: every rank reports)
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=None if r == 0 or every_rank else subprocess.DEVNULL))
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        if any(rc not in (None, 0) for rc in rcs):
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    try:
+                        rcs[i] = p.wait(timeout=20)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[i] = p.wait()
+            break
+        time.sleep(0.05)
+    bad = [abs(rc) for rc in rcs if rc]
+    return max(bad) if bad else 0
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one process per GPU); without a launcher's WORLD_SIZE, N > 1 starts "
+                         "N child ranks of this script itself (spawn_ranks)")
+    ap.add_argument("--rank-probe", action="store_true",
+                    help="test hook: each rank prints its rank / world as JSON and exits before any "
+                         "GPU call")
     ap.add_argument("--steps", type=int, default=2048)
     ap.add_argument("--warmup", type=int, default=256)
     ap.add_argument("--fuse", type=int, default=256)
@@ -380,6 +440,20 @@ def main():
                          "(the host waits by spinning)")
     args = ap.parse_args()
 
+    # ranks: a launcher (torch.distributed.run) sets WORLD_SIZE; without one,
+    # --gpus N > 1 starts the N ranks here, before anything touches the GPU
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:], args.dist_backend))
+    if world_env is not None and int(world_env) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world_env} ranks")
+    if args.rank_probe:
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": int(world_env or 1),
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                          "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}),
+              flush=True)
+        return
+
     import torch
     import torch.distributed as dist
     if args.sched_spin:
@@ -417,7 +491,9 @@ def main():
     from madigan_amd import _lib as L
     lib, h = env.lib, env.h
     total = args.warmup + args.steps
-    actions = env.generate_actions(total, seed=0x6D6164)
+    # rows [total, total + steps): the kernel-timing launches after the timed
+    # region (the same launch plan on the next rows)
+    actions = env.generate_actions(total + args.steps, seed=0x6D6164)
     traj = env.alloc_traj(F, fields=[f for f in ("reward", "shaped", "done", "obs_price", "obs_port",
                                                  "timestamp", "tprice", "tunits", "tcost", "risk",
                                                  "margin_call")])
@@ -460,18 +536,21 @@ def main():
         return rc
 
     warm, timed = plan(0, args.warmup), plan(args.warmup, total)
+    probe_plan = plan(total, total + args.steps)
     # the handle's stream (every launch is on it); --wait spin polls it
     sync = env.stream_synchronizer(spin=args.wait == "spin")
     # kernel durations: HIP events around each step launch on the handle's
-    # stream (mgn_set_timing; pooled events, created during the warmup)
+    # stream (mgn_set_timing; pooled events, created during the warmup) -- on
+    # the kernel-timing launches after the timed region only: the timed
+    # region issues the product path exactly as a caller does, with no events
     tmode = 2 if args.timing == "launch" else 1
     L.check(lib.mgn_set_timing(h, tmode), h)
     L.check(run(warm, "warmup"), h)
     torch.cuda.synchronize()
+    L.check(lib.mgn_set_timing(h, 0), h)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    L.check(lib.mgn_set_timing(h, tmode), h)
     t0 = time.perf_counter()
     rc = run(timed, "timed")
     # the closing wait is on the handle's stream, the only one the steps use
@@ -498,6 +577,14 @@ def main():
             t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # the step kernel's duration: the timed region's launch plan once more,
+    # right after it, on the next action rows, with the launches' own events
+    L.check(lib.mgn_set_timing(h, tmode), h)
+    tp = time.perf_counter()
+    L.check(run(probe_plan, "probe"), h)
+    L.check(sync(), h)
+    probe_s = time.perf_counter() - tp
+    torch.cuda.synchronize()
     tm = (C.c_double * 4)()
     L.check(lib.mgn_get_timing(h, tm), h)
     L.check(lib.mgn_set_timing(h, 0), h)
@@ -510,7 +597,7 @@ def main():
     fused = bytes_per_env_step(A, steps_per_launch, env.D)
     value = world * N * args.steps / elapsed
     episodes = int(gathered[:, 3].sum().item())
-    age = total  # steps the handle has run
+    age = total + args.steps  # steps the handle has run
 
     # after the timed region, rank 0 only: the same handle continues on fresh
     # actions (T_ACT rows, each launch on the next rows, as an agent loop's
@@ -630,7 +717,8 @@ def main():
                 "bytes_note": "SURVEY 8d algorithmic bytes per env-step (C3: 8 x (113 + 48) + 105): "
                               "state r/w + actions + outputs per step",
                 "units_per_launch": units_per_launch, "avg_launch_us": avg_launch_s * 1e6,
-                "timing": ("HIP events recorded by the step launch (hipExtLaunchKernel start / stop)"
+                "timing": ("HIP events recorded by the step launch (hipExtLaunchKernel start / stop), "
+                           "on the timed plan repeated right after the timed region"
                            if args.timing == "launch" else "HIP marker events around the step launch"),
                 "fused_bytes_per_env_step": fused,
                 "fused_achieved_GBs": units_per_launch * fused / avg_launch_s / 1e9,
@@ -670,7 +758,7 @@ def main():
             "config": {"workload": "C3: TrendOU x8 assets per env, slippage 1e-4 + 2% cost broker, "
                                    "DDR eta=.001 n=1, discrete actions via action_to_transaction, "
                                    "auto-reset",
-                       "n_envs_per_gpu": N, "n_assets": A, "window": 0,
+                       "n_envs_per_gpu": N, "n_envs_total": world * N, "n_assets": A, "window": 0,
                        "steps_per_launch": steps_per_launch,
                        "assets_per_lane": int(lib.mgn_get_layout(h)),
                        "schedule": SCHED_NAMES[int(lib.mgn_get_schedule(h))],
@@ -678,6 +766,14 @@ def main():
                                       + (f", {args.dist_backend}" if world > 1 else "")},
             "roofline": roof,
             "kernel_us_per_step": avg_launch_s * 1e6 / steps_per_launch,
+            "timed_region_us_per_launch": elapsed * 1e6 / max(n_launch, 1),
+            "kernel_timing": {
+                "launches": n_launch, "avg_launch_us": avg_launch_s * 1e6,
+                "region_us_with_events": probe_s * 1e6,
+                "note": "the timed region issues the product path with no timing events; the kernel "
+                        "figure (roofline.avg_launch_us) comes from the same launch plan issued right "
+                        "after it on the next action rows, each launch recording its own HIP events "
+                        "(region_us_with_events: that plan's wall time, events included)"},
             "episodes_completed": episodes,
             "stats_allgather_us": allgather_us,
             "allgather_path": allgather_path,
@@ -869,7 +965,8 @@ def windowed(args, world, rank, dev):
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": desc, "n_envs_per_gpu": N, "n_assets": A, "n_feats": env.F,
+            "config": {"workload": desc, "n_envs_per_gpu": N, "n_envs_total": world * N, "n_assets": A,
+                       "n_feats": env.F,
                        "window": W, "steps_per_launch": Kf, "nstep": env.nstep,
                        "schedule": SCHED_NAMES[int(lib.mgn_get_schedule(h))],
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},

@@ -89,18 +89,20 @@ __device__ __forceinline__ bool trio_exit(int j, int K, const int32_t& more) {
   return !__builtin_amdgcn_readfirstlane(more);
 }
 
-// The finish role's done test of the step L ran in the previous iteration
-// (Env.h:216-218), on the records it reads -- the ledger after the orders,
-// the tick's prices, cash, the price-independent sums and the refused-order
-// flag: the same operands and operations, so the same answer, wherever
-// another role needs it (one-step launches, TAIL_EXACT)
+// The done test of the step L ran in the previous iteration (Env.h:216-218),
+// on the records -- the ledger after the orders, the tick's prices, cash, the
+// price-independent sums and the refused-order flag.  The ONE definition:
+// the finish role's own test, and (one-step launches, TAIL_EXACT) the
+// generator's and the ledger's copies of it, which must agree with the
+// finish role's reset flag -- a term added here reaches all three.  q and
+// curEq: the post-tick sums and equity (the finish role's reward reads them)
 template <int M, int S, bool ONE>
 __device__ __forceinline__ bool rec_done(const double (&Lr)[M], const double (&P)[M], double cashv, double ml,
-                                         double shv, double b, bool any_mc, const KParams& p, double& curEq) {
+                                         double shv, double b, bool any_mc, const KParams& p, Sums& q,
+                                         double& curEq) {
   double tlp[M];
 #pragma unroll
   for (int m = 0; m < M; ++m) tlp[m] = Lr[m] * P[m];
-  Sums q;
   q.lp = canon<M, S, ONE>(tlp);
   q.ml = ml;
   q.sh = shv;
@@ -698,9 +700,10 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
               Pr[m] = sh.price[prv][lx + m];
             }
             double eq;
+            Sums qd;
             cand = p.auto_reset && (fl & TR_STEP) && !sh.reset[prv][el] &&
                    rec_done<M, S, ONE>(Lr, Pr, sh.rCash[prv][el], sh.rMl[prv][el], sh.rSh[prv][el],
-                                       sh.rB[prv][el], (fl & TR_ANYMC) != 0, p, eq);
+                                       sh.rB[prv][el], (fl & TR_ANYMC) != 0, p, qd, eq);
             tail_it = true;
           }
           if (cand) {
@@ -1025,7 +1028,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         if (K == 1 && j == 1 && live) {
           if (lflags & TR_STEP) {
             double curEq;
-            const bool dn = rec_done<M, S, ONE>(s.L, s.P, cash, sa.ml, sa.sh, sa.b, (lflags & TR_ANYMC) != 0, p, curEq);
+            Sums qd;
+            const bool dn =
+                rec_done<M, S, ONE>(s.L, s.P, cash, sa.ml, sa.sh, sa.b, (lflags & TR_ANYMC) != 0, p, qd, curEq);
             const int ks = k - 1;  // the step's index
 #pragma unroll
             for (int m = 0; m < M; ++m) {
@@ -1301,24 +1306,17 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       }
       const double cashv = cashrec;
       const double prevEq = prevrec;
-      // post-tick sums, equity, reward, done (Env.h:211-223)
+      // post-tick sums, equity, done (rec_done, the one definition), reward
+      // (Env.h:211-223)
       Sums q;
-      {
-        double tlp[M];
-#pragma unroll
-        for (int m = 0; m < M; ++m) tlp[m] = f.L[m] * f.P[m];
-        q.lp = canon<M, S, ONE>(tlp);
-      }
+      double curEq;
+      const bool done = rec_done<M, S, ONE>(f.L, f.P, cashv, sh.rMl[prv][el], sh.rSh[prv][el], sh.rB[prv][el],
+                                            (flags & TR_ANYMC) != 0, p, q, curEq);
       if (j == 1) MGN_IT(55, 2 * TRIO_W);
-      q.ml = sh.rMl[prv][el];
-      q.sh = sh.rSh[prv][el];
-      q.b = sh.rB[prv][el];
-      const double curEq = (cashv + q.lp) - q.b;
       const double ratio = curEq / prevEq;
       const double clampv = (in_kind == IN_SINGLE) ? 0.01 : 0.3;
       const double reward = log_ratio((ratio < clampv) ? clampv : ratio);
       if (j == 1) MGN_IT(56, 2 * TRIO_W);
-      const bool done = (flags & TR_ANYMC) || margin_call(q, cashv, p.mainM) || (curEq < 0.1 * p.init_cash);
       // ledgerNormedFull, agent reward, PPC, shaper (as k_step_duo's finish)
       double ar[M], portA[M];
       // lobs (one-step launches): State is stored by the ledger role; the

@@ -18,20 +18,27 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_bench_two_ranks_gloo_matches_unsharded(gpu, tmp_path):
+@pytest.mark.parametrize("launcher", ["torchrun", "spawn"])
+def test_bench_two_ranks_gloo_matches_unsharded(gpu, tmp_path, launcher):
+    """launcher "spawn": `bench.py --gpus 2` with no launcher starts its two
+    ranks itself (bench.spawn_ranks) -- the form of the driver's scaling run."""
     N, steps, warmup = 512, 1000, 24  # first margin-call dones come after ~500 steps
     dump = str(tmp_path / "stats.npy")
     port = 29600 + os.getpid() % 300
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", str(steps), "--warmup", str(warmup), "--n-envs", str(N),
+    pre = ([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+            "--master-addr", "127.0.0.1", "--master-port", str(port)] if launcher == "torchrun"
+           else [sys.executable])
+    cmd = pre + [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", str(steps), "--warmup", str(warmup), "--n-envs", str(N),
            "--dist-backend", "gloo", "--no-cpu-baseline", "--no-probe", "--dump-stats", dump]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     res = json.loads(line)
     assert res["n_gpus"] == 2 and res["value"] > 0
+    assert res["config"]["n_envs_total"] == 2 * N
     got = np.load(dump)
     assert got.shape == (2 * N, 4)
 

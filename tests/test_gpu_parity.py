@@ -294,7 +294,7 @@ def test_nstep_rollout(gpu, shaper, mode, n):
 
 
 @pytest.mark.parametrize("A,N,n,shaper", [(8, 8192, 20, "DDR"), (16, 4096, 5, "DSR"), (4, 16384, 3, "DDR")])
-def test_nstep_generator_prefix_vs_oracle(gpu, A, N, n, shaper):
+def test_nstep_trio_256lane_vs_oracle(gpu, A, N, n, shaper):
     """n-step aggregation on the 256-lane three-role kernel with one source
     kind (the n = 20 DDR bench shape's instantiation): the finish role's ring
     and pops (every lane of the env evaluates part of a pop's summands, the
@@ -331,9 +331,12 @@ def test_nstep_agent_output_sets_bit_identical(gpu, A, N, extra):
     counts) have instantiations of their own with the output mask at compile
     time (mgn_launch_impl.h launch_trio_nst, every 256-lane layout): the
     8192 x 8 TrendOU n = 20 DDR shape (and 4 / 16 assets on the three-role
-    kernel) stepped through them equals, bit for bit, the same handle stepped
-    with every output (the runtime-mask kernel the oracle tests pin), over two
-    launches with auto-resets, and the final state matches the oracle."""
+    kernel) stepped through them matches the oracle step by step -- every
+    output of the set, the done-flush rows of `shaped` and the popped counts
+    included (ledger / State / responses bitwise, reward rtol 1e-12, shaped
+    rtol 1e-10) -- and equals, bit for bit, the same handle stepped with every
+    output (the runtime-mask kernel), over two launches with auto-resets; the
+    final state matches the oracle."""
     from madigan_amd import _lib as L
     K = 24
     kw = dict(required_margin=0.02, maintenance_margin=0.25, transaction_cost_rel=0.02,
@@ -353,9 +356,23 @@ def test_nstep_agent_output_sets_bit_identical(gpu, A, N, extra):
         o = g.alloc_traj(K, fields=std)
         g.rollout(a, o)
         full = {k: v.cpu().numpy() for k, v in h.rollout(a).items()}
-        orc.rollout(a.cpu().numpy())
+        ref = orc.rollout(a.cpu().numpy())
         for k, v in o.items():
-            assert_bits(v.cpu().numpy(), full[k], f"{k} {extra} {half}")
+            got = v.cpu().numpy()
+            assert_bits(got, full[k], f"{k} {extra} {half}")
+            tag = f"{k} {extra} {half} vs oracle"
+            if k == "shaped":
+                np.testing.assert_allclose(got, ref[k], rtol=1e-10, atol=1e-14, err_msg=tag)
+            elif k == "reward":
+                close(got, ref[k], tag)
+            elif k == "timestamp":
+                assert np.array_equal(got.astype(np.uint64), ref[k]), tag
+            elif got.dtype == np.float64:
+                assert_bits(got, ref[k], tag)
+            else:
+                assert np.array_equal(got, np.asarray(ref[k]).astype(got.dtype)), tag
+        if "n_shaped" in o:
+            assert int(ref["n_shaped"].max()) > 1, "a done flush (several pops in one step)"
         ends += int(full["done"].sum())
     assert ends > 0
     state_check(g, orc, f"nstep output sets {extra}")
@@ -521,9 +538,11 @@ def test_trio_two_slots_bit_identical(gpu, A, src, kw):
                                        (4, 300, 1, dict(reward_shaper="PPC", cosine_temp=0.05))])
 def test_trio_tail_resets_bit_identical(gpu, A, N, K, kw):
     """Short launches whose last step ends episodes (a leveraged, costly
-    broker: auto-resets in most launches): the three-role kernel absorbs such a
-    tail reset after its loop (the generator's candidate reset tick, the fresh
-    Broker) -- every output and the whole state after each launch equal the
+    broker: auto-resets in most launches) on the three-role kernel's
+    runtime-mask instantiations (these shapes take the 64-lane layout, the
+    two-slot layout or the n-step unit, none of which carries the one-step
+    tail reset of launch_trio_agent_k -- test_trio_k1_tail_paths_bit_identical
+    covers that): every output and the whole state after each launch equal the
     two-role kernel's, bit for bit, launch after launch."""
     from madigan_amd import BatchedEnv
     from madigan_amd import _lib as L
@@ -546,6 +565,68 @@ def test_trio_tail_resets_bit_identical(gpu, A, N, K, kw):
             outs.append(o)
         res.append(outs)
     assert sum(int(o["done"].sum()) for o in res[0]) > n_launch // 2, "too few episode ends"
+    for i, (a, b) in enumerate(zip(*res)):
+        for k, v in a.items():
+            if np.asarray(v).dtype == np.float64:
+                assert_bits(b[k], v, f"launch {i} trio vs duo {k}")
+            else:
+                assert np.array_equal(np.asarray(b[k]), np.asarray(v)), f"launch {i} trio vs duo {k}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("A,N,src,fields", [
+    (8, 8192, "ou", "std"), (8, 8192, "mixed", "all"),  # GSLOT: the generator's candidate reset tick
+    (4, 16384, "trendou", "std"), (2, 32768, "trendou", "all"),  # TAIL_EXACT at S = 4 / 2
+    (8, 8192, "trendou", "std")])  # TAIL_EXACT at S = 8 (the C3 agent loop's unit)
+def test_trio_k1_tail_paths_bit_identical(gpu, A, N, src, fields):
+    """One-step launches on launch_trio_agent_k (the 256-lane layout, the agent
+    loop's output sets O_STD / O_ALL at compile time, K1): an episode that
+    ends at the launch's only step is reset inside the launch -- by the
+    generator role's candidate reset tick where its lanes are slot-major (OU
+    or mixed-kind handles, GSLOT) and by every role's own done test (rec_done,
+    TAIL_EXACT) at S = 2 / 4 / 8.  24 launches with episode ends in most of
+    them: every output and the whole state after each launch equal the
+    two-role kernel's bit for bit, and the final state matches the oracle."""
+    from madigan_amd import BatchedEnv
+    from madigan_amd import _lib as L
+    p = [0.2, 2, 6, 0.05, 0.2, 5.0, 0.15, 0.3, 0.2, 0.99]
+    if src == "ou":
+        sources = ou_sources(A)
+    elif src == "mixed":
+        mixed = composite_sources()[:5] + trendou_sources(3, p)
+        sources = [mixed[i % len(mixed)] for i in range(A)]
+    else:
+        sources = trendou_sources(A, p)
+    base = dict(required_margin=0.02, maintenance_margin=0.25, transaction_cost_rel=0.02,
+                slippage_rel=1e-4, unit_size=0.9, auto_reset=True, init_cash=1e5, seed=31,
+                reward_shaper="DDR")
+    std = ["reward", "shaped", "done", "obs_price", "obs_port", "timestamp", "tprice", "tunits", "tcost",
+           "risk", "margin_call"]
+    n_launch = 24
+    res = []
+    for sched in (L.SCHED_DUO, L.SCHED_TRIO):
+        g = BatchedEnv(spec_from_sources(sources), N, **base)
+        L.check(g.lib.mgn_set_schedule(g.h, sched), g.h)
+        acts = g.generate_actions(n_launch, seed=13)
+        outs = []
+        for i in range(n_launch):
+            if fields == "std":
+                o = g.alloc_traj(1, fields=std)
+                g.rollout(acts[i:i + 1], o)
+            else:
+                o = g.rollout(acts[i:i + 1])
+            o = {k: v.cpu().numpy() for k, v in o.items()}
+            for name in ("ledger", "mean_entry", "borrowed", "cash", "prices", "timestamp", "episode_stats",
+                         "shaper_a", "shaper_b", "draw_skip"):
+                o["st_" + name] = getattr(g, name).cpu().numpy()
+            outs.append(o)
+        res.append(outs)
+        if sched == L.SCHED_TRIO:
+            orc = O.OracleBatch(dict(n_envs=N, **base), sources)
+            orc.rollout(acts.cpu().numpy())
+            state_check(g, orc, f"k1 {src} A{A}")
+    ends = [int(o["done"].sum()) for o in res[0]]
+    assert sum(1 for e in ends if e) > n_launch // 2, f"too few launches with episode ends: {ends}"
     for i, (a, b) in enumerate(zip(*res)):
         for k, v in a.items():
             if np.asarray(v).dtype == np.float64:

@@ -60,7 +60,15 @@ def main():
                                 "line_us": line_us, "trace_mean_us": mean, "trace_median_us": med,
                                 "trace_over_line": mean / line_us, "profiled_line_us": get(tline)}
 
-    fig("timed_region_launch", "timed", lambda d: d["roofline"]["avg_launch_us"])
+    # the line's kernel figure comes from the launches after the timed region
+    # ("probe", the timed plan repeated with launch events; older lines timed
+    # the timed launches themselves)
+    kl = "probe" if "probe" in groups else "timed"
+    fig("timed_region_launch", kl, lambda d: d["roofline"]["avg_launch_us"])
+    if kl == "probe":
+        us = groups["timed"]["us"]
+        res["figures_trace_only"] = {"timed_launches_trace_mean_us": statistics.fmean(us),
+                                     "note": "the timed region's own launches (no events) in the trace"}
     for age in line.get("episode_age", {}):
         key = age if age in tline.get("episode_age", {}) else None
         if key:

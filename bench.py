@@ -277,10 +277,11 @@ def workload_env(name, N, A, rank, dev, **extra):
         shaper = extra.pop("shaper", "DDR")
         sx = {"sortino_exp": 1.1} if shaper.startswith("sortino") else {}
         spec = ou_spec([10.0], [0.08], [0.04])
+        pop = extra.pop("nstep_pop", "exact")
         return (BatchedEnv(spec, N, device=dev, seed=seed, env_offset=off, reward_shaper=shaper,
-                           nstep_return=20, discount=0.99, reward_mode="agent_sum", **sx, **base),
+                           nstep_return=20, discount=0.99, reward_mode="agent_sum", nstep_pop=pop, **sx, **base),
                 f"R1: OU x1 (mu 10, theta .08, phi .04), W=64 window (norm none), n=20 returns "
-                f"(discount .99) of the summed agent reward, {shaper} eta=.001{' exp 1.1' if sx else ''}, "
+                f"(discount .99, {pop} pop) of the summed agent reward, {shaper} eta=.001{' exp 1.1' if sx else ''}, "
                 "2% cost, unit .05 avM, auto-reset (scripts/ou_ddr_.001_nstep20.yaml)", 64)
     if name == "C5":
         import tempfile
@@ -413,6 +414,9 @@ def main():
                     help="C3 diagnostics: pin the step kernel (results are bit-identical)")
     ap.add_argument("--nstep", type=int, default=1,
                     help="C3 diagnostics: n-step aggregation (nstep_return), not the headline")
+    ap.add_argument("--nstep-pop", default="exact", choices=["exact", "running"],
+                    help="n-step lines (C3 --nstep > 1, R1): the exact pop or the running-sum pop "
+                         "(MGN_NSTEP_POP_RUNNING, within 1e-6 of the exact pop)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-k-sweep", dest="k_sweep", action="store_false",
                     help="skip the K = 1 / 16 / 256 launch-length block of the line")
@@ -479,7 +483,7 @@ def main():
     if args.workload != "C3":
         return windowed(args, world, rank, dev)
     N, A, F = args.n_envs, args.assets, args.fuse
-    extra = dict(nstep_return=args.nstep, discount=0.99) if args.nstep > 1 else {}
+    extra = dict(nstep_return=args.nstep, discount=0.99, nstep_pop=args.nstep_pop) if args.nstep > 1 else {}
     env, _, _ = workload_env("C3", N, A, rank, dev, **extra)
     if args.layout:
         env.lib.mgn_set_layout(env.h, args.layout)
@@ -706,7 +710,8 @@ def main():
     if rank == 0:
         K = int(round(steps_per_launch))
         # (n-step handles have PMC entries of their own: the pops' rows)
-        workload = f"C3_trendou_{N}x{A}" + (f"_n{args.nstep}" if args.nstep > 1 else "") + f"_fuse{K}"
+        workload = (f"C3_trendou_{N}x{A}" + (f"_n{args.nstep}" if args.nstep > 1 else "")
+                    + ("_running" if args.nstep > 1 and args.nstep_pop == "running" else "") + f"_fuse{K}")
         traffic, traffic_key = load_pmc_traffic(workload)
         probe = bandwidth_probe(dev) if args.probe else None
         roof = {"bound": "hbm", "achieved": achieved_gbs, "peak": PEAK_HBM_GBS,
@@ -756,8 +761,11 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
             "config": {"workload": "C3: TrendOU x8 assets per env, slippage 1e-4 + 2% cost broker, "
-                                   "DDR eta=.001 n=1, discrete actions via action_to_transaction, "
-                                   "auto-reset",
+                                   + (f"DDR eta=.001 n={args.nstep} (discount .99, {args.nstep_pop} pop; "
+                                      "a diagnostic line, not the headline)" if args.nstep > 1 else
+                                      "DDR eta=.001 n=1")
+                                   + ", discrete actions via action_to_transaction, auto-reset",
+                       "nstep": args.nstep, "nstep_pop": args.nstep_pop if args.nstep > 1 else None,
                        "n_envs_per_gpu": N, "n_envs_total": world * N, "n_assets": A, "window": 0,
                        "steps_per_launch": steps_per_launch,
                        "assets_per_lane": int(lib.mgn_get_layout(h)),
@@ -861,7 +869,8 @@ def windowed(args, world, rank, dev):
     if wl == "C2" and args.win_assets:
         # diagnostic: OU windows at another asset count, at --n-envs envs
         N, A = args.n_envs, args.win_assets
-    env, desc, W = workload_env(wl, N, A, rank, dev, **({"shaper": args.shaper} if wl == "R1" else {}))
+    env, desc, W = workload_env(wl, N, A, rank, dev, **({"shaper": args.shaper, "nstep_pop": args.nstep_pop}
+                                                         if wl == "R1" else {}))
     Kf = max(1, min(args.fuse, args.win_fuse))
     n_warm = max(1, -(-args.warmup // Kf))
     n_time = max(1, -(-args.steps // Kf))
@@ -968,6 +977,7 @@ def windowed(args, world, rank, dev):
             "config": {"workload": desc, "n_envs_per_gpu": N, "n_envs_total": world * N, "n_assets": A,
                        "n_feats": env.F,
                        "window": W, "steps_per_launch": Kf, "nstep": env.nstep,
+                       "nstep_pop": args.nstep_pop if env.nstep > 1 else None,
                        "schedule": SCHED_NAMES[int(lib.mgn_get_schedule(h))],
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MGN_ABI_VERSION 8
+#define MGN_ABI_VERSION 9
 #define MGN_MAX_ASSETS 64
 #define MGN_MAX_NSTEP 64
 
@@ -77,6 +77,18 @@ enum { MGN_SRC_EXTERNAL = 0, MGN_SRC_SINE = 1, MGN_SRC_OU = 2, MGN_SRC_TRENDOU =
        MGN_SRC_SINEADDER = 11, MGN_SRC_SINEDYNAMIC = 12, MGN_SRC_SINEDYNTREND = 13 };
 #define MGN_SRC_PARAMS 64   /* doubles of parameters per asset */
 #define MGN_AUX_WIDTH 24    /* doubles of extra source state per asset (views.aux) */
+
+/* n-step pops (mgn_config.nstep_pop).  EXACT: every pop re-evaluates the
+ * buffer's summands with the current shaper state and sums them in entry order
+ * (nstep_buffer.py:62-91, 128-162 as written; ledger / State bit-exact, pops
+ * within rtol 1e-10 of the reference).  RUNNING: DSR / DDR / PPC / none pops
+ * formed from per-env discounted running sums of the buffer's entries, O(1)
+ * per pop, within north_star's 1e-6 relative of the exact pop (re-formed from
+ * the buffer every n pops); the shaper state A / B stays exact.  A permission,
+ * not a requirement: kernels or shapers without the running form (the naive
+ * shapers, per-asset rewards, the two-role and single-role schedules, or
+ * gamma^n < 1e-3) pop exactly. */
+enum { MGN_NSTEP_POP_EXACT = 0, MGN_NSTEP_POP_RUNNING = 1 };
 
 /* reward shapers (nstep_buffer.py:378-408): DSR :30-98, DDR :101-169, PPC = cosine_port_shaper
  * :182-204, SHARPE = sharpe_shaper :207-239, SORTINO_A/B = sortino_shaperA/B :242-312 */
@@ -146,7 +158,7 @@ typedef struct {
   double unit_size;            /* unit_size_proportion_avM */
   int32_t nstep;               /* n-step return length (nstep_return), 1..MGN_MAX_NSTEP;
                                   NStepBuffer semantics, nstep_buffer.py:315-356 */
-  int32_t pad2_;
+  int32_t nstep_pop;           /* MGN_NSTEP_POP_*: how an n-step pop is evaluated (ABI 9) */
   double discount;             /* gamma of the n-step aggregation */
   int32_t n_feats;             /* F = State.price width: n_assets for the generators
                                   (0 = n_assets); the feature columns of a replay source */

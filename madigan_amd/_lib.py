@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmadigan_hip.so")
 MAX_ASSETS = 64
-ABI_VERSION = 8
+ABI_VERSION = 9
 SRC_PARAMS = 64
 AUX_WIDTH = 24
 MAX_NSTEP = 64
@@ -25,6 +25,7 @@ GREEN, INSUFF_MARGIN, MARGIN_CALL, BLOWN_OUT = range(4)
  SRC_SAWTOOTH, SRC_TRIANGLE, SRC_OUPAIR, SRC_SINEADDER, SRC_SINEDYNAMIC, SRC_SINEDYNTREND) = range(14)
 (SHAPER_NONE, SHAPER_DSR, SHAPER_DDR, SHAPER_PPC, SHAPER_SHARPE, SHAPER_SORTINO_A,
  SHAPER_SORTINO_B) = range(7)
+NSTEP_POP_EXACT, NSTEP_POP_RUNNING = 0, 1  # mgn_config.nstep_pop (ABI 9)
 REWARD_ENV_LOG, REWARD_AGENT_SUM, REWARD_AGENT_PER_ASSET = range(3)
 (NORM_NONE, NORM_LOG, NORM_LOOKBACK, NORM_STANDARD_NORMAL, NORM_LOOKBACK_LOG,
  NORM_LOG_STANDARD_NORMAL) = range(6)
@@ -52,7 +53,7 @@ class Config(C.Structure):
         ("cosine_temp", C.c_double), ("desired_portfolio", C.c_double * (MAX_ASSETS + 1)),
         ("window", C.c_int32), ("norm_type", C.c_int32), ("auto_reset", C.c_int32),
         ("action_atoms", C.c_int32), ("unit_size", C.c_double),
-        ("nstep", C.c_int32), ("pad2_", C.c_int32), ("discount", C.c_double),
+        ("nstep", C.c_int32), ("nstep_pop", C.c_int32), ("discount", C.c_double),
         ("n_feats", C.c_int32), ("pad3_", C.c_int32), ("sortino_exp", C.c_double),
         ("aux", C.c_int32), ("pad4_", C.c_int32),
     ]

@@ -410,6 +410,9 @@ def norm_code(name) -> int:
     return NORM_CODES[name]
 
 
+NSTEP_POPS = {"exact": L.NSTEP_POP_EXACT, "running": L.NSTEP_POP_RUNNING}
+
+
 def build_config(spec: SourceSpec, *, n_envs: int, init_cash: float = 1_000_000.0,
                  required_margin: float = 0.0, maintenance_margin: float = 0.0,
                  slippage_rel: float = 0.0, slippage_abs: float = 0.0,
@@ -418,7 +421,8 @@ def build_config(spec: SourceSpec, *, n_envs: int, init_cash: float = 1_000_000.
                  cosine_temp: float = 0.0, desired_portfolio=None, window: int = 0,
                  norm_type=None, auto_reset: bool = False, action_atoms: int = 3,
                  unit_size: float = 0.05, seed: int = 0, env_offset: int = 0,
-                 nstep_return: int = 1, discount: float = 0.99, sortino_exp=None):
+                 nstep_return: int = 1, discount: float = 0.99, sortino_exp=None,
+                 nstep_pop: str = "exact"):
     A = spec.n_assets
     if A < 1:
         raise ValueError(f"n_assets must be >= 1, got {A}")
@@ -457,6 +461,13 @@ def build_config(spec: SourceSpec, *, n_envs: int, init_cash: float = 1_000_000.
         raise ConfigError(f"nstep_return must be in [1, {L.MAX_NSTEP}] (MGN_MAX_NSTEP), got {nstep_return}")
     c.nstep = int(nstep_return)  # config.py:126 (Agent/Model spec)
     c.discount = float(discount)  # config.py:154
+    # how an n-step pop is evaluated (include/madigan_amd.h MGN_NSTEP_POP_*):
+    # "exact" re-evaluates the buffer's summands as nstep_buffer.py does;
+    # "running" forms DSR / DDR / PPC / none pops from discounted running sums
+    # (O(1) per pop, within 1e-6 of the exact pop) where the kernel has them
+    if nstep_pop not in NSTEP_POPS:
+        raise ConfigError(f"nstep_pop must be one of {sorted(NSTEP_POPS)}, got {nstep_pop!r}")
+    c.nstep_pop = NSTEP_POPS[nstep_pop]
     c.n_feats = int(spec.n_feats) if spec.replay else 0
     if c.shaper in (L.SHAPER_SORTINO_A, L.SHAPER_SORTINO_B):
         if sortino_exp is None:  # shaper_config["sortino_exp"] (nstep_buffer.py:392)

@@ -203,6 +203,10 @@ int validate(const mgn_config* c, const mgn_asset_source* s, std::string& msg) {
     msg = "nstep_return must be in [1, 64]";
     return MGN_ERR_CONFIG;
   }
+  if (c->nstep_pop != MGN_NSTEP_POP_EXACT && c->nstep_pop != MGN_NSTEP_POP_RUNNING) {
+    msg = "unknown nstep_pop";
+    return MGN_ERR_CONFIG;
+  }
   int n_replay = 0;
   for (int i = 0; i < c->n_assets; ++i) n_replay += s[i].kind == MGN_SRC_REPLAY;
   if (n_replay != 0 && n_replay != c->n_assets) {
@@ -289,6 +293,16 @@ mgn::KParams kparams(const mgn_env* e) {
   p.src = e->src_dev; p.src_g = e->src_dev; p.target = e->target_dev;
   p.nstep = c.nstep; p.nring = v.nstep_ring; p.nlen = v.nstep_len; p.nhead = v.nstep_head;
   p.disc = e->disc_dev;
+  // MGN_NSTEP_POP_RUNNING: the shapers with a running-sum pop, scalar
+  // rewards, and a discount whose slides stay well conditioned (the sums'
+  // rounding grows by 1/gamma per pop between the re-sums every n pops)
+  p.nst_run = (c.nstep_pop == MGN_NSTEP_POP_RUNNING && c.nstep > 1 && e->D == 1 &&
+               (c.shaper == MGN_SHAPER_DSR || c.shaper == MGN_SHAPER_DDR || c.shaper == MGN_SHAPER_PPC ||
+                c.shaper == MGN_SHAPER_NONE) &&
+               c.discount > 0. && std::pow(c.discount, (double)c.nstep) >= 1e-3)
+                  ? 1
+                  : 0;
+  p.nst_rg = p.nst_run ? 1.0 / c.discount : 0.;
   p.rcur = e->v.replay_cursor;
   p.aux = e->v.aux;
   const auto& hb = e->hb[e->hcur];

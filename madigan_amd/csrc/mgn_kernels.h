@@ -63,6 +63,8 @@ struct KParams {
   const double *target;         // (A+1)
   // NStepBuffer (n > 1): ring (N,n,D), fill count / oldest index (N), gamma^i (n)
   int nstep;
+  int nst_run;    // MGN_NSTEP_POP_RUNNING granted (mgn_api.hip kparams): the three-role running-sum pop
+  double nst_rg;  // 1 / gamma (nst_run)
   double *nring;
   int32_t *nlen, *nhead;
   const double *disc;
@@ -1211,6 +1213,102 @@ __device__ __forceinline__ double pop_term(int shaper, double r, double A, doubl
   if (shaper == MGN_SHAPER_DSR) f = dsr_one_den(r, A, B, c.dden);
   else if (shaper == MGN_SHAPER_DDR) f = ddr_one_pre(r, A, B, c.q);
   return disc_k * f;
+}
+
+// The running-sum n-step pop (MGN_NSTEP_POP_RUNNING; within north_star's 1e-6
+// of the exact pop): per env, the buffer's discounted sums
+// sum_k gamma^k {1, r_k, r_k^2}, split by DDR's sign test (r > 0 / else).
+// Every DSR / DDR / PPC / none pop is a function of them
+// (nstep_buffer.py:62-91, 128-162, 182-204, 23-27):
+//   DSR   sum_k g^k [B (r_k - A) - A (r_k^2 - B) / 2]
+//           = B (S_r - A S_1) - A/2 (S_rr - B S_1)
+//   DDR   sum_{r>0} g^k (r_k - A/2) / dpos
+//           + sum_{r<=0} g^k [B (r_k - A/2) - A r_k^2 / 2] / dneg
+//   PPC / none  S_r over the stored values
+// An entry appended at position L-1 enters at weight g^(L-1); a pop removes
+// the oldest (weight g^0 = 1) and divides the rest by g (every entry moves
+// one position forward), so a pop costs O(1) instead of L summands and an
+// ordered sum.  The slides' rounding grows by 1/g per pop, so the sums are
+// re-formed from the buffer every n pops and the host grants this pop only
+// where g^n >= 1e-3 (mgn_api.hip kparams): drift <= n eps g^-n of the sums'
+// magnitude, < 1e-11 at n = 64.
+struct NstRun {
+  double p1, pr, prr, n1, nr, nrr;
+};
+__device__ __forceinline__ void nrun_zero(NstRun& s) { s.p1 = s.pr = s.prr = s.n1 = s.nr = s.nrr = 0.; }
+__device__ __forceinline__ void nrun_add(NstRun& s, double r, double w) {
+  const double wr = w * r, wrr = wr * r;
+  const bool pos = r > 0.;
+  s.p1 += pos ? w : 0.;
+  s.pr += pos ? wr : 0.;
+  s.prr += pos ? wrr : 0.;
+  s.n1 += pos ? 0. : w;
+  s.nr += pos ? 0. : wr;
+  s.nrr += pos ? 0. : wrr;
+}
+// the oldest entry r0 leaves; the rest move one position forward
+__device__ __forceinline__ void nrun_slide(NstRun& s, double r0, double rg) {
+  nrun_add(s, r0, -1.0);
+  s.p1 *= rg;
+  s.pr *= rg;
+  s.prr *= rg;
+  s.n1 *= rg;
+  s.nr *= rg;
+  s.nrr *= rg;
+}
+// every lane of an S-lane env segment holds part of the sums -> all of them
+template <int S>
+__device__ __forceinline__ void nrun_allsum(NstRun& s) {
+  s.p1 = seg_sum<S>(s.p1);
+  s.pr = seg_sum<S>(s.pr);
+  s.prr = seg_sum<S>(s.prr);
+  s.n1 = seg_sum<S>(s.n1);
+  s.nr = seg_sum<S>(s.nr);
+  s.nrr = seg_sum<S>(s.nrr);
+}
+// A pop of a buffer of len entries, split into what the sums give (`base`:
+// formed ahead of the step's reward -- the shaper state A, B and len are
+// known when the step's evaluation starts) and the term of the entry v
+// appended at weight w (nrun_fin).  The quotients by len and by the
+// reward-independent denominators are one refined reciprocal per class.
+struct NstPre {
+  double base, cp, cn, hA, A, B;
+};
+__device__ __forceinline__ NstPre nrun_pre(int shaper, const NstRun& s, int len, double A, double B) {
+  NstPre q;
+  q.A = A;
+  q.B = B;
+  q.hA = A / 2;
+  q.cp = q.cn = 0.;
+  if (shaper == MGN_SHAPER_DSR) {
+    const double S1 = s.p1 + s.n1, Sr = s.pr + s.nr, Srr = s.prr + s.nrr;
+    q.cp = rt_rcp(dsr_den(A, B) * len);
+    q.base = q.cp * (B * (Sr - A * S1) - q.hA * (Srr - B * S1));
+  } else if (shaper == MGN_SHAPER_DDR) {
+    const DdrPre d = ddr_pre(A, B);
+    q.cp = rt_rcp(d.dpos * len);
+    q.cn = rt_rcp(d.dneg * len);
+    q.base = q.cp * (s.pr - q.hA * s.p1) + q.cn * (B * (s.nr - q.hA * s.n1) - q.hA * s.nrr);
+  } else {
+    q.base = s.pr + s.nr;
+  }
+  return q;
+}
+// the pop with v appended at weight w; DSR / DDR: clip(sum / len) as
+// __main_func__ (nstep_buffer.py:78, :144)
+__device__ __forceinline__ double nrun_fin(int shaper, const NstPre& q, double v, double w) {
+  if (shaper == MGN_SHAPER_DSR) return clip1(q.base + q.cp * (w * (q.B * (v - q.A) - q.hA * (v * v - q.B))));
+  if (shaper == MGN_SHAPER_DDR) {
+    const bool pos = v > 0.;
+    const double t = pos ? (v - q.hA) : (q.B * (v - q.hA) - q.hA * (v * v));
+    return clip1(q.base + (pos ? q.cp : q.cn) * (w * t));
+  }
+  return q.base + w * v;
+}
+// the pop of a buffer of len entries from its sums alone
+__device__ __forceinline__ double nrun_pop(int shaper, const NstRun& s, int len, double A, double B) {
+  const NstPre q = nrun_pre(shaper, s, len, A, B);
+  return (shaper == MGN_SHAPER_DSR || shaper == MGN_SHAPER_DDR) ? clip1(q.base) : q.base;
 }
 
 // naive shapers (nstep_buffer.py:207-312), benchmark 0.  x**e and x**(1/e) as

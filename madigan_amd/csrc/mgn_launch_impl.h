@@ -144,8 +144,8 @@ struct TrioGo {
 // are built without machine-level LICM (madigan_amd/build.py UNIT_FLAGS: with
 // it, the loop-invariant constants hoisted out of the step loop spilled
 // 87-195 VGPRs of the 256-lane n-step kernels)
-template <int S>
-void launch_trio_nst(const StepArgs& a) {
+template <int S, int NS>
+void launch_trio_nst_k(const StepArgs& a) {
   const bool small = (long long)a.p.N * S < 256LL * TRIO_W;
   const bool disc = a.in_kind == IN_DISCRETE;
   const TrioGo<S> go{a, small};
@@ -155,17 +155,17 @@ void launch_trio_nst(const StepArgs& a) {
     // every batch -- the finish role's window rows and n-step pops need more
     // than the 256-lane layout's 168 registers (it spilled 8)
     const TrioGo<S> go64{a, true};
-    if (a.p.reqm_one) go64(k_step_trio<S, true, true, 0, true, 64, true>, true);
-    else go64(k_step_trio<S, false, true, 0, true, 64, true>, true);
+    if (a.p.reqm_one) go64(k_step_trio<S, true, true, 0, true, 64, NS>, true);
+    else go64(k_step_trio<S, false, true, 0, true, 64, NS>, true);
     return;
   }
   if (small) {
     if (disc) {
-      if (a.p.reqm_one) goN(k_step_trio<S, true, true, 0, false, 64, true>);
-      else goN(k_step_trio<S, false, true, 0, false, 64, true>);
-    } else {
-      if (a.p.reqm_one) goN(k_step_trio<S, true, false, 0, false, 64, true>);
-      else goN(k_step_trio<S, false, false, 0, false, 64, true>);
+      if (a.p.reqm_one) goN(k_step_trio<S, true, true, 0, false, 64, NS>);
+      else goN(k_step_trio<S, false, true, 0, false, 64, NS>);
+    } else if constexpr (NS == 1) {
+      if (a.p.reqm_one) goN(k_step_trio<S, true, false, 0, false, 64, NS>);
+      else goN(k_step_trio<S, false, false, 0, false, 64, NS>);
     }
   } else if (disc && a.gkind == MGN_SRC_TRENDOU) {
     // the agent loop's output sets at compile time (O_STD, with the popped
@@ -173,20 +173,28 @@ void launch_trio_nst(const StepArgs& a) {
     // against 3.67 us/step (profiles/r05s_nst_ab.txt)
     auto pick = [&](auto omc) {
       constexpr uint32_t OM = decltype(omc)::value;
-      if (a.p.reqm_one) goN(k_step_trio<S, true, true, OM, false, TRIO_W, true, MGN_SRC_TRENDOU>);
-      else goN(k_step_trio<S, false, true, OM, false, TRIO_W, true, MGN_SRC_TRENDOU>);
+      if (a.p.reqm_one) goN(k_step_trio<S, true, true, OM, false, TRIO_W, NS, MGN_SRC_TRENDOU>);
+      else goN(k_step_trio<S, false, true, OM, false, TRIO_W, NS, MGN_SRC_TRENDOU>);
     };
     const uint32_t om = traj_mask(a.out);
     if (om == O_STD) pick(std::integral_constant<uint32_t, O_STD>{});
     else if (om == O_STDN) pick(std::integral_constant<uint32_t, O_STDN>{});
     else pick(std::integral_constant<uint32_t, 0u>{});
   } else if (disc) {
-    if (a.p.reqm_one) goN(k_step_trio<S, true, true, 0, false, TRIO_W, true>);
-    else goN(k_step_trio<S, false, true, 0, false, TRIO_W, true>);
-  } else {
-    if (a.p.reqm_one) goN(k_step_trio<S, true, false, 0, false, TRIO_W, true>);
-    else goN(k_step_trio<S, false, false, 0, false, TRIO_W, true>);
+    if (a.p.reqm_one) goN(k_step_trio<S, true, true, 0, false, TRIO_W, NS>);
+    else goN(k_step_trio<S, false, true, 0, false, TRIO_W, NS>);
+  } else if constexpr (NS == 1) {
+    if (a.p.reqm_one) goN(k_step_trio<S, true, false, 0, false, TRIO_W, NS>);
+    else goN(k_step_trio<S, false, false, 0, false, TRIO_W, NS>);
   }
+}
+// the running-sum pop (NS = 2, nrun_pop) where the host granted it
+// (KParams::nst_run) and the steps are discrete (the agent loop); the exact
+// pop (NS = 1) otherwise
+template <int S>
+void launch_trio_nst(const StepArgs& a) {
+  if (a.p.nst_run && a.in_kind == IN_DISCRETE) launch_trio_nst_k<S, 2>(a);
+  else launch_trio_nst_k<S, 1>(a);
 }
 
 // the one-asset envs (ONE, S = 2: the second lane of every env a pad; its
@@ -202,9 +210,10 @@ void launch_trio_one_impl(const StepArgs& a) {
   const bool small = win || (long long)a.p.N * S < 256LL * TRIO_W;
   const TrioGo<S> go{a, small};
   auto pick = [&](auto rq1, auto winc, auto nstc) {
-    constexpr bool R = decltype(rq1)::value, W = decltype(winc)::value, NS = decltype(nstc)::value;
+    constexpr bool R = decltype(rq1)::value, W = decltype(winc)::value;
+    constexpr int NS = decltype(nstc)::value;
     if constexpr (W) {
-      if constexpr (NS) {
+      if constexpr (NS != 0) {
         // the reference's own experiment shape (one OU asset, a window,
         // n-step returns) with the bench's output set (O_WSTD) and the OU
         // generator at compile time: R1 8192 DDR 9.40e8 -> 9.57e8 env-steps/s
@@ -222,7 +231,17 @@ void launch_trio_one_impl(const StepArgs& a) {
   };
   using T = std::true_type;
   using F = std::false_type;
-  using N = std::integral_constant<bool, NS_>;
+  // NS_: n-step handles, with the running-sum pop where the host granted it
+  using N = std::integral_constant<int, NS_ ? 1 : 0>;
+  using NR = std::integral_constant<int, NS_ ? 2 : 0>;
+  if (NS_ && a.p.nst_run) {
+    if (a.p.reqm_one) {
+      win ? pick(T{}, T{}, NR{}) : pick(T{}, F{}, NR{});
+    } else {
+      win ? pick(F{}, T{}, NR{}) : pick(F{}, F{}, NR{});
+    }
+    return;
+  }
   if (a.p.reqm_one) {
     win ? pick(T{}, T{}, N{}) : pick(T{}, F{}, N{});
   } else {

@@ -262,7 +262,7 @@ __device__ __forceinline__ void gen_state_copy(Lane<M>& d, const Lane<M>& s) {
 // MM: asset slots per lane (2: a 16-asset env on 8 lanes per role, so 8192
 // envs fit one workgroup per CU; slots ls MM + m in the canonical order, the
 // ledger's broker_spec_m2; one-step rewards with a scalar shaper, D = 1)
-template <int S, bool RQ1, bool DISC, uint32_t OMC = 0, bool WIN = false, int TW = TRIO_W, bool NST = false,
+template <int S, bool RQ1, bool DISC, uint32_t OMC = 0, bool WIN = false, int TW = TRIO_W, int NST = 0,
           int GK = -1, bool RP = false, int MM = 1, bool ONE = false, bool K1 = false>
 // The leading pointer arguments are the ledger role's state and actions:
 // built with -amdgpu-kernarg-preload-count (madigan_amd/build.py) they arrive
@@ -289,6 +289,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   constexpr bool TAIL = K1 && !RP && !WIN && MM == 1;
   constexpr bool GLOG = WIN && !RP;
   constexpr int NPADS = 2;  // NST: ring, pop summands
+  // NST == 2: the running-sum pop (MGN_NSTEP_POP_RUNNING, nrun_pop; the host
+  // routes only DSR / DDR / PPC / none here); NST == 1: the exact pop
+  constexpr bool NRUN = NST == 2;
   static_assert(M == 1 || (M == 2 && !NST), "two slots per lane: one-step rewards");
   static_assert(!ONE || (S == 2 && M == 1), "a one-asset env on two lanes per role");
   constexpr int APAD = S * M;
@@ -366,6 +369,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   double shA = 0., shB = 0.;                     // F
   int32_t rhead = 0, rlen = 0;                   // F (WIN): the window ring
   int32_t nlen = 0, nhead = 0;                   // F (NST): NStepBuffer fill count / oldest index
+  NstRun nrs{0., 0., 0., 0., 0., 0.};             // F (NRUN): the buffer's running sums, on every lane of the env
+  int32_t nsl = 0;                               // F (NRUN): pops since the sums were last formed from the ring
 #ifdef MGN_TRIO_ABL_PRO  // diagnostic timing build: no state loads (outputs wrong)
   if (false) {
 #else
@@ -426,12 +431,21 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       shA = p.sA[li];
       shB = p.sB[li];
     }
-    if constexpr (NST) {
+    if constexpr (NST != 0) {
       nlen = p.nlen[envc];
       nhead = p.nhead[envc];
       // the env's ring into LDS (every lane of the env copies a share)
       double* ring = s_nst + (size_t)el * NPADS * nst_pad(p.nstep, S);
-      for (int i = ls; i < p.nstep; i += S) ring[i] = p.nring[(size_t)envc * p.nstep + i];
+      for (int i = ls; i < p.nstep; i += S) {
+        const double x = p.nring[(size_t)envc * p.nstep + i];
+        ring[i] = x;
+        if constexpr (NRUN) {  // the sums of the entries the lane copied (position k from the oldest)
+          int k = i - nhead;
+          k += (k < 0) ? p.nstep : 0;
+          if (k < nlen) nrun_add(nrs, x, p.disc[k]);
+        }
+      }
+      if constexpr (NRUN) nrun_allsum<S>(nrs);
     }
   }
   {
@@ -1298,6 +1312,29 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     if (live && (flags & TR_STEP) && !rsv) {
 #endif
       const int k = krec;
+      // NRUN: the sums re-formed from the ring every n pops (term kk on lane
+      // kk mod S; the entries before this step's), then the step's first pop
+      // less its new entry's term and that entry's weight and the oldest
+      // entry, formed ahead of the reward chain (nrun_pre)
+      NstPre npre{};
+      double nst_w = 0., nst_r0 = 0.;
+      if constexpr (NRUN) {
+        const int n = p.nstep;
+        const double* ring = s_nst + (size_t)el * NPADS * nst_pad(n, S);
+        if (nsl >= n) {
+          nrun_zero(nrs);
+          for (int kk = ls; kk < nlen; kk += S) {
+            int idx = nhead + kk;
+            idx -= (idx >= n) ? n : 0;
+            nrun_add(nrs, ring[idx], s_disc[kk]);
+          }
+          nrun_allsum<S>(nrs);
+          nsl = 0;
+        }
+        nst_w = s_disc[nlen];
+        nst_r0 = ring[nhead];
+        npre = nrun_pre(p.shaper, nrs, nlen + 1, g.shA, g.shB);
+      }
       Lane<M> f = s;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
@@ -1388,8 +1425,45 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         // steps between pops as nstep_column's does
         int tail = nhead + nlen;
         tail -= (tail >= n) ? n : 0;
-        if (ls == 0) ring[tail] = v;
         int len = L1, head = nhead;
+        if constexpr (NRUN) {
+          // the running-sum pop (nrun_pre / nrun_fin): every lane of the env
+          // keeps the sums, appends the entry and pops -- the same values on
+          // every lane, the first stores
+          ring[tail] = v;  // (every lane writes it: each lane's own reads below see it)
+          nrun_add(nrs, v, nst_w);
+          for (int pj = 0; pj < pops; ++pj) {
+            double res, r0;
+            if (pj == 0) {
+              res = nrun_fin(p.shaper, npre, v, nst_w);
+              r0 = nlen == 0 ? v : nst_r0;
+            } else {  // a done flush's further pops
+              res = nrun_pop(p.shaper, nrs, len, g.shA, g.shB);
+              r0 = ring[head];
+            }
+            if (p.shaper == MGN_SHAPER_DSR || p.shaper == MGN_SHAPER_DDR) {  // update_parameters (exact)
+              g.shA += p.eta * (r0 - g.shA);
+              if (p.shaper == MGN_SHAPER_DSR) {
+                g.shB += p.eta * (r0 * r0 - g.shB);
+              } else {
+                double m = r0 < 0. ? r0 : 0.;
+                if (r0 != r0) m = r0;
+                g.shB += p.eta * (m * m - g.shB);
+              }
+            }
+            if (row && ls == 0) ost(row + pj, res);
+            head = (head + 1 == n) ? 0 : head + 1;
+            len -= 1;
+            if (len == 0) {  // a flushed buffer: the sums are exactly zero again
+              nrun_zero(nrs);
+              nsl = 0;
+            } else {
+              nrun_slide(nrs, r0, p.nst_rg);
+              nsl += (r0 - r0 == 0.) ? 1 : n;  // a non-finite entry left: re-form at the next step
+            }
+          }
+        } else {
+        if (ls == 0) ring[tail] = v;
         for (int pj = 0; pj < pops; ++pj) {
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
@@ -1436,6 +1510,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           if (row && ls == 0) ost(row + pj, res);
           head = (head + 1 == n) ? 0 : head + 1;
           len -= 1;
+        }
         }
 #ifndef MGN_NST_ABL_ROW  // diagnostic timing build (outputs wrong): no zero entries
         if (row)
@@ -1583,7 +1658,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   return;
 #endif
   if (!live) return;
-  if constexpr (NST) {
+  if constexpr (NST != 0) {
     const double* ring = s_nst + (size_t)el * NPADS * nst_pad(p.nstep, S);
     for (int i = ls; i < p.nstep; i += S) p.nring[(size_t)env * p.nstep + i] = ring[i];
     if (ls == 0) {

@@ -127,8 +127,13 @@ class BatchedEnv:
                  desired_portfolio=None, window: int = 0, norm_type=None,
                  auto_reset: bool = False, action_atoms: int = 3, unit_size: float = 0.05,
                  nstep_return: int = 1, discount: float = 0.99, replay_tape: Optional[dict] = None,
-                 replay_stride: int = 0, sortino_exp=None):
-        """A replay spec (``config.replay_spec`` / HDFSourceSingle) reads its
+                 replay_stride: int = 0, sortino_exp=None, nstep_pop: str = "exact"):
+        """nstep_pop: "exact" (default) re-evaluates every n-step pop's
+        summands as nstep_buffer.py does; "running" lets the three-role kernel
+        pop DSR / DDR / PPC / none from discounted running sums (O(1) per pop,
+        within 1e-6 of the exact pop; include/madigan_amd.h MGN_NSTEP_POP_*).
+
+        A replay spec (``config.replay_spec`` / HDFSourceSingle) reads its
         prices, features and timestamps from a device replay tape: staged from
         the spec's HDF file (``spec.hdf``, cache_size chunks, pinned
         double-buffered H2D) or given as ``replay_tape`` = {price (P,A),
@@ -151,7 +156,7 @@ class BatchedEnv:
             desired_portfolio=desired_portfolio, window=window, norm_type=norm_type,
             auto_reset=auto_reset, action_atoms=action_atoms, unit_size=unit_size, seed=seed,
             env_offset=env_offset, nstep_return=nstep_return, discount=discount,
-            sortino_exp=sortino_exp)
+            sortino_exp=sortino_exp, nstep_pop=nstep_pop)
         self.N = int(n_envs)
         self.A = spec.n_assets
         self.F = int(spec.n_feats) if spec.replay else self.A

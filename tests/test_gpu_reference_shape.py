@@ -31,7 +31,7 @@ BENCH_FIELDS = ["reward", "shaped", "done", "obs_price", "obs_port", "timestamp"
                 "risk", "margin_call", "data_end", "n_shaped"]
 
 
-def _launch_vs_oracle(g, orc, acts, tag, shaped_rtol, fields=None):
+def _launch_vs_oracle(g, orc, acts, tag, shaped_rtol, fields=None, atol=1e-14):
     import ctypes as C
     import torch
     from madigan_amd import _lib as L
@@ -56,7 +56,7 @@ def _launch_vs_oracle(g, orc, acts, tag, shaped_rtol, fields=None):
         close(host["reward"][k], r["reward"][0], f"{tag} reward step {k}")
         if "agent_reward" in host:
             close(host["agent_reward"][k], r["agent_reward"][0], f"{tag} agent reward step {k}")
-        np.testing.assert_allclose(host["shaped"][k], r["shaped"][0], rtol=shaped_rtol, atol=1e-14,
+        np.testing.assert_allclose(host["shaped"][k], r["shaped"][0], rtol=shaped_rtol, atol=atol,
                                    err_msg=f"{tag} n-step row step {k}")
         rpr, rpo, rts = orc.window()
         assert_bits(wp[k].cpu().numpy(), rpr, f"{tag} window price step {k}")

@@ -24,7 +24,7 @@ def main():
     N = int(os.environ.get("N", 8192))
     fuse = int(os.environ.get("FUSE", 64))
     nst = int(os.environ.get("NSTEP", 1))
-    extra = dict(nstep_return=nst, discount=0.99) if nst > 1 else {}
+    extra = dict(nstep_return=nst, discount=0.99, nstep_pop=os.environ.get("NSTEP_POP", "exact")) if nst > 1 else {}
     wl = os.environ.get("WORKLOAD", "C3")
     A = int(os.environ.get("ASSETS", 8))
     env, _, _ = bench.workload_env(wl, N, A, 0, "cuda:0", **(extra if wl == "C3" else {}))

@@ -115,3 +115,49 @@ def test_reference_shape_bench_outputs_vs_oracle(gpu, shaper, extra):
     ends = _launch_vs_oracle(g, orc, acts[:K], f"{shaper} bench set launch 0", 1e-10, BENCH_FIELDS)
     ends += _launch_vs_oracle(g, orc, acts[K:], f"{shaper} bench set launch 1", 1e-10, BENCH_FIELDS)
     assert ends > 8192 // 20, f"{ends} episode ends"
+
+
+@pytest.mark.parametrize("shaper,extra", [("DDR", {}), ("sortino_shaperB", dict(sortino_exp=1.1))])
+def test_reference_shape_trio_equals_single_bitwise(gpu, shaper, extra):
+    """At the bench's batch (8192 envs) the ONE layout's outputs -- the n-step
+    rows (`shaped`) included, which the oracle tests hold to rtol 1e-10 --
+    and every step's window equal the single-role kernel's bit for bit, over
+    two 64-step launches with auto-resets (the same pop summands in the same
+    order on both kernels)."""
+    import ctypes as C
+    import torch
+    from madigan_amd import BatchedEnv
+    from madigan_amd import _lib as L
+    from tests.configs import spec_from_sources
+    kw = dict(REF_KW, reward_shaper=shaper, **extra, seed=0x6D6164 + 51)
+    kw.update(required_margin=0.05, unit_size=0.9)
+    res = []
+    for sched in (L.SCHED_TRIO, L.SCHED_SINGLE):
+        g = BatchedEnv(spec_from_sources(ou_sources(1)), 8192, **kw)
+        L.check(g.lib.mgn_set_schedule(g.h, sched), g.h)
+        acts = g.generate_actions(128, seed=0x6D6164 + 52)
+        outs = []
+        for half in range(2):
+            K = 64
+            traj = g.alloc_traj(K)
+            wp = torch.empty((K, g.N, g.W, g.F), dtype=torch.float64, device=g.device)
+            wo = torch.empty((K, g.N, g.W, g.A + 1), dtype=torch.float64, device=g.device)
+            wt = torch.empty((K, g.N, g.W), dtype=torch.int64, device=g.device)
+            t = g._traj_struct(traj)
+            a = acts[half * K:(half + 1) * K]
+            L.check(g.lib.mgn_rollout_hist(g.h, C.c_void_p(a.data_ptr()), K, C.byref(t)), g.h)
+            L.check(g.lib.mgn_window_hist(g.h, *[C.c_void_p(x.data_ptr()) for x in (wp, wo, wt)]), g.h)
+            o = {k: v.cpu().numpy() for k, v in traj.items()}
+            o.update(win_price=wp.cpu().numpy(), win_port=wo.cpu().numpy(), win_ts=wt.cpu().numpy())
+            outs.append(o)
+        assert g.lib.mgn_get_schedule(g.h) == sched
+        res.append(outs)
+    ends = 0
+    for half, (a, b) in enumerate(zip(*res)):
+        for k, v in a.items():
+            if v.dtype == np.float64:
+                assert_bits(b[k], v, f"{shaper} launch {half} trio vs single {k}")
+            else:
+                assert np.array_equal(b[k], v), f"{shaper} launch {half} trio vs single {k}"
+        ends += int(a["done"].sum())
+    assert ends > 8192 // 20

@@ -8,3 +8,5 @@ for pop in running exact; do
   echo "stamps $pop: $(tail -1 $O/stamps_$pop.json)"
 done
 TAG=r06c/probe ARGS="--nstep 20 --nstep-pop running --steps 400 --warmup 40 --fuse 20" VARS="nrow=tools/_var/nrow/libmadigan_hip.so" ROUNDS=2 bash tools/nst_probe.sh
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_reference_shape.py -k "bitwise" > $O/pytest_one_bitwise.txt 2>&1 || { echo PYTEST_FAIL; tail -30 $O/pytest_one_bitwise.txt; exit 1; }
+tail -2 $O/pytest_one_bitwise.txt

@@ -28,7 +28,7 @@ def main():
     nst = int(os.environ.get("NSTEP", 1))
     wl = os.environ.get("WORKLOAD", "C3")
     A = int(os.environ.get("ASSETS", 8))
-    extra = dict(nstep_return=nst, discount=0.99) if nst > 1 else {}
+    extra = dict(nstep_return=nst, discount=0.99, nstep_pop=os.environ.get("NSTEP_POP", "exact")) if nst > 1 else {}
     env, _, _ = bench.workload_env(wl, N, A, 0, "cuda:0", **(extra if wl == "C3" else {}))
     fields = ["reward", "shaped", "done", "obs_price", "obs_port", "timestamp", "tprice", "tunits", "tcost",
               "risk", "margin_call"]

@@ -17,6 +17,67 @@
 
 namespace mgn {
 
+// The diagnostic switches as the step kernels read them: MGN_ST(...) is code
+// of the stamp builds only (it names the stamp buffers, which exist only
+// there); kAbl* are the ablation builds' switches, false in every product
+// build, so a product kernel reads straight through `if constexpr` blocks
+// that the compiler discards.
+#ifdef MGN_STAMPS
+#define MGN_ST(...) __VA_ARGS__
+#else
+#define MGN_ST(...)
+#endif
+#ifdef MGN_TRIO_ABL_PRO
+constexpr bool kAblPro = true;   // no state loads
+#else
+constexpr bool kAblPro = false;
+#endif
+#ifdef MGN_TRIO_ABL_G
+constexpr bool kAblG = true;     // no tick (prices frozen)
+#else
+constexpr bool kAblG = false;
+#endif
+#ifdef MGN_TRIO_ABL_L
+constexpr bool kAblL = true;     // no Broker orders
+#else
+constexpr bool kAblL = false;
+#endif
+#ifdef MGN_TRIO_ABL_F
+constexpr bool kAblF = true;     // no step finish, no outputs
+#else
+constexpr bool kAblF = false;
+#endif
+#ifdef MGN_TRIO_ABL_EPI
+constexpr bool kAblEpi = true;   // no state write-back
+#else
+constexpr bool kAblEpi = false;
+#endif
+#ifdef MGN_NST_ABL_TERM
+constexpr bool kAblNstTerm = true;  // no n-step summand arithmetic
+#else
+constexpr bool kAblNstTerm = false;
+#endif
+#ifdef MGN_NST_ABL_SUM
+constexpr bool kAblNstSum = true;   // no n-step ordered sum
+#else
+constexpr bool kAblNstSum = false;
+#endif
+#ifdef MGN_NST_ABL_ROW
+constexpr bool kAblNstRow = true;   // no zero entries of the n-step rows
+#else
+constexpr bool kAblNstRow = false;
+#endif
+#ifdef MGN_ABL_NOSTORE_ASSET
+constexpr bool kAblNoStoreAsset = true;  // no per-asset output stores
+#else
+constexpr bool kAblNoStoreAsset = false;
+#endif
+#ifdef MGN_ABL_NOSTORE_ENV
+constexpr bool kAblNoStoreEnv = true;    // no per-env output stores
+#else
+constexpr bool kAblNoStoreEnv = false;
+#endif
+
 #ifdef MGN_STAMPS
 // diagnostic build only: per role, cycles of [work 1, wait A, work 2, wait B]
 // summed over one wave per role and block, then the iteration count

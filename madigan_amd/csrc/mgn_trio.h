@@ -350,12 +350,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   const double* const tgt_g = p.target;  // the PPC target in global memory (F's prologue)
 #pragma unroll
   for (int m = 0; m < M; ++m) {
-#ifdef MGN_TRIO_ABL_PRO
-    s.P[m] = 5.0;
-#else
     // the finish role takes its prices from the generator's LDS records
-    s.P[m] = (s.valid[m] && role != 2) ? kP[li + m] : 0.;
-#endif
+    s.P[m] = kAblPro ? 5.0 : ((s.valid[m] && role != 2) ? kP[li + m] : 0.);
     s.L[m] = s.mep[m] = s.Bm[m] = s.sx[m] = s.oum[m] = s.dy[m] = 0.;
     s.tlen[m] = 0;
     s.tfl[m] = 0;
@@ -371,11 +367,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   int32_t nlen = 0, nhead = 0;                   // F (NST): NStepBuffer fill count / oldest index
   NstRun nrs{0., 0., 0., 0., 0., 0.};             // F (NRUN): the buffer's running sums, on every lane of the env
   int32_t nsl = 0;                               // F (NRUN): pops since the sums were last formed from the ring
-#ifdef MGN_TRIO_ABL_PRO  // diagnostic timing build: no state loads (outputs wrong)
-  if (false) {
-#else
-  if (role == 0) {
-#endif
+  if (!kAblPro && role == 0) {
     // only the fields the kind reads (GK): TrendOU no sine phase, OU none
     constexpr bool r_sx = GK < 0 || GK == MGN_SRC_SINE || GK == MGN_SRC_SAWTOOTH || GK == MGN_SRC_TRIANGLE ||
                           GK == MGN_SRC_TRENDYOU;
@@ -471,9 +463,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     sh.more[1] = 0;
     sh.more[2] = 0;
   }
-#ifdef MGN_STAMPS
-  if (threadIdx.x < 8) s_duo_sub[threadIdx.x] = 0;
-#endif
+  MGN_ST(if (threadIdx.x < 8) s_duo_sub[threadIdx.x] = 0;)
   if (!QREG || K == 0) __syncthreads();
   MGN_IT(1, 0);
 #pragma unroll
@@ -505,11 +495,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int kk = ls + (j + u) * S;
-#ifdef MGN_NST_ABL_TERM  // diagnostic timing build (outputs wrong): no summand arithmetic
-        const double t = rr[u];
-#else
-        const double t = term(rr[u], dd[u]);
-#endif
+        const double t = kAblNstTerm ? rr[u] : term(rr[u], dd[u]);
         if (j + u < R) scr[kk] = (kk < len) ? t : 0.0;
       }
     }
@@ -531,10 +517,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   };
   const auto nst_sum = [&](const double* scr, int len) {
     const int R = (len + S - 1) / S;
+    if constexpr (kAblNstSum) return scr[0];
     double acc = 0.0;
-#ifdef MGN_NST_ABL_SUM  // diagnostic timing build (outputs wrong): no ordered sum
-    acc = scr[0];
-#else
     const d2* sc = reinterpret_cast<const d2*>(scr);
     d2 cur[S / 2];
 #pragma unroll
@@ -552,7 +536,6 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
 #pragma unroll
       for (int u = 0; u < S / 2; ++u) cur[u] = nxt[u];
     }
-#endif
     return acc;
   };
 
@@ -585,10 +568,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     bool shadow = false, tail_it = false, stored = false;
     int jlast = 0;
     __builtin_amdgcn_s_setprio(kPrioG);
-#ifdef MGN_STAMPS
-    unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0;
-    int jn = 0;
-#endif
+    MGN_ST(unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0; int jn = 0;)
     int gpend = 0;  // WIN: refill ticks still to come after the reset tick
     RpCurM<M> rp{};  // RP: the current State's tape row, features, dataEnd
     RpNextM<M> rnx{};
@@ -692,11 +672,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
             }
             svTs = ts;
           }
-#ifndef MGN_TRIO_ABL_G  // diagnostic timing build: no tick (prices frozen)
-          tk = true;
-#else
-          ts = ts + 1;
-#endif
+          if constexpr (kAblG) ts = ts + 1;  // (prices frozen)
+          else tk = true;
           k += 1;
         } else if (TAIL && K == 1) {
           // idle (the launch's ticks done, no reset pending): a reset the
@@ -764,25 +741,17 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       __syncthreads();
       MGN_T(T2);
       MGN_IT(2 + (j < 40 ? j : 40), 0);
-#ifdef MGN_STAMPS
-      acc0 += T1 - T0;
-      acc1 += T2 - T1;
-      jn = j;
-#endif
+      MGN_ST(acc0 += T1 - T0; acc1 += T2 - T1; jn = j;)
       jlast = j;
       if (trio_exit(j, K, sh.more[j % 3])) break;
     }
-#ifdef MGN_STAMPS
-    if (threadIdx.x == 0) {
+    MGN_ST(if (threadIdx.x == 0) {
       atomicAdd(&g_duo_stamps[0], acc0);
       atomicAdd(&g_duo_stamps[1], acc1);
       atomicAdd(&g_duo_stamps[8], (unsigned long long)(jn + 1));
       atomicAdd(&g_duo_stamps[10], 1ull);
-    }
-#endif
-#ifdef MGN_TRIO_ABL_EPI  // diagnostic timing build: no state write-back
-    return;
-#endif
+    })
+    if constexpr (kAblEpi) return;
     if constexpr (TAIL) {
       // the last iteration's candidate stands where the finish role found the
       // episode's end there (a tail reset: it raised no further iteration)
@@ -847,17 +816,14 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       if (ls == 0) p.cash[env] = cash;
     };
     __builtin_amdgcn_s_setprio(kPrioL);  // the orders are the critical path
-#ifdef MGN_STAMPS
-    unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0;
-    // the ledger's phases: prices + pre-order sums, units, the Broker, the records
-    unsigned long long Lp1 = 0, Lp2 = 0, Lp3 = 0, lacc[4] = {0, 0, 0, 0};
-#endif
+    // (stamp builds: the ledger's phases -- prices + pre-order sums, units,
+    // the Broker, the records)
+    MGN_ST(unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0;
+           unsigned long long Lp1 = 0, Lp2 = 0, Lp3 = 0, lacc[4] = {0, 0, 0, 0};)
     for (int j = 0;; ++j) {
       const int cur = j & 1, prv = cur ^ 1;
       MGN_T(T0);
-#ifdef MGN_STAMPS
-      Lp1 = Lp2 = Lp3 = T0;
-#endif
+      MGN_ST(Lp1 = Lp2 = Lp3 = T0;)
       // one-step launches: in the last iteration the finish role's chain is
       // the critical path, this role's work (done test, State, write-back) not
       if (TAIL_EXACT && K == 1 && j == 1) __builtin_amdgcn_s_setprio(kPrioG);
@@ -927,9 +893,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         }
         const double prevEq = (cash + s0.lp) - s0.b;  // Env.h:208
         if (j == 0) MGN_IT(58, TRIO_W);
-#ifdef MGN_STAMPS
-        Lp1 = __builtin_amdgcn_s_memtime();
-#endif
+        MGN_ST(Lp1 = __builtin_amdgcn_s_memtime();)
         double uc[M], tp[M], tu[M], tc[M], prevVal[M];
         int rk[M];
         const size_t oN = (size_t)k * p.N, oNA = (size_t)k * p.N * A;
@@ -975,14 +939,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         }
         Sums after = s0;
         int any_mc = 0;
-#ifdef MGN_STAMPS
-        Lp2 = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef MGN_TRIO_ABL_L  // diagnostic timing build: no Broker orders
-        if (false) {
-#else
-        if (in_kind != IN_NONE) {
-#endif
+        MGN_ST(Lp2 = __builtin_amdgcn_s_memtime();)
+        if (!kAblL && in_kind != IN_NONE) {
           if (j == 0) MGN_IT(52, TRIO_W);
           if constexpr (M == 1)
             broker_spec<S, RQ1, ONE>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, after, any_mc);
@@ -990,9 +948,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
             broker_spec_m2<S, RQ1>(s, p, recs[el], cash, uc, tp, tu, tc, rk, ls, after, any_mc);
           if (j == 0) MGN_IT(53, TRIO_W);
         }
-#ifdef MGN_STAMPS
-        Lp3 = __builtin_amdgcn_s_memtime();
-#endif
+        MGN_ST(Lp3 = __builtin_amdgcn_s_memtime();)
         sa = after;
 #pragma unroll
         for (int m = 0; m < M; ++m) {
@@ -1088,20 +1044,16 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       MGN_T(T1);
       __syncthreads();
       MGN_T(T2);
-#ifdef MGN_STAMPS
-      acc0 += T1 - T0;
-      acc1 += T2 - T1;
-      if (Lp3 != T0) {  // an iteration that stepped
-        lacc[0] += Lp1 - T0;
-        lacc[1] += Lp2 - Lp1;
-        lacc[2] += Lp3 - Lp2;
-        lacc[3] += T1 - Lp3;
-      }
-#endif
+      MGN_ST(acc0 += T1 - T0; acc1 += T2 - T1;
+             if (Lp3 != T0) {  // an iteration that stepped
+               lacc[0] += Lp1 - T0;
+               lacc[1] += Lp2 - Lp1;
+               lacc[2] += Lp3 - Lp2;
+               lacc[3] += T1 - Lp3;
+             })
       if (trio_exit(j, K, sh.more[j % 3])) break;
     }
-#ifdef MGN_STAMPS
-    if (l == 0) {
+    MGN_ST(if (l == 0) {
       atomicAdd(&g_duo_stamps[4], acc0);
       atomicAdd(&g_duo_stamps[5], acc1);
       for (int i = 0; i < 3; ++i) atomicAdd(&g_duo_stamps[13 + i], s_duo_sub[i]);
@@ -1111,11 +1063,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       atomicAdd(&g_duo_stamps[3], s_duo_sub[4]);
       atomicAdd(&g_duo_stamps[6], s_duo_sub[7]);
       for (int i = 0; i < 4; ++i) atomicAdd(&g_duo_stamps[20 + i], lacc[i]);
-    }
-#endif
-#ifdef MGN_TRIO_ABL_EPI  // diagnostic timing build: no state write-back
-    return;
-#endif
+    })
+    if constexpr (kAblEpi) return;
     if constexpr (TAIL) {
       // a tail reset (the finish role found the episode's end in the last
       // iteration): the fresh Broker (Env.h:181-187)
@@ -1278,15 +1227,11 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
   };
   drain_vmem();
   __builtin_amdgcn_s_setprio(kPrioF);
-#ifdef MGN_STAMPS
-  unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0, Tf1 = 0, Tf2 = 0, facc[3] = {0, 0, 0};
-#endif
+  MGN_ST(unsigned long long T0 = 0, T1 = 0, T2 = 0, acc0 = 0, acc1 = 0, Tf1 = 0, Tf2 = 0, facc[3] = {0, 0, 0};)
   for (int j = 0;; ++j) {
     const int cur = j & 1, prv = cur ^ 1;
     MGN_T(T0);
-#ifdef MGN_STAMPS
-    Tf1 = Tf2 = 0;
-#endif
+    MGN_ST(Tf1 = Tf2 = 0;)
     int rst_out = 0;
     bool tail_rst = false;  // TAIL: the launch's last step ended its episode
     // the step L ran in iteration j-1, unless F voided it at iteration j-1
@@ -1306,11 +1251,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     // (a compiler-only memory barrier: the reads stay ahead of the tests --
     // the compiler would sink them into the branch -- and nothing waits here)
     asm volatile("" ::: "memory");
-#ifdef MGN_TRIO_ABL_F  // diagnostic timing build: no step finish, no outputs
-    if (false) {
-#else
-    if (live && (flags & TR_STEP) && !rsv) {
-#endif
+    if (!kAblF && live && (flags & TR_STEP) && !rsv) {
       const int k = krec;
       // NRUN: the sums re-formed from the ring every n pops (term kk on lane
       // kk mod S; the entries before this step's), then the step's first pop
@@ -1400,9 +1341,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
       }
       double shaped_s = 0., rin_s = 0., shaped_v = 0.;
       int pops = 1;
-#ifdef MGN_STAMPS
-      Tf1 = __builtin_amdgcn_s_memtime();
-#endif
+      MGN_ST(Tf1 = __builtin_amdgcn_s_memtime();)
       if (NST) {
         // NStepBuffer.add + pop_nstep_sarsd (nstep_buffer.py:315-356, driven as
         // replay_buffer.py:68-80) for the env's scalar column: append, pop once
@@ -1512,10 +1451,8 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           len -= 1;
         }
         }
-#ifndef MGN_NST_ABL_ROW  // diagnostic timing build (outputs wrong): no zero entries
-        if (row)
+        if (!kAblNstRow && row)
           for (int jj = pops + ls; jj < n; jj += S) ost(row + jj, 0.);
-#endif
         nhead += pops;
         while (nhead >= n) nhead -= n;
         nlen = L1 - pops;
@@ -1535,13 +1472,11 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
         shaped_v = f.valid[0] ? shape(p.shaper, ar[0], g.shA, g.shB, p.eta, cos_term, p.sexp) : 0.;  // M = 1
       }
       if (j == 1) MGN_IT(57, 2 * TRIO_W);
-#ifdef MGN_STAMPS
-      Tf2 = __builtin_amdgcn_s_memtime();
-#endif
+      MGN_ST(Tf2 = __builtin_amdgcn_s_memtime();)
       // outputs of step k (the speculative runs never reach F)
-#ifndef MGN_ABL_NOSTORE_ASSET
 #pragma unroll
       for (int m = 0; m < M; ++m) {
+        if (kAblNoStoreAsset) break;
         if (f.valid[m]) {
           const size_t i = kidx(k, sNA, bA) + m;
           if (!RP && !lobs && (om & O_OPR)) ost(ov.obs_price + (kidx(k, sNF, bP) + m), f.P[m]);
@@ -1552,10 +1487,9 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           }
         }
       }
-      if (RP && live && (om & O_OPR)) put_price(ov.obs_price + kidx(k, sNF, (size_t)env * p.F), f.P, false, prv);
-#endif
-#ifndef MGN_ABL_NOSTORE_ENV
-      if (ls == 0) {
+      if (!kAblNoStoreAsset && RP && live && (om & O_OPR))
+        put_price(ov.obs_price + kidx(k, sNF, (size_t)env * p.F), f.P, false, prv);
+      if (!kAblNoStoreEnv && ls == 0) {
         const size_t ie = kidx(k, sN, (size_t)env);
         if (!lobs && (om & O_OPT)) ost(ov.obs_port + kidx(k, sNA1, bO), port0);
         if (om & O_DONE) ost(ov.done + ie, (uint8_t)(done ? 1 : 0));
@@ -1574,7 +1508,6 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
           if (!NST && (om & O_SHP)) ost(ov.shaped + ie, shaped_s);
         }
       }
-#endif
       if (WIN) {
         push_row(f.P, portA, port0, (uint64_t)sh.ts[prv][el], k, prv);
         if (done && p.auto_reset) {  // a reset empties the window before its refill ticks
@@ -1634,29 +1567,22 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(const double* __restric
     MGN_T(T1);
     __syncthreads();
     MGN_T(T2);
-#ifdef MGN_STAMPS
-    acc0 += T1 - T0;
-    acc1 += T2 - T1;
-    if (Tf2) {  // the iterations that evaluated a step: before / in / after the reward's shaping
-      facc[0] += Tf1 - T0;
-      facc[1] += Tf2 - Tf1;
-      facc[2] += T1 - Tf2;
-    }
-#endif
+    MGN_ST(acc0 += T1 - T0; acc1 += T2 - T1;
+           if (Tf2) {  // the iterations that evaluated a step: before / in / after the reward's shaping
+             facc[0] += Tf1 - T0;
+             facc[1] += Tf2 - Tf1;
+             facc[2] += T1 - Tf2;
+           })
     if (trio_exit(j, K, sh.more[j % 3])) break;
   }
-#ifdef MGN_STAMPS
-  if (l == 0) {
+  MGN_ST(if (l == 0) {
     atomicAdd(&g_duo_stamps[16], acc0);
     atomicAdd(&g_duo_stamps[17], acc1);
     atomicAdd(&g_duo_stamps[9], facc[0]);
     atomicAdd(&g_duo_stamps[11], facc[1]);
     atomicAdd(&g_duo_stamps[12], facc[2]);
-  }
-#endif
-#ifdef MGN_TRIO_ABL_EPI
-  return;
-#endif
+  })
+  if constexpr (kAblEpi) return;
   if (!live) return;
   if constexpr (NST != 0) {
     const double* ring = s_nst + (size_t)el * NPADS * nst_pad(p.nstep, S);

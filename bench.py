@@ -426,6 +426,9 @@ def main():
     ap.add_argument("--nstep-pop", default="exact", choices=["exact", "running"],
                     help="n-step lines (C3 --nstep > 1, R1): the exact pop or the running-sum pop "
                          "(MGN_NSTEP_POP_RUNNING, within 1e-6 of the exact pop)")
+    ap.add_argument("--k1-hist", dest="k1_ring", action="store_false",
+                    help="windowed workloads at --win-fuse 1: the launch-history path (mgn_rollout_hist + "
+                         "mgn_window_hist) instead of mgn_rollout + mgn_window")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-k-sweep", dest="k_sweep", action="store_false",
                     help="skip the K = 1 / 16 / 256 launch-length block of the line")
@@ -910,11 +913,21 @@ def windowed(args, world, rank, dev):
     base = actions.data_ptr()
     wptr = [C.c_void_p(x.data_ptr()) for x in (wp, wo, wt)]
 
+    # one step per launch (--win-fuse 1, the reference's own driving:
+    # offpolicy_q.py:143, 193-194 -- env.step, then stream_state /
+    # current_data): mgn_rollout then mgn_window, the window gathered from the
+    # ring the step kernel pushed to (no launch history to copy into)
+    agent_k1 = Kf == 1 and args.k1_ring
+
     def run(l0, l1):
         rc = 0
         for l in range(l0, l1):
-            rc |= lib.mgn_rollout_hist(h, C.c_void_p(base + l * Kf * per), Kf, tstruct)
-            rc |= lib.mgn_window_hist(h, *wptr)
+            if agent_k1:
+                rc |= lib.mgn_rollout(h, C.c_void_p(base + l * per), 1, tstruct)
+                rc |= lib.mgn_window(h, *wptr)
+            else:
+                rc |= lib.mgn_rollout_hist(h, C.c_void_p(base + l * Kf * per), Kf, tstruct)
+                rc |= lib.mgn_window_hist(h, *wptr)
         L.check(rc, h)
 
     run(0, n_warm)
@@ -987,12 +1000,15 @@ def windowed(args, world, rank, dev):
                        "n_feats": env.F,
                        "window": W, "steps_per_launch": Kf, "nstep": env.nstep,
                        "nstep_pop": args.nstep_pop if env.nstep > 1 else None,
+                       "drive": ("mgn_rollout (one step) + mgn_window (the ring's window) per step, as "
+                                 "offpolicy_q.py:143,193-194 drives env.step / current_data") if agent_k1 else
+                                "mgn_rollout_hist (K steps) + mgn_window_hist (every step's window)",
                        "schedule": SCHED_NAMES[int(lib.mgn_get_schedule(h))],
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                          "traffic": load_pmc_traffic(f"{wl}_gather_{N}x{A}_W{W}")[0],
-                         "kernel": "mgn::k_hist_gather",
+                         "kernel": "mgn::k_ring_gather_lds" if agent_k1 else "mgn::k_hist_gather",
                          "bytes_per_env_step": gb / (N * Kf),
                          "avg_launch_us": gather_us},
             "step_launch_avg_us": step_us,

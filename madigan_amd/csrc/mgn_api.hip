@@ -26,6 +26,7 @@ constexpr size_t kGatherLdsTarget = 40 * 1024;
 constexpr size_t kGatherLdsBudget = 64 * 1024;
 // launch-history gather: windows (steps) per workgroup
 constexpr int kHistStepsPerGroup = 16;
+constexpr size_t kHistGroupBytes = 80 * 1024;  // k_hist_gather: output bytes per workgroup to reach
 
 thread_local std::string g_error;
 
@@ -788,11 +789,15 @@ int mgn_window_clear(mgn_env* e, const uint8_t* mask_dev) {
   return check_hip(e, hipGetLastError(), "mgn_window_clear");
 }
 
+static void time_mark(mgn_env* e, std::vector<hipEvent_t>& v, size_t& n, hipStream_t st);
+
 int mgn_window(mgn_env* e, double* price_dev, double* port_dev, uint64_t* ts_dev) {
   if (!e) return fail(nullptr, MGN_ERR_ARG, "null handle");
   if (e->W == 0) return fail(e, MGN_ERR_CONFIG, "handle has no window (window_length = 0)");
+  time_mark(e, e->t_gather, e->t_gather_n, e->stream);
   launch_gather(ring_desc(e), price_dev ? price_dev : e->v.win_price,
                 port_dev ? port_dev : e->v.win_port, ts_dev ? ts_dev : e->v.win_ts, e->stream);
+  time_mark(e, e->t_gather, e->t_gather_n, e->stream);
   return check_hip(e, hipGetLastError(), "mgn_window");
 }
 
@@ -930,7 +935,15 @@ int mgn_window_hist(mgn_env* e, double* price_dev, double* port_dev, uint64_t* t
     return fail(e, MGN_ERR_CONFIG, "mgn_window_hist: element-wise normalisers only (none, log, lookback, lookback_log)");
   // LDS rows: the window before the launch, one row per step and one reset's
   // refill; a longer span reads the history directly
-  const int ks = std::min(h.K, kHistStepsPerGroup);
+  // steps per workgroup: 16, doubled (up to the launch's K) until a
+  // workgroup writes >= 80 KB -- its two dependent memory round trips (the
+  // history marks, then the staged rows) are paid once per workgroup, so
+  // narrow rows need more windows per workgroup (R1, 2 KB per window: 0.47 of
+  // 8 TB/s at 16 steps, 0.66 at 64; C2 / C4 / C5, 5-17 KB per window: best at
+  // 16; profiles/r06n_gather_ks_ab.txt)
+  int ks = std::min(h.K, kHistStepsPerGroup);
+  while (ks < std::min(h.K, mgn::HIST_KMAX) && (size_t)ks * e->W * (C + 1) * 8 < kHistGroupBytes)
+    ks = std::min(2 * ks, std::min(h.K, mgn::HIST_KMAX));
   const int kb = (h.K + ks - 1) / ks;
   const int lds_rows = std::min(e->W + ks + (e->W + 1), (int)(kGatherLdsBudget / ((size_t)(C + 1) * 8)));
   const size_t lds = (size_t)lds_rows * (C + 1) * 8;

@@ -389,7 +389,9 @@ __global__ __launch_bounds__(BLOCK) void k_hist_prefix(RingDesc r, double* __res
 // read once and every output byte written once with 16-B stores; a span
 // larger than the LDS budget reads the history directly (L2-resident within
 // the workgroup).  Splitting an env's K windows over workgroups of ks keeps
-// the grid fine-grained (no tail of a few long workgroups).
+// the grid fine-grained (no tail of a few long workgroups); mgn_window_hist
+// sizes ks so that a workgroup still writes >= 80 KB (its two dependent
+// memory round trips amortised: narrow rows take more steps per workgroup).
 constexpr int HIST_KMAX = 64;
 
 __global__ __launch_bounds__(BLOCK) void k_hist_gather(HistDesc h, double* __restrict__ price_out,

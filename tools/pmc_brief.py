@@ -31,7 +31,7 @@ def dispatches(gdir):
     ts = {}
     for f in glob.glob(os.path.join(gdir, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "k_step" not in r.get("Kernel_Name", ""):
+            if os.environ.get("PMC_KERNEL", "k_step") not in r.get("Kernel_Name", ""):
                 continue
             i = int(r["Dispatch_Id"])
             c = rows[i]

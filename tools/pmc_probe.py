@@ -30,6 +30,10 @@ def main():
     A = int(os.environ.get("ASSETS", 8))
     extra = dict(nstep_return=nst, discount=0.99, nstep_pop=os.environ.get("NSTEP_POP", "exact")) if nst > 1 else {}
     env, _, _ = bench.workload_env(wl, N, A, 0, "cuda:0", **(extra if wl == "C3" else {}))
+    if os.environ.get("SCHED"):  # force a schedule (single / duo / trio)
+        from madigan_amd import _lib as L
+        L.check(env.lib.mgn_set_schedule(env.h, {"single": L.SCHED_SINGLE, "duo": L.SCHED_DUO,
+                                                 "trio": L.SCHED_TRIO}[os.environ["SCHED"]]), env.h)
     fields = ["reward", "shaped", "done", "obs_price", "obs_port", "timestamp", "tprice", "tunits", "tcost",
               "risk", "margin_call"]
     if age:
@@ -40,11 +44,29 @@ def main():
         del o64
     acts = env.generate_actions(fuse * (reps + 3), seed=5)
     out = env.alloc_traj(fuse, fields=fields)
-    for r in range(reps + 3):
-        env.rollout(acts[r * fuse:(r + 1) * fuse], out)
+    if env.W > 0 and os.environ.get("GATHER", "0") == "1":
+        # windowed workloads: each launch's K steps (mgn_rollout_hist) then
+        # every step's window (mgn_window_hist) -- the bench's windowed() pair;
+        # PMC_KERNEL=k_hist_gather selects the gather's dispatches
+        import ctypes as C
+        from madigan_amd import _lib as L
+        W, F = env.W, env.F
+        wp = torch.empty((fuse, N, W, F), dtype=torch.float64, device="cuda:0")
+        wo = torch.empty((fuse, N, W, A + 1), dtype=torch.float64, device="cuda:0")
+        wt = torch.empty((fuse, N, W), dtype=torch.int64, device="cuda:0")
+        t = env._traj_struct(out)
+        per = N * A
+        for r in range(reps + 3):
+            L.check(env.lib.mgn_rollout_hist(env.h, C.c_void_p(acts.data_ptr() + r * fuse * per), fuse, C.byref(t)),
+                    env.h)
+            L.check(env.lib.mgn_window_hist(env.h, *[C.c_void_p(x.data_ptr()) for x in (wp, wo, wt)]), env.h)
+    else:
+        for r in range(reps + 3):
+            env.rollout(acts[r * fuse:(r + 1) * fuse], out)
     torch.cuda.synchronize()
     print(json.dumps({"workload": wl, "N": N, "assets": env.A, "fuse": fuse, "reps": reps, "age": age,
-                      "nstep": nst, "lib": os.environ.get("MADIGAN_LIB_PATH", "product")}))
+                      "nstep": nst, "sched": os.environ.get("SCHED", "auto"),
+                      "lib": os.environ.get("MADIGAN_LIB_PATH", "product")}))
 
 
 if __name__ == "__main__":

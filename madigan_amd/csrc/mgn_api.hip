@@ -268,6 +268,17 @@ int validate(const mgn_config* c, const mgn_asset_source* s, std::string& msg) {
   return MGN_OK;
 }
 
+// MGN_NSTEP_POP_RUNNING granted: the shapers with a running-sum pop, scalar
+// rewards, and a discount whose slides stay well conditioned (the sums'
+// rounding grows by 1/gamma per pop between the re-sums every n pops)
+static bool nst_run_granted(const mgn_env* e) {
+  const mgn_config& c = e->cfg;
+  return c.nstep_pop == MGN_NSTEP_POP_RUNNING && c.nstep > 1 && e->D == 1 &&
+         (c.shaper == MGN_SHAPER_DSR || c.shaper == MGN_SHAPER_DDR || c.shaper == MGN_SHAPER_PPC ||
+          c.shaper == MGN_SHAPER_NONE) &&
+         c.discount > 0. && std::pow(c.discount, (double)c.nstep) >= 1e-3;
+}
+
 mgn::KParams kparams(const mgn_env* e) {
   mgn::KParams p;
   const mgn_config& c = e->cfg;
@@ -297,12 +308,7 @@ mgn::KParams kparams(const mgn_env* e) {
   // MGN_NSTEP_POP_RUNNING: the shapers with a running-sum pop, scalar
   // rewards, and a discount whose slides stay well conditioned (the sums'
   // rounding grows by 1/gamma per pop between the re-sums every n pops)
-  p.nst_run = (c.nstep_pop == MGN_NSTEP_POP_RUNNING && c.nstep > 1 && e->D == 1 &&
-               (c.shaper == MGN_SHAPER_DSR || c.shaper == MGN_SHAPER_DDR || c.shaper == MGN_SHAPER_PPC ||
-                c.shaper == MGN_SHAPER_NONE) &&
-               c.discount > 0. && std::pow(c.discount, (double)c.nstep) >= 1e-3)
-                  ? 1
-                  : 0;
+  p.nst_run = nst_run_granted(e) ? 1 : 0;
   p.nst_rg = p.nst_run ? 1.0 / c.discount : 0.;
   p.rcur = e->v.replay_cursor;
   p.aux = e->v.aux;
@@ -406,7 +412,10 @@ void choose_sched(mgn_env* e) {
     // single-role kernel's one lane per env measured faster (R1 at 65536:
     // 1098 vs 1507 us per 64-step launch, profiles/r05c_bench_R1_64k{_single,}.json;
     // at 8192 envs the three-role kernel 337 vs 809, r05c_bench_R1_8k{,_single}.json)
-    const bool one_win_big = e->apad == 1 && e->W > 0 && e->N > 16384;
+    // -- with the exact n-step pop.  With the running-sum pop (which only the
+    // three-role kernel has) it stays faster at every batch: R1 at 65536 695
+    // vs 1141 us, at 32768 398 vs 896 (profiles/r06p_*.json)
+    const bool one_win_big = e->apad == 1 && e->W > 0 && e->N > 16384 && !nst_run_granted(e);
     e->trio = trio_eligible(e) && e->m == 1 && !one_win_big &&
               (e->apad <= 8 ||
                (e->apad <= 16 && ((e->W == 0 && e->cfg.nstep == 1) || e->replay ||

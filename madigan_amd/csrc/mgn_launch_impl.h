@@ -258,23 +258,23 @@ void launch_trio_one_impl(const StepArgs& a) {
 // (built with machine LICM), the one-step launches in mgn_launch_a8k1.hip
 // (without: with it they spilled 6 VGPRs and measured 7.3 against 6.9 us,
 // profiles/r05e_licm1)
-template <int S, bool K1_>
+template <int S, bool K1_, int TWv = TRIO_W>
 void launch_trio_agent_k(const StepArgs& a) {
-  const int grid = (a.p.N + TRIO_W / S - 1) / (TRIO_W / S);
+  const int grid = (a.p.N + TWv / S - 1) / (TWv / S);
   auto go = [&](auto kern) {
-    launch_timed(a.ev0, a.ev1, kern, dim3(grid), dim3(TRIO_BLOCK), 0, a.stream, a.p.L, a.p.mep, a.p.Bm, a.p.P,
+    launch_timed(a.ev0, a.ev1, kern, dim3(grid), dim3(3 * TWv), 0, a.stream, a.p.L, a.p.mep, a.p.Bm, a.p.P,
                  a.p.cash, a.act, a.p, a.out, a.in_kind, a.units, a.aidx, a.K);
   };
   auto pick = [&](auto omc) {
     constexpr uint32_t OM = decltype(omc)::value;
     constexpr bool K1 = K1_ && S <= 8;
     if (a.gkind == MGN_SRC_TRENDOU) {
-      if (a.p.reqm_one) go(k_step_trio<S, true, true, OM, false, TRIO_W, false, MGN_SRC_TRENDOU, false, 1, false, K1>);
-      else go(k_step_trio<S, false, true, OM, false, TRIO_W, false, MGN_SRC_TRENDOU, false, 1, false, K1>);
+      if (a.p.reqm_one) go(k_step_trio<S, true, true, OM, false, TWv, 0, MGN_SRC_TRENDOU, false, 1, false, K1>);
+      else go(k_step_trio<S, false, true, OM, false, TWv, 0, MGN_SRC_TRENDOU, false, 1, false, K1>);
     } else if (a.p.reqm_one) {
-      go(k_step_trio<S, true, true, OM, false, TRIO_W, false, -1, false, 1, false, K1>);
+      go(k_step_trio<S, true, true, OM, false, TWv, 0, -1, false, 1, false, K1>);
     } else {
-      go(k_step_trio<S, false, true, OM, false, TRIO_W, false, -1, false, 1, false, K1>);
+      go(k_step_trio<S, false, true, OM, false, TWv, 0, -1, false, 1, false, K1>);
     }
   };
   if (traj_mask(a.out) == O_STD) pick(std::integral_constant<uint32_t, O_STD>{});

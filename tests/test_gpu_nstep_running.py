@@ -83,21 +83,24 @@ def bits_of(a):
     return np.ascontiguousarray(np.asarray(a, dtype=np.float64)).view(np.int64)
 
 
-def test_running_pop_reference_shape_vs_oracle(gpu):
+@pytest.mark.parametrize("N,K", [(2048, 64), (65536, 24)])
+def test_running_pop_reference_shape_vs_oracle(gpu, N, K):
     """The reference's experiment shape (R1: one OU asset, W = 64 window, n =
     20 DDR on the summed agent reward) on the ONE layout's running-sum
-    instantiation: every output, n-step row (1e-6) and window of two 64-step
-    launches with auto-resets against the oracle."""
+    instantiation -- which the automatic schedule keeps at every batch (the
+    exact pop's handles beyond 16384 envs take the single-role kernel):
+    every output, n-step row (1e-6) and window of two launches with
+    auto-resets against the oracle."""
     from madigan_amd import _lib as L
     kw = dict(REF_KW, reward_shaper="DDR", seed=0x6D6164 + 41, nstep_pop="running")
     kw.update(required_margin=0.05, unit_size=0.9)
-    g, orc = make_pair(ou_sources(1), 2048, **kw)
+    g, orc = make_pair(ou_sources(1), N, **kw)
     assert g.lib.mgn_get_schedule(g.h) == L.SCHED_TRIO
-    acts = g.generate_actions(128, seed=0x6D6164 + 42)
-    ends = _launch_vs_oracle(g, orc, acts[:64], "R1 running launch 0", RTOL, atol=ATOL)
-    ends += _launch_vs_oracle(g, orc, acts[64:], "R1 running launch 1", RTOL, atol=ATOL)
-    assert ends > 2048 // 20
-    state_check(g, orc, "R1 running")
+    acts = g.generate_actions(2 * K, seed=0x6D6164 + 42)
+    ends = _launch_vs_oracle(g, orc, acts[:K], f"R1 running N={N} launch 0", RTOL, atol=ATOL)
+    ends += _launch_vs_oracle(g, orc, acts[K:], f"R1 running N={N} launch 1", RTOL, atol=ATOL)
+    assert ends > N // 20
+    state_check(g, orc, f"R1 running N={N}")
 
 
 def test_running_pop_not_granted_pops_exactly(gpu):

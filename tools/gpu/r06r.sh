@@ -1,0 +1,11 @@
+PLAN=""
+for r in 1 2 3; do
+for v in base ddrearly; do
+  if [ $v = base ]; then E=""; else E="MADIGAN_LIB_PATH=tools/_var/$v/libmadigan_hip.so"; fi
+  PLAN="$PLAN
+${v}_drv_$r|$E|--steps 20 --warmup 5 --no-k-sweep --no-cpu-baseline --no-probe
+${v}_k1_$r|$E|--fuse 1 --steps 64 --warmup 16 --no-k-sweep --no-cpu-baseline --no-probe
+${v}_k1_65536_$r|$E|--fuse 1 --n-envs 65536 --steps 64 --warmup 16 --no-k-sweep --no-cpu-baseline --no-probe"
+done; done
+export TAG=r06r PLAN
+bash tools/ab_bench.sh

@@ -44,7 +44,8 @@ FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=
 # their own (mgn_launch_a{1t,2,4,8,16}nst.hip).
 _NO_LICM = ["-mllvm", "-disable-machine-licm"]
 UNIT_FLAGS = {f"mgn_launch_{u}.hip": _NO_LICM
-              for u in ("a1", "a1t", "a1tnst", "a2", "a2nst", "a4", "a4nst", "a8", "a8k1", "a8nst", "a16", "a16m2", "a16nst",
+              for u in ("a1", "a1t", "a1tnst", "a2", "a2nst", "a4", "a4nst", "a8", "a8k1", "a8k1w", "a8nst", "a16", "a16m2",
+                        "a16nst",
                         "a32", "a64")}
 
 

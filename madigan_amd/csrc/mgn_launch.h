@@ -62,6 +62,10 @@ void launch_trio_m2_a16(const StepArgs& a);
 // of their own: multi-step (mgn_launch_a8t.hip), one-step (mgn_launch_a8k1.hip)
 void launch_trio_agent_a8(const StepArgs& a);
 void launch_trio_agent_k1_a8(const StepArgs& a);
+void launch_trio_agent_k1w_a8(const StepArgs& a);
+// one-step launches at APAD 8 from this many envs on: the wide unit
+// (mgn_launch_a8k1w.hip, four waves per SIMD)
+constexpr int kTrioK1WideN = 65536;
 // the n-step three-role launches, in units of their own
 // (mgn_launch_a{2,4,8,16}nst.hip: built without machine LICM)
 void launch_trio_nst_a2(const StepArgs& a);

@@ -3,11 +3,7 @@
 // own unit, built without machine LICM (madigan_amd/build.py)
 #include "mgn_launch_impl.h"
 namespace mgn {
-#ifdef MGN_K1_TW64  // A/B build: one wave per role (192-thread workgroups, four per CU)
-void launch_trio_agent_k1_a8(const StepArgs& a) { launch_trio_agent_k<8, true, 64>(a); }
-#else
 void launch_trio_agent_k1_a8(const StepArgs& a) { launch_trio_agent_k<8, true>(a); }
-#endif
 }  // namespace mgn
 #ifdef MGN_ITERSTAMP
 // diagnostic build: this unit's copy of the iteration stamps (the one-step

@@ -283,7 +283,8 @@ void launch_trio_agent_k(const StepArgs& a) {
 template <int S>
 void launch_trio_agent(const StepArgs& a) {
   if constexpr (S == 8) {
-    if (a.K == 1) launch_trio_agent_k1_a8(a);  // mgn_launch_a8k1.hip
+    if (a.K == 1 && a.p.N >= kTrioK1WideN) launch_trio_agent_k1w_a8(a);  // mgn_launch_a8k1w.hip
+    else if (a.K == 1) launch_trio_agent_k1_a8(a);                       // mgn_launch_a8k1.hip
     else launch_trio_agent_a8(a);              // mgn_launch_a8t.hip
   } else {
     if (a.K == 1) launch_trio_agent_k<S, true>(a);

@@ -268,7 +268,10 @@ template <int S, bool RQ1, bool DISC, uint32_t OMC = 0, bool WIN = false, int TW
 // built with -amdgpu-kernarg-preload-count (madigan_amd/build.py) they arrive
 // in SGPRs with the wave, so the orders' loads issue without waiting for the
 // kernel-argument segment (a one-step launch is one dependent chain)
-#ifdef MGN_K1_LB5  // A/B build: the one-wave-per-role one-step launches at <= 128 VGPRs (five workgroups per CU)
+#ifdef MGN_TRIO_WPE4
+// (mgn_launch_a8k1w.hip defines it: the one-step launches of large batches,
+// one wave per role at four waves per SIMD -- 128 VGPRs, five 192-thread
+// workgroups per CU, each an independent serial chain)
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 3 * TW), amdgpu_waves_per_eu(4))) void k_step_trio(
 #else
 __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(
@@ -1258,12 +1261,6 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(
     asm volatile("" ::: "memory");
     if (!kAblF && live && (flags & TR_STEP) && !rsv) {
       const int k = krec;
-#ifdef MGN_DDR_EARLY  // A/B build
-      // n = 1 DDR: the shaper's reward-independent operands (A / 2, the two
-      // denominators and their refined reciprocals, rt_div's) formed ahead of
-      // the reward chain, unconditionally (no branch: they interleave with it)
-      const DdrPreR ddr_c = ddr_pre_r(g.shA, g.shB);
-#endif
       // NRUN: the sums re-formed from the ring every n pops (term kk on lane
       // kk mod S; the entries before this step's), then the step's first pop
       // less its new entry's term and that entry's weight and the oldest
@@ -1471,11 +1468,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(
         rin_s = (p.reward_mode == MGN_REWARD_AGENT_SUM) ? canon<M, S, ONE>(ar) : reward;
         if (p.shaper == MGN_SHAPER_DDR) {  // shape() for DDR (nstep_buffer.py:128-162)
           const double r = rin_s;
-#ifdef MGN_DDR_EARLY
-          shaped_s = clip1((0.0 + 1.0 * ddr_one_r(r, g.shA, g.shB, ddr_c)) / 1);
-#else
           shaped_s = clip1((0.0 + 1.0 * ddr_one_pre(r, g.shA, g.shB, ddr_pre(g.shA, g.shB))) / 1);
-#endif
           double m = r < 0. ? r : 0.;
           if (r != r) m = r;
           g.shA += p.eta * (r - g.shA);

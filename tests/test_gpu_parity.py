@@ -577,7 +577,8 @@ def test_trio_tail_resets_bit_identical(gpu, A, N, K, kw):
 @pytest.mark.parametrize("A,N,src,fields", [
     (8, 8192, "ou", "std"), (8, 8192, "mixed", "all"),  # GSLOT: the generator's candidate reset tick
     (4, 16384, "trendou", "std"), (2, 32768, "trendou", "all"),  # TAIL_EXACT at S = 4 / 2
-    (8, 8192, "trendou", "std")])  # TAIL_EXACT at S = 8 (the C3 agent loop's unit)
+    (8, 8192, "trendou", "std"),  # TAIL_EXACT at S = 8 (the C3 agent loop's unit)
+    (8, 65536, "trendou", "std"), (8, 65536, "ou", "all")])  # the wide one-step unit (N >= 65536)
 def test_trio_k1_tail_paths_bit_identical(gpu, A, N, src, fields):
     """One-step launches on launch_trio_agent_k (the 256-lane layout, the agent
     loop's output sets O_STD / O_ALL at compile time, K1): an episode that

@@ -15,12 +15,12 @@ T=${TAG:-ev}
 case "$PART" in
 A)
   TAG=$T SUITE=1 DRV=1 TRACE=1 \
-    EXTRA="fuse256|--steps 2048 --warmup 256 --fuse 256 --no-k-sweep;n20|--steps 512 --warmup 64 --fuse 64 --nstep 20 --no-k-sweep;a16|--assets 16 --steps 512 --warmup 64 --fuse 64 --no-k-sweep" \
+    EXTRA="fuse256|--steps 2048 --warmup 256 --fuse 256 --no-k-sweep;n20|--steps 20 --warmup 5 --fuse 20 --nstep 20 --no-k-sweep --no-cpu-baseline;n20r|--steps 20 --warmup 5 --fuse 20 --nstep 20 --nstep-pop running --no-k-sweep --no-cpu-baseline;k1_65536|--fuse 1 --n-envs 65536 --steps 64 --warmup 16 --no-k-sweep --no-cpu-baseline;a16|--assets 16 --steps 512 --warmup 64 --fuse 64 --no-k-sweep" \
     bash tools/gpu_pass.sh
   ;;
 B)
   TAG=$T TRACE=1 \
-    EXTRA="c2|--workload C2 --steps 256 --warmup 64;c4|--workload C4 --steps 256 --warmup 64;c5|--workload C5 --steps 256 --warmup 64;r1_8k|--workload R1 --n-envs 8192 --steps 256 --warmup 64;r1_8k_sortino|--workload R1 --n-envs 8192 --steps 256 --warmup 64 --shaper sortino_shaperB;r1_64k|--workload R1 --n-envs 65536 --steps 128 --warmup 64" \
+    EXTRA="c2|--workload C2 --steps 256 --warmup 64;c4|--workload C4 --steps 256 --warmup 64;c5|--workload C5 --steps 256 --warmup 64;r1_8k|--workload R1 --n-envs 8192 --steps 256 --warmup 64;r1_8k_sortino|--workload R1 --n-envs 8192 --steps 256 --warmup 64 --shaper sortino_shaperB;r1_64k|--workload R1 --n-envs 65536 --steps 128 --warmup 64;r1_64k_running|--workload R1 --n-envs 65536 --steps 128 --warmup 64 --nstep-pop running;r1_8k_running|--workload R1 --n-envs 8192 --steps 256 --warmup 64 --nstep-pop running" \
     bash tools/gpu_pass.sh
   ;;
 C)

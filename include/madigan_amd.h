@@ -52,9 +52,9 @@
 extern "C" {
 #endif
 
-#define MGN_ABI_VERSION 9
+#define MGN_ABI_VERSION 10
 #define MGN_MAX_ASSETS 64
-#define MGN_MAX_NSTEP 64
+#define MGN_MAX_NSTEP 256
 
 /* status codes; the Python layer maps them to the reference's exceptions */
 enum {
@@ -158,7 +158,8 @@ typedef struct {
   double unit_size;            /* unit_size_proportion_avM */
   int32_t nstep;               /* n-step return length (nstep_return), 1..MGN_MAX_NSTEP;
                                   NStepBuffer semantics, nstep_buffer.py:315-356 */
-  int32_t nstep_pop;           /* MGN_NSTEP_POP_*: how an n-step pop is evaluated (ABI 9) */
+  int32_t nstep_pop;           /* MGN_NSTEP_POP_*: how an n-step pop is evaluated (ABI 9;
+                                  ABI 10: MGN_MAX_NSTEP 64 -> 256) */
   double discount;             /* gamma of the n-step aggregation */
   int32_t n_feats;             /* F = State.price width: n_assets for the generators
                                   (0 = n_assets); the feature columns of a replay source */

@@ -12,10 +12,10 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmadigan_hip.so")
 MAX_ASSETS = 64
-ABI_VERSION = 9
+ABI_VERSION = 10
 SRC_PARAMS = 64
 AUX_WIDTH = 24
-MAX_NSTEP = 64
+MAX_NSTEP = 256
 
 # status codes -> the reference's exception types (DataTypes.h:36-46, pybind11)
 OK, ERR_CONFIG, ERR_INDEX, ERR_LENGTH, ERR_DEVICE, ERR_ARG = range(6)

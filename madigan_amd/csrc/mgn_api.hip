@@ -201,7 +201,7 @@ int validate(const mgn_config* c, const mgn_asset_source* s, std::string& msg) {
     return MGN_ERR_CONFIG;
   }
   if (c->nstep < 1 || c->nstep > MGN_MAX_NSTEP) {
-    msg = "nstep_return must be in [1, 64]";
+    msg = "nstep_return must be in [1, 256]";
     return MGN_ERR_CONFIG;
   }
   if (c->nstep_pop != MGN_NSTEP_POP_EXACT && c->nstep_pop != MGN_NSTEP_POP_RUNNING) {

@@ -29,7 +29,7 @@ extern "C" {
 #endif
 
 #define ORC_MAX_ASSETS 64
-#define ORC_MAX_NSTEP 64
+#define ORC_MAX_NSTEP 256
 
 /* RiskInfo enum order: madigan/environments/cpp/DataTypes.h:70-75 */
 enum { ORC_GREEN = 0, ORC_INSUFF_MARGIN = 1, ORC_MARGIN_CALL = 2, ORC_BLOWN_OUT = 3 };

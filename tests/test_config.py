@@ -125,7 +125,7 @@ def test_naive_shaper_config():
 
 def test_build_caps_raise_runtime_error():
     """This build's fixed caps (include/madigan_amd.h MGN_MAX_ASSETS = 64,
-    MGN_MAX_NSTEP = 64; the reference's Eigen vectors and NStepBuffer are
+    MGN_MAX_NSTEP = 256; the reference's Eigen vectors and NStepBuffer are
     unbounded, DataTypes.h:28-29, nstep_buffer.py:315-330) are refused as the
     reference refuses an unsupported config: ConfigError, a RuntimeError
     (DataTypes.h:36-46), before any device call."""

@@ -403,6 +403,29 @@ def test_nstep64_two_assets_auto_schedule(gpu):
     np.testing.assert_allclose(host["shaped"], ref["shaped"], rtol=1e-10, atol=1e-14, err_msg="shaped")
 
 
+@pytest.mark.parametrize("n,shaper,A,extra", [(256, "DDR", 2, {}), (150, "DSR", 4, dict(reward_mode="agent_per_asset")),
+                                              (200, "sortino_shaperB", 1, dict(sortino_exp=1.1, window=8))])
+def test_nstep_long_buffers_vs_oracle(gpu, n, shaper, A, extra):
+    """n up to MGN_MAX_NSTEP = 256 (round 6; the reference's NStepBuffer takes
+    any n, nstep_buffer.py:327): whichever kernel the automatic schedule
+    picks for rings that size (the three-role kernel's LDS rings do not fit;
+    the others keep them in global memory) matches the oracle over launches
+    longer than the buffer, with done flushes of up to n entries."""
+    N, K = 2048, 2 * n + 16
+    kw = dict(required_margin=0.02, maintenance_margin=0.25, transaction_cost_rel=0.02,
+              unit_size=0.9, auto_reset=1, init_cash=1e5, reward_shaper=shaper,
+              adaptation_rate=0.01, nstep_return=n, discount=0.995, **extra)
+    g, orc = make_pair(trendou_sources(A, [0.2, 2, 6, 0.05, 0.2, 5.0, 0.15, 0.3, 0.2, 0.99]), N, **kw)
+    acts = g.generate_actions(K, seed=9)
+    host = {k: v.cpu().numpy() for k, v in g.rollout(acts).items()}
+    ref = orc.rollout(acts.cpu().numpy(), threads=8)
+    assert ref["done"].sum() > 0 and ref["n_shaped"].max() > 1
+    out_check({**host, "shaped": ref["shaped"]}, ref, f"nstep{n}", A if extra.get("reward_mode") else 1)
+    assert np.array_equal(host["n_shaped"], ref["n_shaped"]), "n_shaped"
+    np.testing.assert_allclose(host["shaped"], ref["shaped"], rtol=1e-10, atol=1e-14, err_msg="shaped")
+    state_check(g, orc, f"nstep{n}")
+
+
 @pytest.mark.parametrize("A,kw", [
     (8, dict(reward_shaper="DDR")),
     (16, dict(reward_shaper="DDR")),

@@ -352,6 +352,24 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+def gather_stats(D, env, n_total):
+    """The episode-statistics all-gather after the timed region: the C ABI's
+    mgn_stats_allgather on RCCL where torch's nccl group exposes its
+    communicator, else torch's all-gather (the path is recorded in the line);
+    an all-gather that fails does not lose the measured line -- it is
+    recorded instead, with this rank's own rows."""
+    try:
+        return D.allgather_env_stats(env, n_total=n_total), D.last_allgather_path
+    except D.CollectiveUnavailable as e:
+        try:
+            g = D.allgather_env_stats(env, n_total=n_total, allow_torch_fallback=True)
+            return g, f"{D.last_allgather_path} (no RCCL communicator: {e})"
+        except Exception as e2:  # noqa: BLE001
+            return env.episode_stats, f"failed: {type(e2).__name__}: {e2}"
+    except Exception as e:  # noqa: BLE001
+        return env.episode_stats, f"failed: {type(e).__name__}: {e}"
+
+
 def spawn_ranks(n: int, argv, backend: str) -> int:
     """`bench.py --gpus N` without a launcher: start N child ranks of this
     script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR 127.0.0.1 /
@@ -582,8 +600,7 @@ def main():
     # in a training loop, not per step: after the timed steps, timed on its own
     from madigan_amd import distributed as D
     ta = time.perf_counter()
-    gathered = D.allgather_env_stats(env, n_total=world * N)
-    allgather_path = D.last_allgather_path
+    gathered, allgather_path = gather_stats(D, env, world * N)
     torch.cuda.synchronize()
     # reported only when a collective ran ("local": one rank, no exchange)
     allgather_us = (time.perf_counter() - ta) * 1e6 if allgather_path != "local" else None
@@ -947,8 +964,7 @@ def windowed(args, world, rank, dev):
     elapsed = time.perf_counter() - t0
     # the episode-statistics all-gather (log intervals, not per step): after the timed steps
     from madigan_amd import distributed as D
-    gathered = D.allgather_env_stats(env, n_total=world * N)
-    allgather_path = D.last_allgather_path
+    gathered, allgather_path = gather_stats(D, env, world * N)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         if args.dist_backend == "gloo":

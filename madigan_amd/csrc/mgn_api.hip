@@ -158,7 +158,7 @@ Offsets plan(const mgn_config* c) {
   o.nring = l.add(n > 1 ? N * n * D * 8 : 0);
   o.nlen = l.add(N * 4);
   o.nhead = l.add(N * 4);
-  o.disc = l.add(n * 8);
+  o.disc = l.add(2 * n * 8);  // gamma^i, then (sortino_shaperB's running pop) (gamma^i)^(1/exp)
   o.src = l.add(A * sizeof(mgn_asset_source));
   o.target = l.add((A + 1) * 8);
   o.rcur = l.add(N * 8);
@@ -273,10 +273,13 @@ int validate(const mgn_config* c, const mgn_asset_source* s, std::string& msg) {
 // rounding grows by 1/gamma per pop between the re-sums every n pops)
 static bool nst_run_granted(const mgn_env* e) {
   const mgn_config& c = e->cfg;
-  return c.nstep_pop == MGN_NSTEP_POP_RUNNING && c.nstep > 1 && e->D == 1 &&
-         (c.shaper == MGN_SHAPER_DSR || c.shaper == MGN_SHAPER_DDR || c.shaper == MGN_SHAPER_PPC ||
-          c.shaper == MGN_SHAPER_NONE) &&
-         c.discount > 0. && std::pow(c.discount, (double)c.nstep) >= 1e-3;
+  if (!(c.nstep_pop == MGN_NSTEP_POP_RUNNING && c.nstep > 1 && e->D == 1 && c.discount > 0. &&
+        std::pow(c.discount, (double)c.nstep) >= 1e-3))
+    return false;
+  if (c.shaper == MGN_SHAPER_SORTINO_B)  // (its second sum slides by gamma^(-1/exp))
+    return c.sortino_exp > 0. && std::pow(c.discount, (double)c.nstep / c.sortino_exp) >= 1e-3;
+  return c.shaper == MGN_SHAPER_DSR || c.shaper == MGN_SHAPER_DDR || c.shaper == MGN_SHAPER_PPC ||
+         c.shaper == MGN_SHAPER_NONE;
 }
 
 mgn::KParams kparams(const mgn_env* e) {
@@ -310,6 +313,8 @@ mgn::KParams kparams(const mgn_env* e) {
   // rounding grows by 1/gamma per pop between the re-sums every n pops)
   p.nst_run = nst_run_granted(e) ? 1 : 0;
   p.nst_rg = p.nst_run ? 1.0 / c.discount : 0.;
+  p.nst_rg2 = (p.nst_run && c.shaper == MGN_SHAPER_SORTINO_B) ? 1.0 / std::pow(c.discount, 1.0 / c.sortino_exp) : 0.;
+  p.disc2 = e->disc_dev + c.nstep;
   p.rcur = e->v.replay_cursor;
   p.aux = e->v.aux;
   const auto& hb = e->hb[e->hcur];
@@ -618,8 +623,12 @@ int mgn_create(const mgn_config* cfg, const mgn_asset_source* sources, void* str
   e->target_dev = (double*)(b + o.target);
   e->disc_dev = (double*)(b + o.disc);
   // discounts gamma^i = math.pow(gamma, i) (nstep_buffer.py:328), host libm pow
-  double disc[MGN_MAX_NSTEP];
+  double disc[2 * MGN_MAX_NSTEP];
   for (int i = 0; i < cfg->nstep; ++i) disc[i] = std::pow(cfg->discount, (double)i);
+  // sortino_shaperB's running pop: the discounts' 1/exp-th roots ((x d)^(1/e)
+  // of a negative discounted entry = d^(1/e) x^(1/e))
+  for (int i = 0; i < cfg->nstep; ++i)
+    disc[cfg->nstep + i] = cfg->sortino_exp > 0. ? std::pow(disc[i], 1.0 / cfg->sortino_exp) : 0.;
 
   int rc = check_hip(e, hipMemsetAsync(e->arena, 0, o.total, e->stream), "hipMemsetAsync");
   if (rc == MGN_OK)
@@ -629,7 +638,7 @@ int mgn_create(const mgn_config* cfg, const mgn_asset_source* sources, void* str
     rc = check_hip(e, hipMemcpyAsync(e->target_dev, cfg->desired_portfolio, 8 * (e->A + 1),
                                      hipMemcpyHostToDevice, e->stream), "hipMemcpyAsync(target)");
   if (rc == MGN_OK)
-    rc = check_hip(e, hipMemcpyAsync(e->disc_dev, disc, 8 * cfg->nstep, hipMemcpyHostToDevice,
+    rc = check_hip(e, hipMemcpyAsync(e->disc_dev, disc, 2 * 8 * cfg->nstep, hipMemcpyHostToDevice,
                                      e->stream), "hipMemcpyAsync(discounts)");
   // the constructor's first getData; a replay handle runs it at mgn_attach_replay
   if (rc == MGN_OK && !e->replay) {

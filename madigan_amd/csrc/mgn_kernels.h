@@ -65,6 +65,8 @@ struct KParams {
   int nstep;
   int nst_run;    // MGN_NSTEP_POP_RUNNING granted (mgn_api.hip kparams): the three-role running-sum pop
   double nst_rg;  // 1 / gamma (nst_run)
+  double nst_rg2;        // sortino_shaperB: 1 / gamma^(1/exp)
+  const double *disc2;   // sortino_shaperB: (gamma^k)^(1/exp) (n), after disc in the arena
   double *nring;
   int32_t *nlen, *nhead;
   const double *disc;
@@ -1308,13 +1310,18 @@ __device__ __forceinline__ NstPre nrun_pre(int shaper, const NstRun& s, int len,
     q.cp = dneg * r;
     q.cn = dpos * r;
     q.base = q.cp * (s.pr - q.hA * s.p1) + q.cn * (B * (s.nr - q.hA * s.n1) - q.hA * s.nrr);
+  } else if (shaper == MGN_SHAPER_SORTINO_B) {
+    q.base = s.p1 - s.n1;
   } else {
     q.base = s.pr + s.nr;
   }
   return q;
 }
-// the pop with v appended at weight w; DSR / DDR: clip(sum / len) as
-// __main_func__ (nstep_buffer.py:78, :144)
+// the pop with v appended at weight w (sortino_shaperB: its root at weight
+// w2); DSR / DDR: clip(sum / len) as __main_func__ (nstep_buffer.py:78, :144)
+__device__ __forceinline__ double nrun_fin_sb(const NstPre& q, double v, double root, double w, double w2) {
+  return clip1(q.base + ((v > 0.) ? w * v : ((v < 0.) ? -(w2 * root) : 0.)));
+}
 __device__ __forceinline__ double nrun_fin(int shaper, const NstPre& q, double v, double w) {
   if (shaper == MGN_SHAPER_DSR) return clip1(q.base + q.cp * (w * (q.B * (v - q.A) - q.hA * (v * v - q.B))));
   if (shaper == MGN_SHAPER_DDR) {
@@ -1327,7 +1334,8 @@ __device__ __forceinline__ double nrun_fin(int shaper, const NstPre& q, double v
 // the pop of a buffer of len entries from its sums alone
 __device__ __forceinline__ double nrun_pop(int shaper, const NstRun& s, int len, double A, double B) {
   const NstPre q = nrun_pre(shaper, s, len, A, B);
-  return (shaper == MGN_SHAPER_DSR || shaper == MGN_SHAPER_DDR) ? clip1(q.base) : q.base;
+  return (shaper == MGN_SHAPER_DSR || shaper == MGN_SHAPER_DDR || shaper == MGN_SHAPER_SORTINO_B) ? clip1(q.base)
+                                                                                                 : q.base;
 }
 
 // naive shapers (nstep_buffer.py:207-312), benchmark 0.  x**e and x**(1/e) as
@@ -1346,6 +1354,26 @@ __device__ __forceinline__ double min_0(double x) { return (x < 0. || x != x) ? 
 __device__ __forceinline__ double sortinoB_term(double r, double disc_k, double ex) {
   const double v = max_m1((r - 0.) * disc_k);
   return (v < 0.) ? -root_e(-v, ex) : v;
+}
+
+// sortino_shaperB's running-sum pop (MGN_NSTEP_POP_RUNNING): with
+// x_k = gamma^k r_k, the pop is clip(sum_k (x_k >= 0 ? x_k : -(-x_k)^(1/e)))
+// and -(-x_k)^(1/e) = -(gamma^k)^(1/e) (-r_k)^(1/e), so two discounted sums
+// carry it -- NstRun.p1 = sum_{r>0} gamma^k r_k, .n1 = sum_{r<0}
+// (gamma^k)^(1/e) (-r_k)^(1/e) (the entry's root formed once, at its
+// append) -- while no entry can reach the per-term clip at -1 (x_k < -1 needs
+// r_k < -1: .prr counts those entries, and a pop with any of them is the exact
+// one).  A pop removes the oldest entry and divides p1 by gamma, n1 by
+// gamma^(1/e).
+__device__ __forceinline__ void nrun_add_sb(NstRun& s, double r, double root, double w, double w2) {
+  s.p1 += (r > 0.) ? w * r : 0.;
+  s.n1 += (r < 0.) ? w2 * root : 0.;
+  s.prr += (r < -1. || r != r) ? 1. : 0.;
+}
+__device__ __forceinline__ void nrun_slide_sb(NstRun& s, double r0, double root0, double rg, double rg2) {
+  s.p1 = (s.p1 - ((r0 > 0.) ? r0 : 0.)) * rg;
+  s.n1 = (s.n1 - ((r0 < 0.) ? root0 : 0.)) * rg2;
+  s.prr -= (r0 < -1. || r0 != r0) ? 1. : 0.;
 }
 
 // the len(nstep_buffer) == 1 heuristics (:212-216, :244-249, :286-291)

@@ -193,8 +193,12 @@ void launch_trio_nst_k(const StepArgs& a) {
 // pop (NS = 1) otherwise
 template <int S>
 void launch_trio_nst(const StepArgs& a) {
-  if (a.p.nst_run && a.in_kind == IN_DISCRETE) launch_trio_nst_k<S, 2>(a);
-  else launch_trio_nst_k<S, 1>(a);
+  // (sortino_shaperB's running form only at one wave per role: SBR)
+  const bool wave64 = a.p.W > 0 || (long long)a.p.N * S < 256LL * TRIO_W;
+  if (a.p.nst_run && a.in_kind == IN_DISCRETE && (a.p.shaper != MGN_SHAPER_SORTINO_B || wave64))
+    launch_trio_nst_k<S, 2>(a);
+  else
+    launch_trio_nst_k<S, 1>(a);
 }
 
 // the one-asset envs (ONE, S = 2: the second lane of every env a pad; its
@@ -234,7 +238,7 @@ void launch_trio_one_impl(const StepArgs& a) {
   // NS_: n-step handles, with the running-sum pop where the host granted it
   using N = std::integral_constant<int, NS_ ? 1 : 0>;
   using NR = std::integral_constant<int, NS_ ? 2 : 0>;
-  if (NS_ && a.p.nst_run) {
+  if (NS_ && a.p.nst_run && (a.p.shaper != MGN_SHAPER_SORTINO_B || small)) {
     if (a.p.reqm_one) {
       win ? pick(T{}, T{}, NR{}) : pick(T{}, F{}, NR{});
     } else {

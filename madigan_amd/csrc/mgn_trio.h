@@ -164,7 +164,7 @@ template <int S, int TW, bool NST, int M = 1>
 constexpr size_t trio_static_lds() {
   return sizeof(TrioShared<S, TW, M>) + (size_t)(TW / S) * sizeof(EnvRecs<S * M>) +
          S * M * sizeof(mgn_asset_source) + (MGN_MAX_ASSETS + 1) * sizeof(double) +
-         (NST ? MGN_MAX_NSTEP : 1) * sizeof(double) + 256;
+         (NST ? 2 * MGN_MAX_NSTEP : 1) * sizeof(double) + 256;  // s_disc (+ s_disc2 of the running pop)
 }
 
 // The replay tape's tick for the lane's M slots (duo_replay_tick's, per slot:
@@ -300,6 +300,10 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(
   // NST == 2: the running-sum pop (MGN_NSTEP_POP_RUNNING, nrun_pop; the host
   // routes only DSR / DDR / PPC / none here); NST == 1: the exact pop
   constexpr bool NRUN = NST == 2;
+  // sortino_shaperB's running pop: the one-wave-per-role layouts only (the
+  // windowed and small-batch handles, R1 among them); at 256 lanes its code
+  // would spill the running kernels (the launcher runs the exact pop there)
+  constexpr bool SBR = NRUN && TW == 64;
   static_assert(M == 1 || (M == 2 && !NST), "two slots per lane: one-step rewards");
   static_assert(!ONE || (S == 2 && M == 1), "a one-asset env on two lanes per role");
   constexpr int APAD = S * M;
@@ -311,6 +315,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(
   __shared__ mgn_asset_source s_src[APAD];
   __shared__ double s_tgt[MGN_MAX_ASSETS + 1];
   __shared__ double s_disc[NST ? MGN_MAX_NSTEP : 1];                     // NST: gamma^k
+  __shared__ double s_disc2[SBR ? MGN_MAX_NSTEP : 1];                     // SBR: (gamma^k)^(1/exp)
   extern __shared__ __attribute__((aligned(16))) double s_nst[];          // NST: (EPB, NPADS nst_pad(n, S))
   const int role = threadIdx.x / TRIO_W;  // 0 generator, 1 ledger, 2 finish
   const int l = threadIdx.x % TRIO_W;
@@ -442,7 +447,14 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(
         if constexpr (NRUN) {  // the sums of the entries the lane copied (position k from the oldest)
           int k = i - nhead;
           k += (k < 0) ? p.nstep : 0;
-          if (k < nlen) nrun_add(nrs, x, p.disc[k]);
+          if (SBR && p.shaper == MGN_SHAPER_SORTINO_B) {
+            // (each entry's root kept beside the ring, in the summands' slots)
+            const double rt = (x < 0.) ? root_e(-x, p.sexp) : 0.;
+            ring[nst_pad(p.nstep, S) + i] = rt;
+            if (k < nlen) nrun_add_sb(nrs, x, rt, p.disc[k], p.disc2[k]);
+          } else if (k < nlen) {
+            nrun_add(nrs, x, p.disc[k]);
+          }
         }
       }
       if constexpr (NRUN) nrun_allsum<S>(nrs);
@@ -459,7 +471,10 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(
     if (p.target)
       for (int i = threadIdx.x; i <= p.A; i += TRIO_BLOCK) s_tgt[i] = p.target[i];
     if (NST)
-      for (int i = threadIdx.x; i < p.nstep; i += TRIO_BLOCK) s_disc[i] = p.disc[i];
+      for (int i = threadIdx.x; i < p.nstep; i += TRIO_BLOCK) {
+        s_disc[i] = p.disc[i];
+        if constexpr (SBR) s_disc2[i] = p.disc2[i];
+      }
     p.src = s_src;
     if (p.target) p.target = s_tgt;
   }
@@ -1266,7 +1281,7 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(
       // less its new entry's term and that entry's weight and the oldest
       // entry, formed ahead of the reward chain (nrun_pre)
       NstPre npre{};
-      double nst_w = 0., nst_r0 = 0.;
+      double nst_w = 0., nst_r0 = 0., nst_w2 = 0., nst_rt0 = 0.;
       if constexpr (NRUN) {
         const int n = p.nstep;
         const double* ring = s_nst + (size_t)el * NPADS * nst_pad(n, S);
@@ -1275,13 +1290,20 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(
           for (int kk = ls; kk < nlen; kk += S) {
             int idx = nhead + kk;
             idx -= (idx >= n) ? n : 0;
-            nrun_add(nrs, ring[idx], s_disc[kk]);
+            if (SBR && p.shaper == MGN_SHAPER_SORTINO_B)
+              nrun_add_sb(nrs, ring[idx], ring[nst_pad(n, S) + idx], s_disc[kk], s_disc2[kk]);
+            else
+              nrun_add(nrs, ring[idx], s_disc[kk]);
           }
           nrun_allsum<S>(nrs);
           nsl = 0;
         }
         nst_w = s_disc[nlen];
         nst_r0 = ring[nhead];
+        if (SBR && p.shaper == MGN_SHAPER_SORTINO_B) {
+          nst_w2 = s_disc2[nlen];
+          nst_rt0 = ring[nst_pad(n, S) + nhead];
+        }
         npre = nrun_pre(p.shaper, nrs, nlen + 1, g.shA, g.shB);
       }
       Lane<M> f = s;
@@ -1377,11 +1399,31 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(
           // the running-sum pop (nrun_pre / nrun_fin): every lane of the env
           // keeps the sums, appends the entry and pops -- the same values on
           // every lane, the first stores
+          // (sortino_shaperB: the entry's root, kept beside the ring)
+          const bool SB = SBR && p.shaper == MGN_SHAPER_SORTINO_B;
+          double* rts = ring + nst_pad(n, S);
+          const double vrt = (SB && v < 0.) ? root_e(-v, p.sexp) : 0.;
           ring[tail] = v;  // (every lane writes it: each lane's own reads below see it)
-          nrun_add(nrs, v, nst_w);
+          if (SB) {
+            rts[tail] = vrt;
+            nrun_add_sb(nrs, v, vrt, nst_w, nst_w2);
+          } else {
+            nrun_add(nrs, v, nst_w);
+          }
+          // sortino_shaperB with an entry below -1 in the buffer (the
+          // per-term clip can bind): the exact pop, naive_n's order
+          // (sortinoB_term over the entries in order -- naive_n's sum; one entry:
+          // naive1's, the same operations with gamma^0 = 1 -- inline: a call
+          // would spill the caller's registers)
+          const auto sb_exact = [&]() {
+            double acc = 0.0;
+            for (int kk = 0, idx = head; kk < len; ++kk, idx = (idx + 1 == n) ? 0 : idx + 1)
+              acc += sortinoB_term(ring[idx], s_disc[kk], p.sexp);
+            return clip1(acc);
+          };
           // one pop: the shaper state steps (update_parameters, exact), the
           // oldest entry leaves the sums
-          const auto pop_done = [&](int pj, double res, double r0) {
+          const auto pop_done = [&](int pj, double res, double r0, double rt0) {
             if (p.shaper == MGN_SHAPER_DSR || p.shaper == MGN_SHAPER_DDR) {
               g.shA += p.eta * (r0 - g.shA);
               if (p.shaper == MGN_SHAPER_DSR) {
@@ -1399,15 +1441,20 @@ __global__ __launch_bounds__(3 * TW, 1) void k_step_trio(
               nrun_zero(nrs);
               nsl = 0;
             } else {
-              nrun_slide(nrs, r0, p.nst_rg);
+              if (SB) nrun_slide_sb(nrs, r0, rt0, p.nst_rg, p.nst_rg2);
+              else nrun_slide(nrs, r0, p.nst_rg);
               nsl += (r0 - r0 == 0.) ? 1 : n;  // a non-finite entry left: re-form at the next step
             }
           };
           // (the first pop taken out of the loop measured 2.73-2.79 against
           // 2.60 us/step, profiles/r06h_ab.txt)
           for (int pj = 0; pj < pops; ++pj) {
-            if (pj == 0) pop_done(0, nrun_fin(p.shaper, npre, v, nst_w), nlen == 0 ? v : nst_r0);
-            else pop_done(pj, nrun_pop(p.shaper, nrs, len, g.shA, g.shB), ring[head]);  // a done flush's further pops
+            double res;
+            if (SB && nrs.prr > 0.) res = sb_exact();
+            else if (pj == 0) res = SB ? nrun_fin_sb(npre, v, vrt, nst_w, nst_w2) : nrun_fin(p.shaper, npre, v, nst_w);
+            else res = nrun_pop(p.shaper, nrs, len, g.shA, g.shB);  // a done flush's further pops
+            if (pj == 0) pop_done(0, res, nlen == 0 ? v : nst_r0, nlen == 0 ? vrt : nst_rt0);
+            else pop_done(pj, res, ring[head], rts[head]);
           }
         } else {
         if (ls == 0) ring[tail] = v;

@@ -44,6 +44,9 @@ def _check_launch(host, ref, tag):
     (4, 512, "ou", "DSR", 5, 0.9, [256] * 40),
     (2, 1024, "trendou", "PPC", 20, 0.97, [64] * 20),
     (8, 512, "trendou", None, 16, 0.99, [256] * 8),
+    # sortino_shaperB's running form (one wave per role): exp 1.1 and 3
+    (4, 512, "ou", "sortino_shaperB", 20, 0.99, [256] * 8),
+    (2, 1024, "trendou", "sortino_shaperB3", 12, 0.95, [64] * 20),
 ])
 def test_running_pop_vs_oracle(gpu, A, N, src, shaper, n, gamma, launches):
     from madigan_amd import _lib as L
@@ -52,6 +55,8 @@ def test_running_pop_vs_oracle(gpu, A, N, src, shaper, n, gamma, launches):
               discount=gamma, seed=0x6E7275 + A)
     if shaper == "PPC":
         kw.update(cosine_temp=0.05, desired_portfolio=[0.5] + [0.5 / A] * A)
+    if shaper and shaper.startswith("sortino_shaperB"):
+        kw.update(reward_shaper="sortino_shaperB", sortino_exp=3.0 if shaper.endswith("3") else 1.1)
     sources = trendou_sources(A, TOU) if src == "trendou" else ou_sources(A)
     g, orc = make_pair(sources, N, nstep_pop="running", **kw)
     L.check(g.lib.mgn_set_schedule(g.h, L.SCHED_TRIO), g.h)
@@ -71,7 +76,7 @@ def test_running_pop_vs_oracle(gpu, A, N, src, shaper, n, gamma, launches):
         state_check(g, orc, f"{shaper} launch {i}")
     assert N * k0 >= 1e6  # (the OU DSR case: 10240 steps)
     assert ends > 0 and int(ref["n_shaped"].max()) > 1, "done flushes"
-    if shaper in ("DSR", "DDR"):
+    if shaper in ("DSR", "DDR") or (shaper or "").startswith("sortino"):
         assert sat > 0, "clip saturation"
     # the running pop sums differently: its values are not the exact pop's bits
     assert diff > 0, "the running-sum kernel ran"
@@ -83,8 +88,9 @@ def bits_of(a):
     return np.ascontiguousarray(np.asarray(a, dtype=np.float64)).view(np.int64)
 
 
-@pytest.mark.parametrize("N,K", [(2048, 64), (65536, 24)])
-def test_running_pop_reference_shape_vs_oracle(gpu, N, K):
+@pytest.mark.parametrize("N,K,shaper", [(2048, 64, "DDR"), (65536, 24, "DDR"), (2048, 64, "sortino_shaperB"),
+                                         (8192, 32, "sortino_shaperB")])
+def test_running_pop_reference_shape_vs_oracle(gpu, N, K, shaper):
     """The reference's experiment shape (R1: one OU asset, W = 64 window, n =
     20 DDR on the summed agent reward) on the ONE layout's running-sum
     instantiation -- which the automatic schedule keeps at every batch (the
@@ -92,22 +98,24 @@ def test_running_pop_reference_shape_vs_oracle(gpu, N, K):
     every output, n-step row (1e-6) and window of two launches with
     auto-resets against the oracle."""
     from madigan_amd import _lib as L
-    kw = dict(REF_KW, reward_shaper="DDR", seed=0x6D6164 + 41, nstep_pop="running")
+    sx = dict(sortino_exp=1.1) if shaper.startswith("sortino") else {}  # ou_sortinoB_exp_1.1_nstep20.yaml
+    kw = dict(REF_KW, reward_shaper=shaper, seed=0x6D6164 + 41, nstep_pop="running", **sx)
     kw.update(required_margin=0.05, unit_size=0.9)
     g, orc = make_pair(ou_sources(1), N, **kw)
     assert g.lib.mgn_get_schedule(g.h) == L.SCHED_TRIO
     acts = g.generate_actions(2 * K, seed=0x6D6164 + 42)
-    ends = _launch_vs_oracle(g, orc, acts[:K], f"R1 running N={N} launch 0", RTOL, atol=ATOL)
-    ends += _launch_vs_oracle(g, orc, acts[K:], f"R1 running N={N} launch 1", RTOL, atol=ATOL)
+    ends = _launch_vs_oracle(g, orc, acts[:K], f"R1 {shaper} running N={N} launch 0", RTOL, atol=ATOL)
+    ends += _launch_vs_oracle(g, orc, acts[K:], f"R1 {shaper} running N={N} launch 1", RTOL, atol=ATOL)
     assert ends > N // 20
-    state_check(g, orc, f"R1 running N={N}")
+    state_check(g, orc, f"R1 {shaper} running N={N}")
 
 
 def test_running_pop_not_granted_pops_exactly(gpu):
     """nstep_pop="running" is a permission: where the kernel has no running
-    form (sortino_shaperB) or the discount would amplify the slides' rounding
-    (gamma^n < 1e-3), the pops stay the exact ones -- bit for bit the handle
-    without the switch."""
+    form (sortino_shaperB at the 256-lane layout: it has one at one wave per
+    role only) or the discount would amplify the slides' rounding (gamma^n <
+    1e-3), the pops stay the exact ones -- bit for bit the handle without the
+    switch."""
     from madigan_amd import BatchedEnv
     for extra in (dict(reward_shaper="sortino_shaperB", sortino_exp=1.1, discount=0.99),
                   dict(reward_shaper="DDR", discount=0.5)):

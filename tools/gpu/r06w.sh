@@ -2,7 +2,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/r06w; mkdir -p $O
+O=gpurun_out/${TAG:-r06w}; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.txt 2>&1 || { echo PYTEST_FAIL; grep -E "FAILED|Error" $O/pytest_gpu.txt | head; tail -30 $O/pytest_gpu.txt; exit 1; }
 tail -1 $O/pytest_gpu.txt
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { echo SMOKE_FAIL; tail -20 $O/smoke.txt; exit 1; }

@@ -523,6 +523,9 @@ void launch_gather(const mgn::RingDesc& r, double* price, double* port, uint64_t
     const size_t per_env = (size_t)r.W * (C + 1) * 8;
     mgn::GatherLds g;
     g.epb = (int)std::min<size_t>(64, std::max<size_t>(1, kGatherLdsTarget / per_env));
+    // small batches (the agent loop's one window per step at a few thousand
+    // envs): no fewer than four workgroups per CU, so the chip fills
+    g.epb = std::max(1, std::min(g.epb, r.N / (4 * 256)));
     g.inv_f = 1.0f / (float)r.F;
     g.inv_p = 1.0f / (float)r.Pn;
     g.inv_w = 1.0f / (float)r.W;
